@@ -1,0 +1,262 @@
+"""ORACLE — test infrastructure only (see oracle/__init__.py).
+
+CPU fp32 restatement of the reference TransformerVAE training hot path, written from the
+reference's behaviour (file:line cited per function), functional over a parameter dict whose
+keys are the reference `state_dict` keys (oracle/params.py).
+
+Padding semantics of the reference's PaddedTensor (padded_tensor.py:54-69) are restated
+explicitly: the token mask `pad = ids == 0` ([B, L]) reaches an attention call iff the KEY
+sequence length equals L (the getter returns None on a length mismatch, :68-69).
+"""
+import math
+from typing import Dict, Optional
+
+import torch
+import torch.nn.functional as F
+
+__all__ = [
+    'rotary', 'attention', 'transformer_layer', 'perceiver', 'conditional_gaussian',
+    'sample_z', 'reconstruct', 'output_layer', 'robust_cross_entropy', 'marginal_kl',
+    'training_step', 'radam_step', 'clip_grad_norm', 'cosine_decay', 'kl_anneal',
+    'RAdamState',
+]
+
+
+def rotary(x: torch.Tensor, start: int = 0, max_pos: int = 10000) -> torch.Tensor:
+    """encode_position_rotary, attention.py:194-208. Interleaved pairs (2i, 2i+1) over the FULL
+    last dim, angles computed in x.dtype; (a, b) -> (a cos + (-b) sin, b cos + a sin)."""
+    half = x.shape[-1] // 2
+    freqs = torch.arange(half, dtype=x.dtype)
+    pos = torch.arange(start, start + x.shape[-2], dtype=x.dtype)
+    theta = max_pos ** (-freqs / half)
+    ang = pos[:, None] * theta
+    c, s = ang.cos(), ang.sin()
+    a, b = x[..., 0::2], x[..., 1::2]
+    out0 = a * c + (-b) * s
+    out1 = b * c + a * s
+    return torch.stack([out0, out1], dim=-1).flatten(-2)
+
+
+def _linear(p, name, x, bias=True):
+    return F.linear(x, p[name + '.weight'], p[name + '.bias'] if bias else None)
+
+
+def attention(p: Dict[str, torch.Tensor], pre: str, q_in, k_in, v_in, pad: Optional[torch.Tensor],
+              num_heads: int, causal: bool = False) -> torch.Tensor:
+    """Dense Attention.forward, attention.py:51-105 (sparse branch :78-81 out of scope)."""
+    B = k_in.shape[0]
+    lq = p.get(pre + 'learned_queries')
+    if lq is not None:                                   # :55-56
+        q = lq.expand(B, *lq.shape[1:])
+    else:                                                # :60-61
+        q = rotary(_linear(p, pre + 'q_linear', q_in))
+    k = rotary(_linear(p, pre + 'k_linear', k_in))       # :67, :70
+    v = _linear(p, pre + 'v_linear', v_in)
+    mask = pad if (pad is not None and pad.shape[-1] == k.shape[-2]) else None   # :75 + getter
+    d = q.shape[-1]
+    hd = d // num_heads
+
+    def split(t):                                        # :76 '... l (h d) -> ... h l d'
+        return t.reshape(t.shape[0], t.shape[1], num_heads, hd).transpose(1, 2)
+
+    q, k, v = split(q), split(k), split(v)
+    scores = q @ k.transpose(-1, -2) * k.shape[-1] ** -0.5          # :83
+    causal_mask = None
+    if causal:                                           # :85-87
+        ql = q.shape[-2]
+        causal_mask = torch.ones(ql, ql, dtype=torch.bool).triu(1)
+    if mask is not None:                                 # :93
+        mask = mask[..., None, None, :]
+    if causal_mask is not None:                          # :94-95
+        mask = mask | causal_mask if mask is not None else causal_mask
+    if mask is not None:                                 # :97-98
+        scores = scores - mask * 1e7
+    out = scores.softmax(dim=-1) @ v                     # :100
+    out = out.transpose(1, 2).reshape(out.shape[0], -1, d)            # :102
+    return _linear(p, pre + 'output_linear', out)        # :103
+
+
+def _ln(p, name, x):
+    return F.layer_norm(x, (x.shape[-1],), p[name + '.weight'], p[name + '.bias'], 1e-5)
+
+
+def transformer_layer(p, pre, x, pad, num_heads, causal=False, context=None,
+                      dropout_mask: Optional[torch.Tensor] = None, dropout_p: float = 0.1):
+    """TransformerLayer.forward, transformer_layer.py:44-61 (pre-LN). `dropout_mask`, if given,
+    is the keep-mask of nn.Dropout(0.1) at :58 (None = dropout disabled)."""
+    y = _ln(p, pre + 'attn_layer_norm', x)
+    y = attention(p, pre + 'attention.', y, y, y, pad, num_heads, causal)
+    x = x + y if x.shape == y.shape else y               # :49
+    if (pre + 'cross_attention.k_linear.weight') in p and context is not None:   # :51-54
+        ctx = _ln(p, pre + 'context_layer_norm', context)
+        y = _ln(p, pre + 'cross_attn_layer_norm', x)
+        y = attention(p, pre + 'cross_attention.', y, ctx, ctx, pad, num_heads)
+        x = x + y
+    y = _ln(p, pre + 'ffn_layer_norm', x)                # :56-57
+    y = F.linear(F.gelu(_linear(p, pre + 'ffn.0', y)), p[pre + 'ffn.2.weight'])
+    if dropout_mask is not None:                         # :58
+        y = y * dropout_mask / (1.0 - dropout_p)
+    return x + y
+
+
+def perceiver(p, x, pad, hp, dropout_masks=None):
+    """Perceiver.forward, perceiver.py:39-50: first (64 learned queries) -> middle (self + cross)
+    -> bottleneck (1 learned query). Heads = d_model // 64 (:13)."""
+    h = hp.enc_heads
+    dm = dropout_masks or {}
+    z = transformer_layer(p, 'encoder.first_layer.', x, pad, h, dropout_mask=dm.get('encoder.first_layer'))
+    for j in range(hp.enc_layers - 2):
+        name = f'encoder.middle_layers.{j}'
+        z = transformer_layer(p, name + '.', z, pad, h, context=x, dropout_mask=dm.get(name))
+    return transformer_layer(p, 'encoder.bottleneck.', z, pad, h, dropout_mask=dm.get('encoder.bottleneck'))
+
+
+def conditional_gaussian(p, h):
+    """ConditionalGaussian.forward(get_kl=True), conditional_gaussian.py:18-28."""
+    mu, logvar = _linear(p, 'q_of_z_given_x.linear', h).chunk(2, dim=-1)
+    var = logvar.exp()
+    scale = var.sqrt()
+    kl = 0.5 * (mu ** 2 + var - logvar - 1.0)
+    return mu, logvar, scale, kl
+
+
+def sample_z(p, h, num_tokens, eps):
+    """ContinuousVAE.sample_z, continuous_autoencoder.py:42-52 (rsample = loc + eps * scale)."""
+    mu, logvar, scale, kl = conditional_gaussian(p, h)
+    z = mu + eps * scale
+    raw_kl = kl.flatten(1).sum(dim=-1)
+    kl_mean = raw_kl.div(num_tokens).mean()
+    return z, kl_mean, raw_kl, mu, logvar, scale
+
+
+def output_layer(p, x):
+    """output_layer, transformer_language_model.py:55-63 (Linear, GELU, LayerNorm, tied Linear)."""
+    y = F.gelu(_linear(p, 'output_layer.0', x))
+    y = _ln(p, 'output_layer.2', y)
+    return F.linear(y, p['input_layer.0.weight'], p['output_layer.3.bias'])
+
+
+def reconstruct(p, x, z, pad, hp, dropout_masks=None):
+    """TransformerVAE.reconstruct, transformer_vae.py:85-93: position 0 of the residual stream is
+    replaced by z_projections[i](z) before EVERY decoder layer."""
+    dm = dropout_masks or {}
+    for i in range(hp.num_layers):
+        zh = _linear(p, f'z_projections.{i}', z)
+        x = torch.cat([zh, x[..., 1:, :]], dim=-2)
+        x = transformer_layer(p, f'decoder_layers.{i}.', x, pad, hp.num_heads, causal=True,
+                              dropout_mask=dm.get(f'decoder_layers.{i}'))
+    return output_layer(p, x)
+
+
+def robust_cross_entropy(logits, labels):
+    """language_model.py:161-170: one F.cross_entropy(ignore_index=0) when numel <= 2**30, else the
+    mean of per-sequence-chunk means (torch.chunk along the sequence dim)."""
+    chunks = -(-logits.numel() // 2 ** 30)
+    if chunks == 1:
+        return F.cross_entropy(logits.flatten(end_dim=1), labels.flatten(), ignore_index=0)
+    return torch.stack([
+        F.cross_entropy(lc.flatten(end_dim=1), yc.flatten(), ignore_index=0)
+        for lc, yc in zip(logits.chunk(chunks, dim=-2), labels.chunk(chunks, dim=-1))
+    ]).mean()
+
+
+def marginal_kl(mu, scale, eps_samples):
+    """math_utils.py:51-58 with the 10 rsample draws injected (eps_samples [10, *mu.shape])."""
+    samples = mu + eps_samples * scale
+    x = samples[:, :, None]
+    var = scale ** 2
+    log_prob = -((x - mu) ** 2) / (2 * var) - scale.log() - math.log(math.sqrt(2 * math.pi))
+    cross = log_prob.sum(dim=-1)
+    marginal = cross.logsumexp(dim=2) - math.log(samples.shape[1])
+    sample_prob = -0.5 * (samples.pow(2.0).sum(dim=-1).mean() + samples.shape[-1] * math.log(2 * math.pi))
+    return sample_prob - marginal.mean()
+
+
+def training_step(p, hp, ids, num_tokens, eps, kl_weight=None, eps_marginal=None,
+                  pad: Optional[torch.Tensor] = 'auto', dropout_masks=None):
+    """TransformerVAE.training_step, transformer_vae.py:42-66 (stage='train').
+
+    ids: int64 [B, L]; pad: [B, L] bool key-padding mask ('auto' = ids == 0, as PaddedTensor.from_raw
+    does at padded_tensor.py:13-17; None = plain tensor, no mask). Returns the loss and the values the
+    reference logs."""
+    if isinstance(pad, str):
+        pad = ids.eq(0)
+    kl_weight = hp.kl_weight if kl_weight is None else kl_weight
+    x = F.embedding(ids, p['input_layer.0.weight'])                       # :45
+    enc = perceiver(p, x, pad, hp, dropout_masks)                          # :46
+    z, kl, raw_kl, mu, logvar, scale = sample_z(p, enc, num_tokens, eps)   # :48
+    logits = reconstruct(p, x, z, pad, hp, dropout_masks)[..., :-1, :]     # :50
+    nll = robust_cross_entropy(logits, ids[..., 1:])                       # :51
+    loss = nll + kl_weight * kl                                            # :55
+    out = dict(loss=loss, nll=nll, kl=kl, raw_kl=raw_kl, train_kl=raw_kl.mean(),
+               mu=mu, logvar=logvar, z=z, logits=logits)
+    if ids.shape[0] > 1 and eps_marginal is not None:                      # :59-61
+        out['mutual_info'] = kl - marginal_kl(mu, scale, eps_marginal)
+    return out
+
+
+# ---- host-side step pieces -----------------------------------------------------------------------
+
+def clip_grad_norm(grads, max_norm):
+    """torch.nn.utils.clip_grad_norm_ as called at language_model.py:120-122 (2-norm)."""
+    norms = torch.stack([g.detach().double().norm() for g in grads])
+    total = norms.norm()
+    coef = torch.clamp(max_norm / (total + 1e-6), max=1.0)
+    return total, [g * coef.to(g.dtype) for g in grads]
+
+
+class RAdamState:
+    def __init__(self):
+        self.step = 1
+        self.exp_avg = {}
+        self.exp_avg_sq = {}
+
+
+def radam_step(params, grads, state: RAdamState, lr, betas=(0.9, 0.999), eps=1e-6, weight_decay=0.01):
+    """RAdam.step (lamb=False), rectified_adam.py:16-88. 1-indexed step; variance rectification when
+    rho_t > 4, SGD-momentum update otherwise; decoupled weight decay. Returns new params."""
+    beta1, beta2 = betas
+    step = state.step
+    beta2_t = beta2 ** step
+    bcv = (1 - beta2_t) ** 0.5
+    rho_inf = 2.0 / (1.0 - beta2) - 1.0
+    rho_t = rho_inf - 2 * step * beta2_t / (1 - beta2_t)
+    if rho_t > 4:
+        r_t = (((rho_t - 4.0) * (rho_t - 2.0) * rho_inf) / ((rho_inf - 4.0) * (rho_inf - 2.0) * rho_t)) ** 0.5
+        lr = lr * (r_t * bcv)
+    bcm = 1 - beta1 ** step
+    out = {}
+    for name, prm in params.items():
+        g = grads.get(name)
+        if g is None:
+            out[name] = prm
+            continue
+        m = state.exp_avg.get(name, torch.zeros_like(prm))
+        v = state.exp_avg_sq.get(name, torch.zeros_like(prm))
+        m = m * beta1 + g * (1 - beta1)
+        v = v * beta2 + g * g * (1 - beta2)
+        state.exp_avg[name], state.exp_avg_sq[name] = m, v
+        prm = prm * (1 - lr * weight_decay)
+        if rho_t > 4:
+            denom = v.sqrt() / bcv + eps
+            prm = prm - (lr / bcm) * (m / denom)
+        else:
+            prm = prm - (lr / bcm) * m
+        out[name] = prm
+    state.step += 1
+    return out
+
+
+def cosine_decay(decay_steps: int, cur_step: int) -> float:
+    """language_model.py:135-141 (raises KeyboardInterrupt once fully decayed)."""
+    progress = cur_step / max(1, decay_steps)
+    if progress >= 1.0:
+        raise KeyboardInterrupt
+    return max(0.0, 0.5 * (1.0 + math.cos(math.pi * progress)))
+
+
+def kl_anneal(kl_weight, kl_start, kl_end, max_steps, cur_step):
+    """ContinuousVAE.on_after_backward, continuous_autoencoder.py:28-39."""
+    if not max_steps or kl_weight >= kl_end:
+        return kl_weight
+    return kl_start + (kl_end - kl_start) * (cur_step / max_steps)

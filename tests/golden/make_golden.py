@@ -1,0 +1,180 @@
+"""Generate golden vectors by running the REAL reference (`/root/reference`) on CPU, fp32.
+
+Run in the survey/build container only (the GPU box has no /root/reference):
+
+    python tests/golden/make_golden.py
+
+Writes tests/golden/<name>.npz (+ reference_keys.json). Weights are never stored: both the reference and
+every consumer regenerate them from `oracle.params.init_params(hp, seed)` (portable splitmix64 normals).
+Determinism controls: dropout p=0, `Normal.rsample` patched to use injected eps,
+kl_weight pinned.
+"""
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, HERE)
+
+from oracle.params import HParams, init_params, portable_normal, portable_ids, TIED_ALIASES  # noqa: E402
+import ref_stubs  # noqa: E402
+
+# name -> (d_model, num_heads, num_layers, L, B, padded)
+CONFIGS = {
+    'tiny': (128, 8, 4, 128, 4, False),          # minimal buildable "tiny" (4 layers, decoder hd 16)
+    'tiny_pad': (128, 8, 4, 128, 4, True),
+    'small6_pad': (256, 4, 6, 192, 3, True),     # hd 64, one middle (cross-attention) encoder layer
+    'hd96': (384, 4, 6, 128, 2, True),           # decoder hd 96, encoder 6 heads x 64
+    'c2shape': (512, 8, 6, 512, 2, False),       # the C2 model at B=2
+}
+N_SAMPLE = 64   # gradient elements sampled per parameter
+
+
+def lengths_for(B, L, padded):
+    if not padded:
+        return [L] * B
+    return [L - (37 * b) % (L // 2) for b in range(B)]
+
+
+def make_batch(B, L, padded, seed):
+    ids = portable_ids((B, L), seed)
+    lens = lengths_for(B, L, padded)
+    for b, n in enumerate(lens):
+        ids[b, n:] = 0
+    return ids, np.asarray(lens, dtype=np.int64)
+
+
+def sample_indices(n, key):
+    z = portable_normal(N_SAMPLE, 'idx:' + key, 99)
+    return (np.abs(z * 1e6).astype(np.int64) % n).astype(np.int64)
+
+
+def run_config(sv, name, cfg, seed=1234):
+    d, H, NL, L, B, padded = cfg
+    hp = HParams(d_model=d, num_heads=H, num_layers=NL, latent_depth=64, kl_weight=0.7)
+    rhp = sv.TransformerVAEHparams(d_model=d, num_heads=H, num_layers=NL, latent_depth=64,
+                                   sparse_self_attention=False, kl_weight=0.7, start_token=1, end_token=2)
+    torch.manual_seed(0)
+    model = sv.TransformerVAE(rhp)
+    params = init_params(hp, seed)
+    sd = dict(params)
+    for alias in TIED_ALIASES:
+        sd[alias] = params['input_layer.0.weight']
+    missing = set(model.state_dict().keys()) ^ set(sd.keys())
+    assert not missing, missing
+    model.load_state_dict(sd, strict=True)
+    for m in model.modules():
+        if isinstance(m, torch.nn.Dropout):
+            m.p = 0.0
+
+    ids, lens = make_batch(B, L, padded, seed + 1)
+    eps = torch.from_numpy(portable_normal(B * 64, 'eps', seed).reshape(B, 1, 64).astype(np.float32))
+    eps10 = torch.from_numpy(portable_normal(10 * B * 64, 'eps10', seed).reshape(10, B, 1, 64).astype(np.float32))
+
+    from torch.distributions import Normal
+
+    def rsample(self, sample_shape=torch.Size()):
+        e = eps if len(sample_shape) == 0 else eps10
+        return self.loc + e * self.scale
+
+    Normal.rsample = rsample
+    PaddedTensor = sys.modules['sparse_vae.core.padded_tensor'].PaddedTensor
+    batch = {
+        'token_ids': PaddedTensor.from_raw(torch.from_numpy(ids.astype(np.int16))),
+        'num_tokens': torch.from_numpy(lens),
+        'num_bytes': torch.from_numpy(lens),
+    }
+    out = model.training_step(batch, 0)
+    out['loss'].backward()
+
+    rec = {
+        'ids': ids.astype(np.int32), 'lens': lens, 'eps': eps.numpy(), 'eps10': eps10.numpy(),
+        'cfg': np.asarray([d, H, NL, L, B, int(padded), seed], dtype=np.int64),
+        'kl_weight': np.float64(0.7),
+        'loss': np.float64(out['loss'].item()),
+        'train_nll': np.float64(model.logged['train_nll'].item()),
+        'train_kl': np.float64(model.logged['train_kl'].item()),
+        'mutual_info': np.float64(model.logged['train_mc_mutual_info'].item()),
+        'mu': out['posterior'].loc.numpy().reshape(B, 64),
+        'scale': out['posterior'].scale.numpy().reshape(B, 64),
+    }
+    names = []
+    for pname, prm in model.named_parameters():
+        if prm.grad is None:
+            continue
+        names.append(pname)
+        g = prm.grad.detach().flatten().double().numpy()
+        rec['gnorm/' + pname] = np.float64(np.linalg.norm(g))
+        idx = sample_indices(g.size, pname)
+        rec['gidx/' + pname] = idx
+        rec['gval/' + pname] = g[idx].astype(np.float32)
+    rec['grad_names'] = np.asarray(names)
+
+    with torch.no_grad():                         # argmax reconstructions at z = mu
+        x = model.input_layer(batch['token_ids'].long())
+        logits = model.reconstruct(x, out['posterior'].loc)[..., :-1, :]
+        top2 = logits.topk(2, dim=-1)
+        rec['argmax'] = top2.indices[..., 0].numpy().astype(np.int32)
+        rec['margin'] = (top2.values[..., 0] - top2.values[..., 1]).numpy().astype(np.float32)
+        rec['logit_rows'] = logits[0, [0, L // 2]].numpy().astype(np.float32)
+    np.savez_compressed(os.path.join(HERE, name + '.npz'), **rec)
+    print(f'{name}: loss={rec["loss"]:.6f} nll={rec["train_nll"]:.6f} kl={rec["train_kl"]:.6f} '
+          f'grads={len(names)}')
+    return model
+
+
+def op_vectors(sv):
+    core = sys.modules['sparse_vae.core.attention']
+    rec = {}
+    for i, (shape, start, max_pos) in enumerate([((2, 5, 16), 0, 10000), ((3, 7, 64), 3, 10000),
+                                                  ((1, 300, 32), 0, 256)]):
+        x = torch.from_numpy(portable_normal(int(np.prod(shape)), f'rot{i}', 5).reshape(shape).astype(np.float32))
+        rec[f'rot{i}_in'] = x.numpy().copy()
+        rec[f'rot{i}_meta'] = np.asarray([start, max_pos])
+        rec[f'rot{i}_out'] = core.encode_position_rotary(x.clone(), start, max_pos=max_pos).numpy()
+
+    # RAdam: 8 steps crosses the SGD-momentum (steps 1-4) -> rectified (>= 5) switch.
+    RAdam = sys.modules['sparse_vae.core.rectified_adam'].RAdam
+    p0 = torch.from_numpy(portable_normal(300, 'radam_p', 5).astype(np.float32)).reshape(10, 30)
+    p1 = torch.from_numpy(portable_normal(7, 'radam_q', 5).astype(np.float32))
+    prm = [torch.nn.Parameter(p0.clone()), torch.nn.Parameter(p1.clone())]
+    opt = RAdam(prm, lr=3e-3, weight_decay=0.01)
+    rec['radam_p0'], rec['radam_p1'] = p0.numpy(), p1.numpy()
+    for s in range(8):
+        g0 = portable_normal(300, f'radam_g0_{s}', 5).astype(np.float32).reshape(10, 30)
+        g1 = portable_normal(7, f'radam_g1_{s}', 5).astype(np.float32)
+        rec[f'radam_g0_{s}'], rec[f'radam_g1_{s}'] = g0, g1
+        prm[0].grad, prm[1].grad = torch.from_numpy(g0), torch.from_numpy(g1)
+        opt.step()
+        rec[f'radam_out0_{s}'] = prm[0].detach().numpy().copy()
+        rec[f'radam_out1_{s}'] = prm[1].detach().numpy().copy()
+
+    lm = sys.modules['sparse_vae.core.language_model']
+    rec['cosine'] = np.asarray([lm.cosine_decay(1000, s) for s in (0, 1, 250, 500, 999)])
+    np.savez_compressed(os.path.join(HERE, 'ops.npz'), **rec)
+    print('ops: written')
+
+
+def main():
+    torch.set_num_threads(min(8, os.cpu_count()))
+    sv = ref_stubs.import_reference()
+    keys = {}
+    only = sys.argv[1:]
+    for name, cfg in CONFIGS.items():
+        if only and name not in only:
+            continue
+        model = run_config(sv, name, cfg)
+        keys[name] = {k: list(v.shape) for k, v in model.state_dict().items()}
+    if not only:
+        with open(os.path.join(HERE, 'reference_keys.json'), 'w') as f:
+            json.dump(keys, f, indent=0)
+        op_vectors(sv)
+
+
+if __name__ == '__main__':
+    main()

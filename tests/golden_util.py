@@ -1,0 +1,24 @@
+"""Helpers shared by the tests: load a golden fixture and rebuild its inputs/weights."""
+import os
+
+import numpy as np
+import torch
+
+from oracle.params import HParams, init_params
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden')
+CONFIG_NAMES = ['tiny', 'tiny_pad', 'small6_pad', 'hd96', 'c2shape']
+
+
+def load(name):
+    with np.load(os.path.join(GOLDEN, name + '.npz'), allow_pickle=False) as z:
+        return {k: z[k] for k in z.files}
+
+
+def setup(name):
+    g = load(name)
+    d, H, NL, L, B, padded, seed = [int(v) for v in g['cfg']]
+    hp = HParams(d_model=d, num_heads=H, num_layers=NL, latent_depth=64, kl_weight=float(g['kl_weight']))
+    params = init_params(hp, seed)
+    ids = torch.from_numpy(g['ids'].astype(np.int64))
+    return g, hp, params, ids

@@ -1,0 +1,89 @@
+"""Pin the CPU oracle (oracle/) against golden vectors produced by the real reference
+(tests/golden/make_golden.py). CPU only."""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from oracle.params import param_shapes, TIED_ALIASES
+from golden_util import GOLDEN, CONFIG_NAMES, load, setup
+
+
+def _rel(a, b):
+    return abs(float(a) - float(b)) / max(abs(float(b)), 1e-30)
+
+
+@pytest.mark.parametrize('name', CONFIG_NAMES)
+def test_param_inventory_matches_reference(name):
+    with open(os.path.join(GOLDEN, 'reference_keys.json')) as f:
+        ref = json.load(f)[name]
+    g, hp, params, _ = setup(name)
+    mine = {k: list(v) for k, v in param_shapes(hp).items()}
+    for alias in TIED_ALIASES:
+        mine[alias] = mine['input_layer.0.weight']
+    assert mine == ref
+
+
+@pytest.mark.parametrize('name', CONFIG_NAMES)
+def test_training_step_matches_reference(name):
+    torch.set_num_threads(min(8, os.cpu_count()))
+    g, hp, params, ids = setup(name)
+    p = {k: v.clone().requires_grad_(True) for k, v in params.items()}
+    out = oracle.training_step(p, hp, ids, torch.from_numpy(g['lens']), torch.from_numpy(g['eps']),
+                               eps_marginal=torch.from_numpy(g['eps10']))
+    out['loss'].backward()
+    assert _rel(out['loss'].item(), g['loss']) < 1e-6
+    assert _rel(out['nll'].item(), g['train_nll']) < 1e-6
+    assert _rel(out['train_kl'].item(), g['train_kl']) < 1e-5
+    assert abs(out['mutual_info'].item() - g['mutual_info']) < 1e-4 * max(1.0, abs(g['mutual_info']))
+    np.testing.assert_allclose(out['mu'].detach().numpy().reshape(g['mu'].shape), g['mu'], rtol=1e-5, atol=1e-6)
+    names = [str(n) for n in g['grad_names']]
+    have = {k for k, v in p.items() if v.grad is not None}
+    assert set(names) == have            # pos_linear etc. receive no gradient in either
+    for n in names:
+        gr = p[n].grad.detach().flatten().double().numpy()
+        assert _rel(np.linalg.norm(gr), g['gnorm/' + n]) < 1e-4, n
+        np.testing.assert_allclose(gr[g['gidx/' + n]], g['gval/' + n], rtol=2e-3, atol=2e-7 + 2e-4 * np.abs(g['gval/' + n]).max())
+
+
+@pytest.mark.parametrize('name', ['tiny', 'small6_pad'])
+def test_argmax_reconstruction_matches_reference(name):
+    g, hp, params, ids = setup(name)
+    with torch.no_grad():
+        pad = ids.eq(0)
+        x = torch.nn.functional.embedding(ids, params['input_layer.0.weight'])
+        mu = torch.from_numpy(g['mu']).reshape(-1, 1, 64)
+        logits = oracle.reconstruct(params, x, mu, pad, hp)[..., :-1, :]
+    am = logits.argmax(-1).numpy()
+    assert (am == g['argmax']).all()
+    np.testing.assert_allclose(logits[0, [0, ids.shape[1] // 2]].numpy(), g['logit_rows'], rtol=1e-4, atol=1e-5)
+
+
+def test_rotary_matches_reference():
+    g = load('ops')
+    for i in range(3):
+        start, max_pos = [int(v) for v in g[f'rot{i}_meta']]
+        out = oracle.rotary(torch.from_numpy(g[f'rot{i}_in']), start, max_pos)
+        np.testing.assert_array_equal(out.numpy(), g[f'rot{i}_out'])
+
+
+def test_radam_matches_reference():
+    g = load('ops')
+    params = {'p0': torch.from_numpy(g['radam_p0']), 'p1': torch.from_numpy(g['radam_p1'])}
+    st = oracle.RAdamState()
+    for s in range(8):
+        grads = {'p0': torch.from_numpy(g[f'radam_g0_{s}']), 'p1': torch.from_numpy(g[f'radam_g1_{s}'])}
+        params = oracle.radam_step(params, grads, st, lr=3e-3, weight_decay=0.01)
+        np.testing.assert_allclose(params['p0'].numpy(), g[f'radam_out0_{s}'], rtol=1e-6, atol=1e-7)
+        np.testing.assert_allclose(params['p1'].numpy(), g[f'radam_out1_{s}'], rtol=1e-6, atol=1e-7)
+
+
+def test_cosine_decay_matches_reference():
+    g = load('ops')
+    got = [oracle.cosine_decay(1000, s) for s in (0, 1, 250, 500, 999)]
+    np.testing.assert_allclose(got, g['cosine'], rtol=0, atol=0)
+    with pytest.raises(KeyboardInterrupt):
+        oracle.cosine_decay(1000, 1000)
