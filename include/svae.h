@@ -1,0 +1,178 @@
+/*
+ * svae.h — C ABI of libsvae.so, the MI355X (gfx950) kernels behind the sparse-vae TransformerVAE
+ * training step.
+ *
+ * The reference (norabelrose/sparse-vae) has NO native layer: its hot path is PyTorch ATen ops called
+ * from nn.Modules. Each entry point below replaces the ATen op sequence of one
+ * reference call site (cited per function); the Python host package (sparse-vae_amd/sparse_vae) keeps
+ * the reference's nn.Module / LightningModule surface and calls these through ctypes.
+ *
+ * Conventions (all entry points):
+ *   - device pointers are plain addresses of memory owned by the caller (PyTorch's caching allocator);
+ *     the library never allocates, frees or synchronises;
+ *   - element types: bf16 = 16-bit bfloat16 storage, f32 = IEEE float;
+ *   - `stream` is a hipStream_t; work is enqueued asynchronously on it;
+ *   - return 0 on success, SVAE_EINVAL (1) on a bad argument (nothing launched), SVAE_ELAUNCH (2) if
+ *     the launch failed. The Python layer raises RuntimeError on any non-zero status.
+ */
+#ifndef SVAE_H
+#define SVAE_H
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* svae_stream_t; /* hipStream_t */
+
+/* ---- GEMM: C[M,N] = epi(alpha * A[M,K] . B[K,N]) ------------------------------------------------
+ * Replaces nn.Linear forward (addmm) and its autograd backward (mm for dX and dW) at every Linear of
+ * the path: attention.py:33-38,60,67,103; transformer_layer.py:17-21; transformer_language_model.py:55-63;
+ * conditional_gaussian.py:18; transformer_vae.py:37-40,89.
+ * a_t = 0: A stored [M][K] (lda >= K); a_t = 1: A stored [K][M] (lda >= M).
+ * b_t = 0: B stored [N][K] (nn.Linear weight layout); b_t = 1: B stored [K][N].
+ * Requirements: K % 8 == 0 unless a_t && b_t; for a_t: M % 8 == 0; for b_t: N % 8 == 0; lda, ldb % 8 == 0;
+ * A, B 16-byte aligned. */
+enum svae_epi {
+  SVAE_EPI_BF16 = 0,          /* C bf16 = alpha*acc + bias                                            */
+  SVAE_EPI_F32 = 1,           /* C f32  = alpha*acc + bias (+ resid)                                  */
+  SVAE_EPI_F32_ACC = 2,       /* C f32 += alpha*acc                                                   */
+  SVAE_EPI_F32_ATOMIC = 3,    /* atomicAdd(C f32, alpha*acc)   (split-K / shared destinations)        */
+  SVAE_EPI_GELU = 4,          /* aux bf16 = acc + bias;  C bf16 = gelu(acc + bias)                     */
+  SVAE_EPI_GELU_BWD = 5,      /* C bf16 = acc * gelu'(aux)                                             */
+  SVAE_EPI_DROPOUT_RESID = 6, /* C f32 = resid + keep(seed, m*N+n) * acc / (1 - p)                     */
+  SVAE_EPI_ROTARY_BF16 = 7,   /* C bf16 = rotary(acc + bias) on cols < rot_cols (attention.py:194-208) */
+  SVAE_EPI_CE_STATS = 8       /* C bf16 = acc + bias; per (row, 128-col tile) online (max, sumexp) to
+                                 aux f32 [M][ceil(N/128)][2]; label logit (f32) to resid-as-out [M]   */
+};
+
+typedef struct svae_gemm_desc {
+  const void* A;
+  const void* B;
+  int64_t lda, ldb, batch_stride_a, batch_stride_b;
+  int32_t M, N, K;
+  int32_t batch, splits;
+  int32_t a_t, b_t;
+  int32_t epi;
+  void* C;
+  int64_t ldc, batch_stride_c;
+  const float* bias;        /* [N] f32 or NULL */
+  const float* resid;       /* f32 [M][ldr] or NULL (DROPOUT_RESID / F32); may alias C */
+  int64_t ldr;
+  void* aux;                /* see svae_epi */
+  int64_t ldaux;
+  float alpha;
+  float drop_p;
+  uint64_t seed;
+  const float* rot_tab;     /* [rot_seq][rot_d/2] x (cos, sin) f32 */
+  int32_t rot_cols, rot_d, rot_seq;
+  const int32_t* labels;    /* CE_STATS: [M] target column per row (0 = ignored) */
+  float* label_logit;       /* CE_STATS: [M] f32 out */
+} svae_gemm_desc;
+
+int svae_gemm(const svae_gemm_desc* d, svae_stream_t stream);
+
+/* ---- LayerNorm ---------------------------------------------------------------------------------
+ * nn.LayerNorm(d, eps=1e-5) forward/backward: transformer_layer.py:23-24,39-40,47,52,56;
+ * transformer_language_model.py:59. x_dtype: 0 = f32 input, 1 = bf16 input. y is bf16.
+ * Backward: dx = dres + LN'(dy) (dres may be NULL), written f32 to dx and (optionally) bf16 to dx_bf;
+ * per-block partial (dw, db) sums go to part[nblk][2][D] (reduce with svae_colsum). Rows with
+ * (row % zero_mod == 0) get dx = 0 when zero_mod > 0 (position-0 overwrite, transformer_vae.py:89-90). */
+int svae_layernorm_fwd(const void* x, int32_t x_dtype, const float* w, const float* b, void* y,
+                       float* mean, float* rstd, int32_t rows, int32_t D, svae_stream_t stream);
+int svae_layernorm_bwd(const void* dy, const void* x, int32_t x_dtype, const float* w, const float* mean,
+                       const float* rstd, const float* dres, float* dx, void* dx_bf, float* part,
+                       int32_t nblk, int32_t rows, int32_t D, int32_t zero_mod, svae_stream_t stream);
+int svae_layernorm_nblk(int32_t rows);
+
+/* ---- column sums: out[j] (+)= sum_i in[i*ld + j] (bias grads, LN affine grads, batch sums) ----------
+ * in_dtype 0 = f32, 1 = bf16. accumulate: 0 = overwrite, 1 = add into out. */
+int svae_colsum(const void* in, int32_t in_dtype, int32_t rows, int32_t cols, int64_t ld, float* out,
+                int32_t accumulate, svae_stream_t stream);
+
+/* ---- Flash attention (dense path of Attention.forward, attention.py:51-105) ------------------------
+ * q/k/v/o: bf16 rows of H*hd (token-major, head-interleaved, exactly the nn.Linear output layout),
+ * row strides sq/sk/sv/so elements, batch strides bq/bk/bv/bo elements (bq = 0 for learned queries).
+ * key_pad: uint8 [B][Lk] (1 = masked, padded_tensor.py:16) or NULL. causal: mask key > query
+ * (attention.py:85-95). lse: f32 [B][H][Lq]. scale = hd^-0.5 (attention.py:83). */
+typedef struct svae_attn_desc {
+  const void* q; const void* k; const void* v; void* o;
+  int64_t sq, sk, sv, so, bq, bk, bv, bo;
+  const uint8_t* key_pad;
+  float* lse;
+  int32_t B, H, Lq, Lk, hd, causal;
+  float scale;
+  /* backward only */
+  const void* dout; int64_t sdo, bdo;
+  float* delta;             /* [B][H][Lq] f32 workspace */
+  float* dq;                /* f32 [B][Lq][H*hd] accumulator, batch stride bdq (must be zeroed) */
+  int64_t bdq;
+  void* dk; void* dv;       /* bf16 outputs, row stride sdk/sdv, batch stride bdk/bdv */
+  int64_t sdk, sdv, bdk, bdv;
+  const float* rot_tab;     /* inverse rotary applied to dk when non-NULL ([Lk][d/2] (cos, sin)) */
+  int32_t rot_d;
+} svae_attn_desc;
+
+int svae_attn_fwd(const svae_attn_desc* d, svae_stream_t stream);
+int svae_attn_bwd(const svae_attn_desc* d, svae_stream_t stream);
+/* dq f32 [rows][H*hd] -> bf16 out (row stride ldo) with optional inverse rotary (pos = row % seq). */
+int svae_dq_finalize(const float* dq, void* out, int64_t ldo, int32_t rows, int32_t D, const float* rot_tab,
+                     int32_t seq, svae_stream_t stream);
+
+/* ---- embedding (transformer_language_model.py:40-48): gather rows / scatter-add grads ------------- */
+int svae_embedding_fwd(const int32_t* ids, const void* table_bf, float* out, void* out_bf, int32_t rows,
+                       int32_t D, svae_stream_t stream);
+int svae_embedding_bwd(const int32_t* ids, const float* dout, float* dtable, int32_t rows, int32_t D,
+                       svae_stream_t stream);
+
+/* ---- reparameterise + KL (conditional_gaussian.py:18-28, continuous_autoencoder.py:42-52) -----------
+ * stats: f32 [B][2*Z] (mu | logvar). eps: f32 [B][Z] or NULL (then drawn from (seed) in-kernel).
+ * z out bf16 [B][Z] and f32 copy; raw_kl f32 [B]; kl_out f32[2] = {mean(raw_kl / ntok), mean(raw_kl)}.
+ * Backward: dstats from dz (bf16 or f32) and the scalar kl gradient weight. */
+int svae_reparam_kl_fwd(const float* stats, const float* eps, uint64_t seed, const int64_t* ntok,
+                        float* z, void* z_bf, float* eps_out, float* raw_kl, float* kl_out, int32_t B,
+                        int32_t Z, svae_stream_t stream);
+int svae_reparam_kl_bwd(const float* stats, const float* eps, const float* dz, const int64_t* ntok,
+                        const float* gkl, float* dstats, int32_t B, int32_t Z, svae_stream_t stream);
+
+/* ---- cross entropy over materialised bf16 logits (robust_cross_entropy, language_model.py:161-170) --
+ * part: f32 [rows][ntile][2] (max, sumexp) from SVAE_EPI_CE_STATS; label_logit f32 [rows].
+ * Row r is position (r % seq) of its sequence; label 0 = ignore_index. The sequence positions are cut
+ * into nchunks chunks of chunk_len (torch.chunk semantics) and nll = mean over chunks of the per-chunk
+ * mean loss. finalize: lse[rows], row_loss[rows], chunk_w[nchunks] (= 1 / (count_c * nchunks)),
+ * nll_out[1]. grad: in place, logits -> gscale[0] * chunk_w[c] * (softmax - onehot) in bf16 (0 for
+ * ignored rows). nchunks <= 8. */
+int svae_ce_finalize(const float* part, int32_t ntile, const float* label_logit, const int32_t* labels,
+                     int32_t rows, int32_t seq, int32_t nchunks, int32_t chunk_len, float* lse, float* row_loss,
+                     float* chunk_w, float* nll_out, svae_stream_t stream);
+int svae_ce_grad(void* logits, int64_t ld, const float* lse, const float* chunk_w, const int32_t* labels,
+                 const float* gscale, int32_t rows, int32_t V, int32_t seq, int32_t nchunks, int32_t chunk_len,
+                 svae_stream_t stream);
+
+/* ---- elementwise helpers ------------------------------------------------------------------------ */
+/* dropout backward + cast: out bf16 = keep(seed, idx) * g / (1-p) (p = 0: plain cast). */
+int svae_dropout_bwd_cast(const float* g, void* out, float p, uint64_t seed, int64_t n, int32_t cols,
+                          int64_t ld_in, svae_stream_t stream);
+/* GELU backward (transformer_language_model.py:57 head GELU): out bf16 = dx * gelu'(pre). */
+int svae_gelu_bwd(const float* dx, const void* pre, void* out, int64_t n, svae_stream_t stream);
+/* cast f32 -> bf16 (n elements). */
+int svae_cast_bf16(const float* in, void* out, int64_t n, svae_stream_t stream);
+/* rows of x (f32 [rows][D], stride ld) whose (row % mod == 0) are copied to out [rows/mod][D] and zeroed
+ * (the position-0 gradient of the z-projection splice, transformer_vae.py:89-90). */
+int svae_extract_rows(float* x, int64_t ld, int32_t rows, int32_t mod, int32_t D, float* out,
+                      svae_stream_t stream);
+
+/* ---- optimiser (RAdam, rectified_adam.py:16-88; clip_grad_norm_, language_model.py:120-122) -------
+ * sumsq: partial sums of g^2 over n elements into part[nblk]; radam: reads part to form the global
+ * norm, clips, updates m, v, p (f32) and the bf16 shadow pbf in one pass. scal: {lr_eff, bcm, bcv,
+ * rho_ok, beta1, beta2, eps, wd_lr, max_norm}. norm_out[0] = total grad norm (pre-clip). */
+int svae_sumsq(const float* g, int64_t n, float* part, int32_t nblk, svae_stream_t stream);
+int svae_radam(float* p, void* pbf, const float* g, float* m, float* v, int64_t n, const float* part,
+               int32_t nblk, const float* scal, float* norm_out, svae_stream_t stream);
+
+/* library identification: returns a static string (build id, target arch). */
+const char* svae_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

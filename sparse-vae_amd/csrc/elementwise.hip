@@ -1,0 +1,442 @@
+// HBM-bound and latency-bound pieces of the TransformerVAE step:
+//   embedding gather / scatter-add      transformer_language_model.py:40-48 (tied head, :62-63)
+//   reparameterise + KL (wave per sample) conditional_gaussian.py:18-28, continuous_autoencoder.py:42-52
+//   cross-entropy finalize / gradient   language_model.py:98-113, 161-170
+//   dropout-backward cast, splice-row extraction, dq finalize (inverse rotary, attention.py:194-208)
+//   RAdam + clip (fused, one pass)      rectified_adam.py:16-88, language_model.py:120-122
+#include "common.h"
+#include "../../include/svae.h"
+
+using namespace svae;
+
+namespace {
+
+// ------------------------------------------------------------------ embedding
+__global__ __launch_bounds__(256) void emb_fwd_kernel(const int* __restrict__ ids, const float* __restrict__ table,
+                                                      float* __restrict__ out, bf16* __restrict__ out_bf, int rows,
+                                                      int D) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const long long src = (long long)ids[row] * D;
+  for (int c = lane * 4; c < D; c += 256) {
+    const f32x4 v = *(const f32x4*)(table + src + c);
+    *(f32x4*)(out + (long long)row * D + c) = v;
+    if (out_bf)
+      *(bf16x4*)(out_bf + (long long)row * D + c) = (bf16x4){f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
+  }
+}
+
+__global__ __launch_bounds__(256) void emb_bwd_kernel(const int* __restrict__ ids, const float* __restrict__ dout,
+                                                      float* __restrict__ dtable, int rows, int D) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const long long dst = (long long)ids[row] * D;
+  for (int c = lane; c < D; c += 64) atomicAdd(dtable + dst + c, dout[(long long)row * D + c]);
+}
+
+// ------------------------------------------------------------------ reparameterise + KL
+// One wave per sample (latent index on the lane); one block of 4 waves walks all samples so the batch
+// means come out of the same launch.
+__global__ __launch_bounds__(256) void reparam_fwd_kernel(const float* __restrict__ stats, const float* __restrict__ eps_in,
+                                                          unsigned long long seed, const long long* __restrict__ ntok,
+                                                          float* __restrict__ z, bf16* __restrict__ z_bf,
+                                                          float* __restrict__ eps_out, float* __restrict__ raw_kl,
+                                                          float* __restrict__ kl_out, int B, int Z) {
+  __shared__ float red[2][4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float acc_norm = 0.f, acc_raw = 0.f;
+  for (int b = wave; b < B; b += 4) {
+    float klsum = 0.f;
+    for (int j = lane; j < Z; j += 64) {
+      const float mu = stats[(long long)b * 2 * Z + j];
+      const float lv = stats[(long long)b * 2 * Z + Z + j];
+      const float var = __expf(lv);
+      const float sd = sqrtf(var);
+      float e;
+      if (eps_in) {
+        e = eps_in[(long long)b * Z + j];
+      } else {  // Box-Muller over two counter-based uniforms
+        const unsigned long long idx = ((unsigned long long)b * Z + j) * 2ull;
+        const float u1 = rand_uniform(seed, idx), u2 = rand_uniform(seed, idx + 1);
+        e = sqrtf(-2.f * __logf(u1)) * __cosf(6.283185307179586f * u2);
+      }
+      if (eps_out) eps_out[(long long)b * Z + j] = e;
+      const float zz = mu + e * sd;
+      z[(long long)b * Z + j] = zz;
+      if (z_bf) z_bf[(long long)b * Z + j] = f2bf(zz);
+      klsum += 0.5f * (mu * mu + var - lv - 1.0f);
+    }
+    klsum = wave_sum(klsum);
+    if (lane == 0) raw_kl[b] = klsum;
+    acc_raw += klsum;
+    acc_norm += klsum / (float)ntok[b];
+  }
+  if (lane == 0) { red[0][wave] = acc_norm; red[1][wave] = acc_raw; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    kl_out[0] = (red[0][0] + red[0][1] + red[0][2] + red[0][3]) / B;
+    kl_out[1] = (red[1][0] + red[1][1] + red[1][2] + red[1][3]) / B;
+  }
+}
+
+__global__ __launch_bounds__(256) void reparam_bwd_kernel(const float* __restrict__ stats, const float* __restrict__ eps,
+                                                          const float* __restrict__ dz, const long long* __restrict__ ntok,
+                                                          const float* __restrict__ gkl, float* __restrict__ dstats,
+                                                          int B, int Z) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= B * Z) return;
+  const int b = i / Z, j = i % Z;
+  const float mu = stats[(long long)b * 2 * Z + j];
+  const float lv = stats[(long long)b * 2 * Z + Z + j];
+  const float var = __expf(lv), sd = sqrtf(var);
+  const float w = gkl[0] / ((float)B * (float)ntok[b]);   // d loss / d raw_kl[b]
+  const float g = dz ? dz[i] : 0.f;
+  dstats[(long long)b * 2 * Z + j] = g + w * mu;
+  dstats[(long long)b * 2 * Z + Z + j] = g * eps[i] * sd * 0.5f + w * 0.5f * (var - 1.0f);
+}
+
+// ------------------------------------------------------------------ cross entropy
+// Row pass: lse from the per-128-column (max, sumexp) partials of the logits GEMM, per-row loss.
+__global__ __launch_bounds__(256) void ce_rows_kernel(const float* __restrict__ part, int ntile,
+                                                      const float* __restrict__ label_logit, const int* __restrict__ labels,
+                                                      int rows, float* __restrict__ lse, float* __restrict__ row_loss) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const float2* pr = (const float2*)part + (long long)row * ntile;
+  float mx = -INFINITY;
+  for (int t = lane; t < ntile; t += 64) mx = fmaxf(mx, pr[t].x);
+  mx = wave_max(mx);
+  float se = 0.f;
+  for (int t = lane; t < ntile; t += 64) {
+    const float2 v = pr[t];
+    se += (v.x == -INFINITY) ? 0.f : v.y * __expf(v.x - mx);
+  }
+  se = wave_sum(se);
+  if (lane == 0) {
+    const float l = mx + __logf(se);
+    lse[row] = l;
+    row_loss[row] = labels[row] != 0 ? l - label_logit[row] : 0.f;
+  }
+}
+
+// Chunked mean-of-means (robust_cross_entropy): single block; writes nll and per-chunk row weights.
+__global__ __launch_bounds__(1024) void ce_reduce_kernel(const float* __restrict__ row_loss, const int* __restrict__ labels,
+                                                         int rows, int seq, int nchunks, int chunk_len,
+                                                         float* __restrict__ chunk_w, float* __restrict__ nll_out) {
+  __shared__ float ssum[32][8];
+  __shared__ float scnt[32][8];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;   // 16 waves
+  float s[8], c[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { s[k] = 0.f; c[k] = 0.f; }
+  for (int r = threadIdx.x; r < rows; r += 1024) {
+    const int pos = r % seq;
+    const int ch = min(pos / chunk_len, nchunks - 1);
+    if (labels[r] != 0) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (k == ch) { s[k] += row_loss[r]; c[k] += 1.f; }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { s[k] = wave_sum(s[k]); c[k] = wave_sum(c[k]); }
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { ssum[wave][k] = s[k]; scnt[wave][k] = c[k]; }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float nll = 0.f;
+    for (int k = 0; k < nchunks; ++k) {
+      float ts = 0.f, tc = 0.f;
+      for (int w = 0; w < 16; ++w) { ts += ssum[w][k]; tc += scnt[w][k]; }
+      nll += ts / tc;
+      chunk_w[k] = 1.0f / (tc * (float)nchunks);
+    }
+    nll_out[0] = nll / nchunks;
+  }
+}
+
+// dlogits = g * w_row * (softmax - onehot), in place on bf16 logits; 8 elements per thread.
+__global__ __launch_bounds__(256) void ce_grad_kernel(bf16* __restrict__ logits, long long ld, const float* __restrict__ lse,
+                                                      const float* __restrict__ chunk_w, const int* __restrict__ labels,
+                                                      const float* __restrict__ gscale, int rows, int V, int seq,
+                                                      int nchunks, int chunk_len) {
+  const long long vec_per_row = V / 8;
+  const long long total = (long long)rows * vec_per_row;
+  const float g = gscale[0];
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const int row = (int)(i / vec_per_row);
+    const int c0 = (int)(i % vec_per_row) * 8;
+    bf16x8* ptr = (bf16x8*)(logits + (long long)row * ld + c0);
+    const int lab = labels[row];
+    if (lab == 0) { *ptr = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0}; continue; }
+    const int ch = min((row % seq) / chunk_len, nchunks - 1);
+    const float w = g * chunk_w[ch];
+    const float l = lse[row];
+    bf16x8 v = *ptr;
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float pr = __expf((float)v[e] - l);
+      if (c0 + e == lab) pr -= 1.0f;
+      o[e] = f2bf(w * pr);
+    }
+    *ptr = o;
+  }
+}
+
+// ------------------------------------------------------------------ misc elementwise
+__global__ __launch_bounds__(256) void dropout_bwd_cast_kernel(const float* __restrict__ g, bf16* __restrict__ out, float p,
+                                                               unsigned long long seed, long long n, int cols, long long ld_in) {
+  const float scale = p > 0.f ? 1.0f / (1.0f - p) : 1.0f;
+  for (long long i = ((long long)blockIdx.x * 256 + threadIdx.x) * 4; i < n; i += (long long)gridDim.x * 1024) {
+    const long long r = i / cols;
+    const int c = (int)(i % cols);
+    const f32x4 v = *(const f32x4*)(g + r * ld_in + c);
+    bf16x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float x = v[e];
+      if (p > 0.f) x = (rand_uniform(seed, (unsigned long long)(i + e)) >= p) ? x * scale : 0.f;
+      o[e] = f2bf(x);
+    }
+    *(bf16x4*)(out + i) = o;
+  }
+}
+
+__global__ __launch_bounds__(256) void gelu_bwd_kernel(const float* __restrict__ dx, const bf16* __restrict__ pre,
+                                                       bf16* __restrict__ out, long long n) {
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256)
+    out[i] = f2bf(dx[i] * gelu_grad_f((float)pre[i]));
+}
+
+__global__ __launch_bounds__(256) void cast_kernel(const float* __restrict__ in, bf16* __restrict__ out, long long n) {
+  for (long long i = ((long long)blockIdx.x * 256 + threadIdx.x) * 4; i < n; i += (long long)gridDim.x * 1024) {
+    if (i + 4 <= n) {
+      const f32x4 v = *(const f32x4*)(in + i);
+      *(bf16x4*)(out + i) = (bf16x4){f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
+    } else {
+      for (long long j = i; j < n; ++j) out[j] = f2bf(in[j]);
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void extract_rows_kernel(float* __restrict__ x, long long ld, int nout, int mod, int D,
+                                                           float* __restrict__ out) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= nout * D) return;
+  const int r = i / D, c = i % D;
+  float* src = x + (long long)r * mod * ld + c;
+  out[(long long)r * D + c] = *src;
+  *src = 0.f;
+}
+
+__global__ __launch_bounds__(256) void dq_finalize_kernel(const float* __restrict__ dq, bf16* __restrict__ out, long long ldo,
+                                                          int rows, int D, const float* __restrict__ rot, int seq) {
+  const long long n2 = (long long)rows * (D / 2);
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n2; i += (long long)gridDim.x * 256) {
+    const int row = (int)(i / (D / 2));
+    const int pr = (int)(i % (D / 2));
+    const float2 v = *(const float2*)(dq + (long long)row * D + 2 * pr);
+    float a = v.x, b = v.y;
+    if (rot) {  // inverse of (a c - b s, b c + a s)
+      const float2 cs = ((const float2*)rot)[(long long)(row % seq) * (D / 2) + pr];
+      a = v.x * cs.x + v.y * cs.y;
+      b = -v.x * cs.y + v.y * cs.x;
+    }
+    bf16* o = out + (long long)row * ldo + 2 * pr;
+    o[0] = f2bf(a);
+    o[1] = f2bf(b);
+  }
+}
+
+// ------------------------------------------------------------------ optimiser
+__global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ g, long long n, float* __restrict__ part) {
+  __shared__ float red[4];
+  float s = 0.f;
+  for (long long i = ((long long)blockIdx.x * 256 + threadIdx.x) * 4; i < n; i += (long long)gridDim.x * 1024) {
+    if (i + 4 <= n) {
+      const f32x4 v = *(const f32x4*)(g + i);
+      s += v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3];
+    } else {
+      for (long long j = i; j < n; ++j) s += g[j] * g[j];
+    }
+  }
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+// scal: {lr_eff, bcm, bcv, rho_ok, beta1, beta2, eps, wd, max_norm}
+__global__ __launch_bounds__(256) void radam_kernel(float* __restrict__ p, bf16* __restrict__ pbf, const float* __restrict__ g,
+                                                    float* __restrict__ m, float* __restrict__ v, long long n,
+                                                    const float* __restrict__ part, int nblk, const float* __restrict__ scal,
+                                                    float* __restrict__ norm_out) {
+  __shared__ float red[4];
+  __shared__ float s_coef;
+  float s = 0.f;
+  for (int i = threadIdx.x; i < nblk; i += 256) s += part[i];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float norm = sqrtf(red[0] + red[1] + red[2] + red[3]);
+    const float max_norm = scal[8];
+    s_coef = fminf(1.0f, max_norm / (norm + 1e-6f));
+    if (blockIdx.x == 0 && norm_out) norm_out[0] = norm;
+  }
+  __syncthreads();
+  const float coef = s_coef;
+  const float lr = scal[0], bcm = scal[1], bcv = scal[2], rho_ok = scal[3], b1 = scal[4], b2 = scal[5], eps = scal[6],
+              wd = scal[7];
+  const float step = lr / bcm, decay = 1.0f - lr * wd;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    const float gi = g[i] * coef;
+    const float mi = m[i] * b1 + (1.0f - b1) * gi;
+    const float vi = v[i] * b2 + (1.0f - b2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    float pi = p[i] * decay;
+    if (rho_ok != 0.f) pi -= step * (mi / (sqrtf(vi) / bcv + eps));
+    else pi -= step * mi;
+    p[i] = pi;
+    if (pbf) pbf[i] = f2bf(pi);
+  }
+}
+
+inline int grid_for(long long work, int per_block, int cap = 4096) {
+  long long g = (work + per_block - 1) / per_block;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (int)g;
+}
+
+}  // namespace
+
+SVAE_EXPORT int svae_embedding_fwd(const int32_t* ids, const void* table, float* out, void* out_bf, int32_t rows,
+                                   int32_t D, svae_stream_t stream) {
+  if (!ids || !table || !out || rows <= 0 || D % 4) return SVAE_EINVAL;
+  hipLaunchKernelGGL(emb_fwd_kernel, dim3((rows + 3) / 4), dim3(256), 0, (hipStream_t)stream, ids, (const float*)table,
+                     out, (bf16*)out_bf, rows, D);
+  SVAE_LAUNCH_CHECK();
+  return SVAE_OK;
+}
+
+SVAE_EXPORT int svae_embedding_bwd(const int32_t* ids, const float* dout, float* dtable, int32_t rows, int32_t D,
+                                   svae_stream_t stream) {
+  if (!ids || !dout || !dtable || rows <= 0 || D <= 0) return SVAE_EINVAL;
+  hipLaunchKernelGGL(emb_bwd_kernel, dim3((rows + 3) / 4), dim3(256), 0, (hipStream_t)stream, ids, dout, dtable, rows, D);
+  SVAE_LAUNCH_CHECK();
+  return SVAE_OK;
+}
+
+SVAE_EXPORT int svae_reparam_kl_fwd(const float* stats, const float* eps, uint64_t seed, const int64_t* ntok, float* z,
+                                    void* z_bf, float* eps_out, float* raw_kl, float* kl_out, int32_t B, int32_t Z,
+                                    svae_stream_t stream) {
+  if (!stats || !ntok || !z || !raw_kl || !kl_out || B <= 0 || Z <= 0) return SVAE_EINVAL;
+  hipLaunchKernelGGL(reparam_fwd_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, stats, eps, seed,
+                     (const long long*)ntok, z, (bf16*)z_bf, eps_out, raw_kl, kl_out, B, Z);
+  SVAE_LAUNCH_CHECK();
+  return SVAE_OK;
+}
+
+SVAE_EXPORT int svae_reparam_kl_bwd(const float* stats, const float* eps, const float* dz, const int64_t* ntok,
+                                    const float* gkl, float* dstats, int32_t B, int32_t Z, svae_stream_t stream) {
+  if (!stats || !eps || !ntok || !gkl || !dstats || B <= 0 || Z <= 0) return SVAE_EINVAL;
+  hipLaunchKernelGGL(reparam_bwd_kernel, dim3((B * Z + 255) / 256), dim3(256), 0, (hipStream_t)stream, stats, eps, dz,
+                     (const long long*)ntok, gkl, dstats, B, Z);
+  SVAE_LAUNCH_CHECK();
+  return SVAE_OK;
+}
+
+SVAE_EXPORT int svae_ce_finalize(const float* part, int32_t ntile, const float* label_logit, const int32_t* labels,
+                                 int32_t rows, int32_t seq, int32_t nchunks, int32_t chunk_len, float* lse,
+                                 float* row_loss, float* chunk_w, float* nll_out, svae_stream_t stream) {
+  if (!part || !label_logit || !labels || !lse || !row_loss || !chunk_w || !nll_out) return SVAE_EINVAL;
+  if (rows <= 0 || ntile <= 0 || seq <= 0 || nchunks <= 0 || nchunks > 8 || chunk_len <= 0) return SVAE_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(ce_rows_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, part, ntile, label_logit, labels, rows, lse,
+                     row_loss);
+  hipLaunchKernelGGL(ce_reduce_kernel, dim3(1), dim3(1024), 0, s, row_loss, labels, rows, seq, nchunks, chunk_len,
+                     chunk_w, nll_out);
+  SVAE_LAUNCH_CHECK();
+  return SVAE_OK;
+}
+
+SVAE_EXPORT int svae_ce_grad(void* logits, int64_t ld, const float* lse, const float* chunk_w, const int32_t* labels,
+                             const float* gscale, int32_t rows, int32_t V, int32_t seq, int32_t nchunks,
+                             int32_t chunk_len, svae_stream_t stream) {
+  if (!logits || !lse || !chunk_w || !labels || !gscale || rows <= 0 || V % 8 || ld % 8) return SVAE_EINVAL;
+  const long long work = (long long)rows * (V / 8);
+  hipLaunchKernelGGL(ce_grad_kernel, dim3(grid_for(work, 256, 8192)), dim3(256), 0, (hipStream_t)stream, (bf16*)logits,
+                     ld, lse, chunk_w, labels, gscale, rows, V, seq, nchunks, chunk_len);
+  SVAE_LAUNCH_CHECK();
+  return SVAE_OK;
+}
+
+SVAE_EXPORT int svae_dropout_bwd_cast(const float* g, void* out, float p, uint64_t seed, int64_t n, int32_t cols,
+                                      int64_t ld_in, svae_stream_t stream) {
+  if (!g || !out || n <= 0 || cols <= 0 || cols % 4 || n % cols || ld_in % 4) return SVAE_EINVAL;
+  hipLaunchKernelGGL(dropout_bwd_cast_kernel, dim3(grid_for(n, 1024)), dim3(256), 0, (hipStream_t)stream, g, (bf16*)out,
+                     p, seed, n, cols, ld_in);
+  SVAE_LAUNCH_CHECK();
+  return SVAE_OK;
+}
+
+SVAE_EXPORT int svae_gelu_bwd(const float* dx, const void* pre, void* out, int64_t n, svae_stream_t stream) {
+  if (!dx || !pre || !out || n <= 0) return SVAE_EINVAL;
+  hipLaunchKernelGGL(gelu_bwd_kernel, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream, dx, (const bf16*)pre,
+                     (bf16*)out, n);
+  SVAE_LAUNCH_CHECK();
+  return SVAE_OK;
+}
+
+SVAE_EXPORT int svae_cast_bf16(const float* in, void* out, int64_t n, svae_stream_t stream) {
+  if (!in || !out || n <= 0) return SVAE_EINVAL;
+  hipLaunchKernelGGL(cast_kernel, dim3(grid_for(n, 1024)), dim3(256), 0, (hipStream_t)stream, in, (bf16*)out, n);
+  SVAE_LAUNCH_CHECK();
+  return SVAE_OK;
+}
+
+SVAE_EXPORT int svae_extract_rows(float* x, int64_t ld, int32_t rows, int32_t mod, int32_t D, float* out,
+                                  svae_stream_t stream) {
+  if (!x || !out || rows <= 0 || mod <= 0 || rows % mod || D <= 0) return SVAE_EINVAL;
+  const int nout = rows / mod;
+  hipLaunchKernelGGL(extract_rows_kernel, dim3((nout * D + 255) / 256), dim3(256), 0, (hipStream_t)stream, x, ld, nout,
+                     mod, D, out);
+  SVAE_LAUNCH_CHECK();
+  return SVAE_OK;
+}
+
+SVAE_EXPORT int svae_dq_finalize(const float* dq, void* out, int64_t ldo, int32_t rows, int32_t D, const float* rot_tab,
+                                 int32_t seq, svae_stream_t stream) {
+  if (!dq || !out || rows <= 0 || D <= 0 || D % 2 || (rot_tab && seq <= 0)) return SVAE_EINVAL;
+  const long long work = (long long)rows * (D / 2);
+  hipLaunchKernelGGL(dq_finalize_kernel, dim3(grid_for(work, 256)), dim3(256), 0, (hipStream_t)stream, dq, (bf16*)out,
+                     ldo, rows, D, rot_tab, seq);
+  SVAE_LAUNCH_CHECK();
+  return SVAE_OK;
+}
+
+SVAE_EXPORT int svae_sumsq(const float* g, int64_t n, float* part, int32_t nblk, svae_stream_t stream) {
+  if (!g || !part || n <= 0 || nblk <= 0 || nblk > 4096) return SVAE_EINVAL;
+  hipLaunchKernelGGL(sumsq_kernel, dim3(nblk), dim3(256), 0, (hipStream_t)stream, g, n, part);
+  SVAE_LAUNCH_CHECK();
+  return SVAE_OK;
+}
+
+SVAE_EXPORT int svae_radam(float* p, void* pbf, const float* g, float* m, float* v, int64_t n, const float* part,
+                           int32_t nblk, const float* scal, float* norm_out, svae_stream_t stream) {
+  if (!p || !g || !m || !v || !part || !scal || n <= 0 || nblk <= 0) return SVAE_EINVAL;
+  hipLaunchKernelGGL(radam_kernel, dim3(grid_for(n, 256, 2048)), dim3(256), 0, (hipStream_t)stream, p, (bf16*)pbf, g, m,
+                     v, n, part, nblk, scal, norm_out);
+  SVAE_LAUNCH_CHECK();
+  return SVAE_OK;
+}
+
+SVAE_EXPORT const char* svae_version(void) { return "libsvae 0.1 gfx950"; }

@@ -1,0 +1,222 @@
+// LayerNorm (eps 1e-5, affine) forward / backward, one wave64 per row, and the column-sum reduction used
+// for bias / LayerNorm-affine gradients.
+//
+// Reference: nn.LayerNorm(d) in TransformerLayer (transformer_layer.py:23-24, 39-40, 47, 52, 56) and the
+// output head (transformer_language_model.py:59). HBM-bound: forward moves 4d (f32 in) + 2d (bf16 out)
+// bytes per row; backward reads dy (2d), x (4d), dres (4d) and writes dx (4d + 2d).
+#include "common.h"
+#include "../../include/svae.h"
+
+using namespace svae;
+
+namespace {
+
+constexpr int MAXV = 4;  // float4 chunks per lane: D <= 64 * 4 * MAXV = 1024
+
+template <typename T>
+__device__ __forceinline__ f32x4 load4(const T* p);
+template <>
+__device__ __forceinline__ f32x4 load4<float>(const float* p) { return *(const f32x4*)p; }
+template <>
+__device__ __forceinline__ f32x4 load4<bf16>(const bf16* p) {
+  bf16x4 v = *(const bf16x4*)p;
+  return (f32x4){(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
+}
+__device__ __forceinline__ void store4_bf(bf16* p, f32x4 v) {
+  *(bf16x4*)p = (bf16x4){f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, const float* __restrict__ w,
+                                                     const float* __restrict__ b, bf16* __restrict__ y,
+                                                     float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                     int rows, int D) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const T* xr = x + (long long)row * D;
+  f32x4 v[MAXV];
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < MAXV; ++j) {
+    const int c = (lane + 64 * j) * 4;
+    v[j] = (c < D) ? load4<T>(xr + c) : (f32x4){0.f, 0.f, 0.f, 0.f};
+    s += v[j][0] + v[j][1] + v[j][2] + v[j][3];
+  }
+  const float mean = wave_sum(s) / D;
+  float sq = 0.f;
+#pragma unroll
+  for (int j = 0; j < MAXV; ++j) {
+    const int c = (lane + 64 * j) * 4;
+    if (c < D) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { const float t = v[j][e] - mean; sq += t * t; }
+    }
+  }
+  const float rstd = rsqrtf(wave_sum(sq) / D + 1e-5f);
+#pragma unroll
+  for (int j = 0; j < MAXV; ++j) {
+    const int c = (lane + 64 * j) * 4;
+    if (c < D) {
+      const f32x4 ww = *(const f32x4*)(w + c), bb = *(const f32x4*)(b + c);
+      f32x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = (v[j][e] - mean) * rstd * ww[e] + bb[e];
+      store4_bf(y + (long long)row * D + c, o);
+    }
+  }
+  if (lane == 0) { mean_out[row] = mean; rstd_out[row] = rstd; }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16* __restrict__ dy, const T* __restrict__ x,
+                                                     const float* __restrict__ w, const float* __restrict__ mean_in,
+                                                     const float* __restrict__ rstd_in, const float* __restrict__ dres,
+                                                     float* __restrict__ dx, bf16* __restrict__ dx_bf,
+                                                     float* __restrict__ part, int rows, int D, int zero_mod) {
+  __shared__ float red[4][2][1024];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  f32x4 adw[MAXV], adb[MAXV];
+#pragma unroll
+  for (int j = 0; j < MAXV; ++j) { adw[j] = (f32x4){0.f, 0.f, 0.f, 0.f}; adb[j] = adw[j]; }
+  for (int row = blockIdx.x * 4 + wave; row < rows; row += gridDim.x * 4) {
+    const long long base = (long long)row * D;
+    const float mean = mean_in[row], rstd = rstd_in[row];
+    f32x4 xh[MAXV], g[MAXV];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < MAXV; ++j) {
+      const int c = (lane + 64 * j) * 4;
+      if (c < D) {
+        const f32x4 xv = load4<T>(x + base + c);
+        const f32x4 dv = load4<bf16>(dy + base + c);
+        const f32x4 ww = *(const f32x4*)(w + c);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          xh[j][e] = (xv[e] - mean) * rstd;
+          g[j][e] = dv[e] * ww[e];
+          s1 += g[j][e];
+          s2 += g[j][e] * xh[j][e];
+          adw[j][e] += dv[e] * xh[j][e];
+          adb[j][e] += dv[e];
+        }
+      }
+    }
+    const float m1 = wave_sum(s1) / D, m2 = wave_sum(s2) / D;
+    const bool zero = zero_mod > 0 && (row % zero_mod) == 0;
+#pragma unroll
+    for (int j = 0; j < MAXV; ++j) {
+      const int c = (lane + 64 * j) * 4;
+      if (c < D) {
+        f32x4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = rstd * (g[j][e] - m1 - xh[j][e] * m2);
+        if (dres) {
+          const f32x4 r = *(const f32x4*)(dres + base + c);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] += r[e];
+        }
+        if (zero) o = (f32x4){0.f, 0.f, 0.f, 0.f};
+        *(f32x4*)(dx + base + c) = o;
+        if (dx_bf) store4_bf(dx_bf + base + c, o);
+      }
+    }
+  }
+  // reduce the 4 waves' affine-gradient partials, write this block's slab
+#pragma unroll
+  for (int j = 0; j < MAXV; ++j) {
+    const int c = (lane + 64 * j) * 4;
+    if (c < D) {
+      *(f32x4*)&red[wave][0][c] = adw[j];
+      *(f32x4*)&red[wave][1][c] = adb[j];
+    }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < 2 * D; c += 256) {
+    const int which = c / D, col = c % D;
+    const float s = red[0][which][col] + red[1][which][col] + red[2][which][col] + red[3][which][col];
+    part[((long long)blockIdx.x * 2 + which) * D + col] = s;
+  }
+}
+
+// out[j] += sum_i in[i*ld + j]; block = 4 row-waves x 64 lanes x 4 columns; grid (colblocks, rowsplits).
+template <typename T>
+__global__ __launch_bounds__(256) void colsum_kernel(const T* __restrict__ in, int rows, int cols, long long ld,
+                                                     float* __restrict__ out, int rows_per_split) {
+  __shared__ f32x4 red[4][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = (blockIdx.x * 64 + lane) * 4;
+  const int r0 = blockIdx.y * rows_per_split;
+  const int r1 = min(rows, r0 + rows_per_split);
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  if (c < cols) {
+    for (int r = r0 + wave; r < r1; r += 4) {
+      const f32x4 v = load4<T>(in + (long long)r * ld + c);
+      acc += v;
+    }
+  }
+  red[wave][lane] = acc;
+  __syncthreads();
+  if (wave == 0 && c < cols) {
+    const f32x4 s = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) atomicAdd(out + c + e, s[e]);
+  }
+}
+
+}  // namespace
+
+SVAE_EXPORT int svae_layernorm_fwd(const void* x, int32_t x_dtype, const float* w, const float* b, void* y,
+                                   float* mean, float* rstd, int32_t rows, int32_t D, svae_stream_t stream) {
+  if (!x || !w || !b || !y || !mean || !rstd || rows <= 0 || D <= 0 || D % 4 || D > 1024) return SVAE_EINVAL;
+  dim3 grid((rows + 3) / 4);
+  hipStream_t s = (hipStream_t)stream;
+  if (x_dtype == 0)
+    hipLaunchKernelGGL(ln_fwd_kernel<float>, grid, dim3(256), 0, s, (const float*)x, w, b, (bf16*)y, mean, rstd, rows, D);
+  else
+    hipLaunchKernelGGL(ln_fwd_kernel<bf16>, grid, dim3(256), 0, s, (const bf16*)x, w, b, (bf16*)y, mean, rstd, rows, D);
+  SVAE_LAUNCH_CHECK();
+  return SVAE_OK;
+}
+
+SVAE_EXPORT int svae_layernorm_nblk(int32_t rows) {
+  int n = (rows + 3) / 4;
+  return n < 1024 ? n : 1024;
+}
+
+SVAE_EXPORT int svae_layernorm_bwd(const void* dy, const void* x, int32_t x_dtype, const float* w, const float* mean,
+                                   const float* rstd, const float* dres, float* dx, void* dx_bf, float* part,
+                                   int32_t nblk, int32_t rows, int32_t D, int32_t zero_mod, svae_stream_t stream) {
+  if (!dy || !x || !w || !mean || !rstd || !dx || !part || rows <= 0 || D <= 0 || D % 4 || D > 1024 || nblk <= 0)
+    return SVAE_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  if (x_dtype == 0)
+    hipLaunchKernelGGL(ln_bwd_kernel<float>, dim3(nblk), dim3(256), 0, s, (const bf16*)dy, (const float*)x, w, mean,
+                       rstd, dres, dx, (bf16*)dx_bf, part, rows, D, zero_mod);
+  else
+    hipLaunchKernelGGL(ln_bwd_kernel<bf16>, dim3(nblk), dim3(256), 0, s, (const bf16*)dy, (const bf16*)x, w, mean,
+                       rstd, dres, dx, (bf16*)dx_bf, part, rows, D, zero_mod);
+  SVAE_LAUNCH_CHECK();
+  return SVAE_OK;
+}
+
+SVAE_EXPORT int svae_colsum(const void* in, int32_t in_dtype, int32_t rows, int32_t cols, int64_t ld, float* out,
+                            int32_t accumulate, svae_stream_t stream) {
+  if (!in || !out || rows <= 0 || cols <= 0 || cols % 4 || ld % 4) return SVAE_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  if (!accumulate && hipMemsetAsync(out, 0, sizeof(float) * cols, s) != hipSuccess) return SVAE_ELAUNCH;
+  const int colblocks = (cols + 255) / 256;
+  int splits = (512 + colblocks - 1) / colblocks;
+  int max_splits = (rows + 63) / 64;
+  if (splits > max_splits) splits = max_splits;
+  if (splits < 1) splits = 1;
+  const int rps = (rows + splits - 1) / splits;
+  splits = (rows + rps - 1) / rps;
+  dim3 grid(colblocks, splits);
+  if (in_dtype == 0)
+    hipLaunchKernelGGL(colsum_kernel<float>, grid, dim3(256), 0, s, (const float*)in, rows, cols, ld, out, rps);
+  else
+    hipLaunchKernelGGL(colsum_kernel<bf16>, grid, dim3(256), 0, s, (const bf16*)in, rows, cols, ld, out, rps);
+  SVAE_LAUNCH_CHECK();
+  return SVAE_OK;
+}

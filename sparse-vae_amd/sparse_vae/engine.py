@@ -1,0 +1,545 @@
+"""The TransformerVAE training step on MI355X: explicit forward / backward over libsvae kernels.
+
+Reference path (norabelrose/sparse-vae): `TransformerVAE.training_step` (transformer_vae.py:42-66) with the
+Perceiver encoder (perceiver.py:39-50), `sample_z` (continuous_autoencoder.py:42-52), `reconstruct`
+(transformer_vae.py:85-93), the tied output head (transformer_language_model.py:55-63) and
+`robust_cross_entropy` (language_model.py:161-170), differentiated by autograd.
+
+Here the step is one explicit pass each way. Parameters live in one flat f32 arena (master weights) with a
+bf16 shadow (GEMM operands) and one flat f32 gradient arena, laid out in gradient-ready order so that
+data-parallel buckets are contiguous ranges. Activations stay resident in HBM between the passes (no
+recomputation: 288 GB per GPU makes activation checkpointing unnecessary at these sizes).
+
+Numerics: GEMM/attention operands bf16 with f32 accumulation; residual stream, LayerNorm statistics,
+mu/logvar, KL, softmax statistics and all gradients of the residual stream in f32.
+"""
+import math
+from collections import OrderedDict
+
+import torch
+
+from . import kernels as K
+from ._native import EPI_BF16, EPI_F32, EPI_F32_ACC, EPI_GELU, EPI_GELU_BWD, EPI_DROPOUT_RESID, \
+    EPI_ROTARY_BF16, EPI_CE_STATS
+
+bf16, f32 = torch.bfloat16, torch.float32
+ALIGN = 64
+CE_CHUNK_NUMEL = 2 ** 30      # language_model.py:163
+
+
+# ---------------------------------------------------------------------------------------- layout
+def _attn_entries(pre, d, learned):
+    out = []
+    if learned:
+        out.append((pre + 'learned_queries', (1, learned, d)))
+        names = ['k_linear', 'v_linear']
+    else:
+        names = ['q_linear', 'k_linear', 'v_linear']
+    out += [(pre + n + '.weight', (d, d)) for n in names]      # adjacent -> one [n*d, d] GEMM operand
+    out += [(pre + n + '.bias', (d,)) for n in names]           # adjacent -> one bias vector
+    out += [(pre + 'output_linear.weight', (d, d)), (pre + 'output_linear.bias', (d,))]
+    return out
+
+
+def _layer_entries(pre, d, learned=None, cross=False):
+    out = _attn_entries(pre + 'attention.', d, learned)
+    out += [(pre + 'attn_layer_norm.weight', (d,)), (pre + 'attn_layer_norm.bias', (d,))]
+    if cross:
+        out += _attn_entries(pre + 'cross_attention.', d, None)
+        out += [(pre + 'cross_attn_layer_norm.weight', (d,)), (pre + 'cross_attn_layer_norm.bias', (d,)),
+                (pre + 'context_layer_norm.weight', (d,)), (pre + 'context_layer_norm.bias', (d,))]
+    out += [(pre + 'ffn.0.weight', (4 * d, d)), (pre + 'ffn.0.bias', (4 * d,)), (pre + 'ffn.2.weight', (d, 4 * d)),
+            (pre + 'ffn_layer_norm.weight', (d,)), (pre + 'ffn_layer_norm.bias', (d,))]
+    return out
+
+
+def _pos_linear_entries(pre, d):
+    return [(pre + 'pos_linear.weight', (d, d)), (pre + 'pos_linear.bias', (d,))]
+
+
+def layout_entries(hp):
+    """(name, shape) in gradient-ready order (head -> decoder L-1..0 -> q(z|x) -> encoder -> embedding),
+    then the parameters that never receive a gradient (Attention.pos_linear, attention.py:39)."""
+    d, V, Z, N = hp.d_model, hp.vocab_size, hp.latent_depth, hp.num_latents
+    live = [('output_layer.0.weight', (d, d)), ('output_layer.0.bias', (d,)),
+            ('output_layer.2.weight', (d,)), ('output_layer.2.bias', (d,)), ('output_layer.3.bias', (V,))]
+    dead = []
+    for i in reversed(range(hp.num_layers)):
+        live += _layer_entries(f'decoder_layers.{i}.', d)
+        live += [(f'z_projections.{i}.weight', (d, Z)), (f'z_projections.{i}.bias', (d,))]
+        dead += _pos_linear_entries(f'decoder_layers.{i}.attention.', d)
+    live += [('q_of_z_given_x.linear.weight', (2 * Z, d)), ('q_of_z_given_x.linear.bias', (2 * Z,))]
+    live += _layer_entries('encoder.bottleneck.', d, learned=1)
+    dead += _pos_linear_entries('encoder.bottleneck.attention.', d)
+    for j in reversed(range(hp.enc_layers - 2)):
+        live += _layer_entries(f'encoder.middle_layers.{j}.', d, cross=True)
+        dead += _pos_linear_entries(f'encoder.middle_layers.{j}.attention.', d)
+        dead += _pos_linear_entries(f'encoder.middle_layers.{j}.cross_attention.', d)
+    live += _layer_entries('encoder.first_layer.', d, learned=N)
+    dead += _pos_linear_entries('encoder.first_layer.attention.', d)
+    live += [('input_layer.0.weight', (V, d))]
+    return live, dead
+
+
+class FlatParams:
+    """f32 master arena + bf16 shadow + f32 grad arena; `views[name]` etc. are shaped views."""
+
+    def __init__(self, hp, device):
+        live, dead = layout_entries(hp)
+        self.offsets = OrderedDict()
+        off = 0
+        for name, shape in live + dead:
+            n = math.prod(shape)
+            self.offsets[name] = (off, shape)
+            off += -(-n // ALIGN) * ALIGN
+            if name == live[-1][0]:
+                self.n_live = off
+        self.total = off
+        self.live_names = [n for n, _ in live]
+        self.device = torch.device(device)
+        self.master = torch.zeros(self.total, dtype=f32, device=self.device)
+        self.shadow = torch.zeros(self.total, dtype=bf16, device=self.device) if self.device.type == 'cuda' else None
+        self.grad = torch.zeros(self.total, dtype=f32, device=self.device)
+        self.shadow_version = -1
+
+    def view(self, name, buf=None):
+        off, shape = self.offsets[name]
+        buf = self.master if buf is None else buf
+        return buf[off:off + math.prod(shape)].view(shape)
+
+    def w(self, name):      # bf16 GEMM operand
+        return self.view(name, self.shadow)
+
+    def f(self, name):      # f32 master (biases, LayerNorm affine)
+        return self.view(name)
+
+    def g(self, name):
+        return self.view(name, self.grad)
+
+    def sync_shadow(self, force=False):
+        """Refresh the bf16 shadow if the master changed outside the fused optimiser (load_state_dict,
+        initialize_weights, manual edits) — detected through the arena's shared version counter."""
+        if force or self.master._version != self.shadow_version:
+            K.cast_bf16(self.master, self.shadow)
+            self.shadow_version = self.master._version
+
+
+# ---------------------------------------------------------------------------------------- workspace
+class Workspace:
+    def __init__(self, device):
+        self.device = device
+        self.bufs = {}
+
+    def get(self, name, shape, dtype=bf16, zero=False):
+        t = self.bufs.get(name)
+        if t is None or t.shape != torch.Size(shape) or t.dtype != dtype:
+            t = torch.empty(shape, dtype=dtype, device=self.device)
+            self.bufs[name] = t
+        if zero:
+            t.zero_()
+        return t
+
+
+def rotary_table(positions, d):
+    """cos/sin table exactly as encode_position_rotary builds it (attention.py:194-200), in fp32 on the
+    host so the factors are bitwise those of the fp32 reference; layout [pos][d/2][2]."""
+    half = d // 2
+    freqs = torch.arange(half, dtype=f32)
+    pos = torch.arange(0, positions, dtype=f32)
+    theta = 10000 ** (-freqs / half)
+    ang = pos[:, None] * theta
+    return torch.stack([ang.cos(), ang.sin()], dim=-1).contiguous()
+
+
+def _mix_seed(a, b):
+    x = (a * 0x9E3779B97F4A7C15 + b * 0xBF58476D1CE4E5B9 + 0x94D049BB133111EB) & 0xFFFFFFFFFFFFFFFF
+    x ^= x >> 31
+    return x
+
+
+# ---------------------------------------------------------------------------------------- engine
+class VAEEngine:
+    def __init__(self, hp, flat: FlatParams):
+        self.hp = hp
+        self.P = flat
+        self.ws = Workspace(flat.device)
+        self.d = hp.d_model
+        self.H = hp.num_heads
+        self.He = hp.d_model // 64
+        assert self.d % self.H == 0 and self.d % 64 == 0
+        self.hd = self.d // self.H
+        self._rot = None
+        self.saved = None
+
+    # ------------------------------------------------------------------ helpers
+    def rot(self, L):
+        need = max(L, self.hp.num_latents)
+        if self._rot is None or self._rot.shape[0] < need:
+            self._rot = rotary_table(max(need, 512), self.d).to(self.P.device)
+        return self._rot
+
+    def _ln_fwd(self, name, x, rows, tag):
+        D = self.d
+        y = self.ws.get(tag + '.y', (rows, D))
+        mean = self.ws.get(tag + '.mean', (rows,), f32)
+        rstd = self.ws.get(tag + '.rstd', (rows,), f32)
+        K.layernorm_fwd(x, self.P.f(name + '.weight'), self.P.f(name + '.bias'), y, mean, rstd, rows, D)
+        return y, (x, mean, rstd)
+
+    def _ln_bwd(self, name, dy, st, rows, dres, dx, dx_bf=None):
+        x, mean, rstd = st
+        D = self.d
+        part = self.ws.get('ln.part', (1024 * 2 * D,), f32)
+        wg = self.P.grad[self.P.offsets[name + '.weight'][0]:][:2 * D]   # [weight | bias] grads (adjacent)
+        K.layernorm_bwd(dy, x, self.P.f(name + '.weight'), mean, rstd, dres, dx, dx_bf, wg, rows, D, part)
+
+    def _dw(self, dY, X, wname, rows, n_out, n_in, ldy=None, ldx=None):
+        K.linear_dw(dY, X, self.P.g(wname), rows, n_out, n_in, ldy, ldx)
+
+    def _db(self, dY, bname, rows, cols, ld=None):
+        off = self.P.offsets[bname][0]
+        K.colsum(dY, rows, cols, ld or cols, self.P.grad[off:off + cols])
+
+    # ------------------------------------------------------------------ one transformer layer
+    def layer_fwd(self, pre, x, B, Sx, L, pad, *, learned=0, cross=False, causal=False, ctx=None, heads, hd,
+                  drop_p=0.0, seed=0, tag, out=None):
+        """TransformerLayer.forward (transformer_layer.py:44-61) on x f32 [B*Sx, d]. Returns the f32 output
+        [B*Lq, d] and the saved state for layer_bwd."""
+        d, ws, P = self.d, self.ws, self.P
+        rows_x = B * Sx
+        rot = self.rot(max(Sx, L))
+        st = {'pre': pre, 'B': B, 'Sx': Sx, 'L': L, 'learned': learned, 'cross': cross, 'causal': causal,
+              'heads': heads, 'hd': hd, 'drop_p': drop_p, 'seed': seed, 'x': x, 'tag': tag}
+        a = pre + 'attention.'
+        h, st['ln_a'] = self._ln_fwd(pre + 'attn_layer_norm', x, rows_x, tag + '.ln_a')
+        st['h'] = h
+        pad_k = pad if Sx == L else None          # PaddedTensor getter: mask iff key length == L
+        if learned:
+            Lq = learned
+            kv = ws.get(tag + '.kv', (rows_x, 2 * d))
+            K.gemm(h, P.w(a + 'k_linear.weight'), kv, rows_x, 2 * d, d, epi=EPI_ROTARY_BF16,
+                   bias=P.f(a + 'k_linear.bias'), rot=rot, rot_cols=d, rot_d=d, rot_seq=Sx)
+            q = P.w(a + 'learned_queries').view(Lq, d)
+            qargs = dict(sq=d, bq=0)
+            kt, vt, sk = kv, kv[:, d:], 2 * d
+            st['kv'] = kv
+        else:
+            Lq = Sx
+            qkv = ws.get(tag + '.qkv', (rows_x, 3 * d))
+            K.gemm(h, P.w(a + 'q_linear.weight'), qkv, rows_x, 3 * d, d, epi=EPI_ROTARY_BF16,
+                   bias=P.f(a + 'q_linear.bias'), rot=rot, rot_cols=2 * d, rot_d=d, rot_seq=Sx)
+            q = qkv
+            qargs = dict(sq=3 * d, bq=Sx * 3 * d)
+            kt, vt, sk = qkv[:, d:], qkv[:, 2 * d:], 3 * d
+            st['qkv'] = qkv
+        rows_q = B * Lq
+        O = ws.get(tag + '.O', (rows_q, d))
+        lse = ws.get(tag + '.lse', (B, heads, Lq), f32)
+        K.attention(q, kt, vt, O, lse, B=B, H=heads, Lq=Lq, Lk=Sx, hd=hd, so=d, bo=Lq * d, sk=sk, sv=sk,
+                    bk=Sx * sk, bv=Sx * sk, key_pad=pad_k, causal=causal, **qargs)
+        st.update(O=O, lse=lse, Lq=Lq, pad_k=pad_k)
+        resid = Lq == Sx                           # transformer_layer.py:49
+        x1 = ws.get(tag + '.x1', (rows_q, d), f32)
+        K.gemm(O, P.w(a + 'output_linear.weight'), x1, rows_q, d, d, epi=EPI_F32, bias=P.f(a + 'output_linear.bias'),
+               resid=x if resid else None, ldr=d)
+        st['resid'] = resid
+        st['x1'] = x1
+        xc = x1
+        if cross:                                  # transformer_layer.py:51-54
+            c = pre + 'cross_attention.'
+            rows_c = B * L
+            cx, st['ln_ctx'] = self._ln_fwd(pre + 'context_layer_norm', ctx, rows_c, tag + '.ln_ctx')
+            hq, st['ln_cross'] = self._ln_fwd(pre + 'cross_attn_layer_norm', x1, rows_q, tag + '.ln_cross')
+            qc = ws.get(tag + '.qc', (rows_q, d))
+            K.gemm(hq, P.w(c + 'q_linear.weight'), qc, rows_q, d, d, epi=EPI_ROTARY_BF16, bias=P.f(c + 'q_linear.bias'),
+                   rot=rot, rot_cols=d, rot_d=d, rot_seq=Lq)
+            kvc = ws.get(tag + '.kvc', (rows_c, 2 * d))
+            K.gemm(cx, P.w(c + 'k_linear.weight'), kvc, rows_c, 2 * d, d, epi=EPI_ROTARY_BF16,
+                   bias=P.f(c + 'k_linear.bias'), rot=rot, rot_cols=d, rot_d=d, rot_seq=L)
+            Oc = ws.get(tag + '.Oc', (rows_q, d))
+            lsec = ws.get(tag + '.lsec', (B, heads, Lq), f32)
+            K.attention(qc, kvc, kvc[:, d:], Oc, lsec, B=B, H=heads, Lq=Lq, Lk=L, hd=hd, sq=d, bq=Lq * d, sk=2 * d,
+                        sv=2 * d, bk=L * 2 * d, bv=L * 2 * d, so=d, bo=Lq * d, key_pad=pad, causal=False)
+            x2 = ws.get(tag + '.x2', (rows_q, d), f32)
+            K.gemm(Oc, P.w(c + 'output_linear.weight'), x2, rows_q, d, d, epi=EPI_F32,
+                   bias=P.f(c + 'output_linear.bias'), resid=x1, ldr=d)
+            st.update(cx=cx, hq=hq, qc=qc, kvc=kvc, Oc=Oc, lsec=lsec, x2=x2, pad_ctx=pad)
+            xc = x2
+        h2, st['ln_f'] = self._ln_fwd(pre + 'ffn_layer_norm', xc, rows_q, tag + '.ln_f')
+        preact = ws.get(tag + '.pre', (rows_q, 4 * d))
+        f = ws.get(tag + '.f', (rows_q, 4 * d))
+        K.gemm(h2, P.w(pre + 'ffn.0.weight'), f, rows_q, 4 * d, d, epi=EPI_GELU, bias=P.f(pre + 'ffn.0.bias'),
+               aux=preact, ldaux=4 * d)
+        out = ws.get(tag + '.out', (rows_q, d), f32) if out is None else out
+        K.gemm(f, P.w(pre + 'ffn.2.weight'), out, rows_q, d, 4 * d, epi=EPI_DROPOUT_RESID, resid=xc, ldr=d,
+               drop_p=drop_p, seed=seed)
+        st.update(h2=h2, preact=preact, f=f, xc=xc, rows_q=rows_q)
+        return out, st
+
+    def layer_bwd(self, st, dout, dx_out, *, dx_accumulate=False, dctx=None):
+        """Backward of layer_fwd. dout f32 [B*Lq, d] (consumed as scratch). Writes d x into dx_out
+        (accumulating into it when dx_accumulate and the layer has no residual); cross-attention context
+        gradients accumulate into dctx."""
+        d, ws, P = self.d, self.ws, self.P
+        pre, B, Sx, L, Lq = st['pre'], st['B'], st['Sx'], st['L'], st['Lq']
+        heads, hd = st['heads'], st['hd']
+        rows_x, rows_q = B * Sx, st['rows_q']
+        rot = self.rot(max(Sx, L))
+        a = pre + 'attention.'
+        # ---- FFN (transformer_layer.py:56-61)
+        g2 = ws.get('b.g2', (rows_q, d))
+        K.dropout_bwd_cast(dout, g2, st['drop_p'], st['seed'], rows_q, d)
+        self._dw(g2, st['f'], pre + 'ffn.2.weight', rows_q, d, 4 * d)
+        dpre = ws.get('b.dpre', (rows_q, 4 * d))
+        K.gemm(g2, P.w(pre + 'ffn.2.weight'), dpre, rows_q, 4 * d, d, b_t=True, epi=EPI_GELU_BWD, aux=st['preact'],
+               ldaux=4 * d)
+        self._dw(dpre, st['h2'], pre + 'ffn.0.weight', rows_q, 4 * d, d)
+        self._db(dpre, pre + 'ffn.0.bias', rows_q, 4 * d)
+        dh2 = ws.get('b.dh2', (rows_q, d))
+        K.gemm(dpre, P.w(pre + 'ffn.0.weight'), dh2, rows_q, d, 4 * d, b_t=True, epi=EPI_BF16)
+        dxc = ws.get('b.dxc', (rows_q, d), f32)
+        gxc = ws.get('b.gxc', (rows_q, d))
+        self._ln_bwd(pre + 'ffn_layer_norm', dh2, st['ln_f'], rows_q, dout, dxc, gxc)
+        dx1, gx1 = dxc, gxc
+        if st['cross']:
+            c = pre + 'cross_attention.'
+            rows_c = B * L
+            self._dw(gxc, st['Oc'], c + 'output_linear.weight', rows_q, d, d)
+            self._db(gxc, c + 'output_linear.bias', rows_q, d)
+            dOc = ws.get('b.dO', (rows_q, d))
+            K.gemm(gxc, P.w(c + 'output_linear.weight'), dOc, rows_q, d, d, b_t=True, epi=EPI_BF16)
+            dq32 = ws.get('b.dq32', (rows_q, d), f32, zero=True)
+            dkvc = ws.get('b.dkvc', (rows_c, 2 * d))
+            delta = ws.get('b.delta', (B, heads, Lq), f32)
+            K.attention(st['qc'], st['kvc'], st['kvc'][:, d:], st['Oc'], st['lsec'], B=B, H=heads, Lq=Lq, Lk=L,
+                        hd=hd, sq=d, bq=Lq * d, sk=2 * d, sv=2 * d, bk=L * 2 * d, bv=L * 2 * d, so=d, bo=Lq * d,
+                        key_pad=st['pad_ctx'], causal=False, backward=True,
+                        dout=dOc, sdo=d, bdo=Lq * d, delta=delta, dq=dq32, bdq=Lq * d, dk=dkvc, dv=dkvc[:, d:],
+                        sdk=2 * d, sdv=2 * d, bdk=L * 2 * d, bdv=L * 2 * d, rot=rot, rot_d=d)
+            dqc = ws.get('b.dqc', (rows_q, d))
+            K.dq_finalize(dq32, dqc, d, rows_q, d, rot, Lq)
+            self._dw(dqc, st['hq'], c + 'q_linear.weight', rows_q, d, d)
+            self._db(dqc, c + 'q_linear.bias', rows_q, d)
+            dhq = ws.get('b.dhq', (rows_q, d))
+            K.gemm(dqc, P.w(c + 'q_linear.weight'), dhq, rows_q, d, d, b_t=True, epi=EPI_BF16)
+            self._dw(dkvc, st['cx'], c + 'k_linear.weight', rows_c, 2 * d, d)
+            self._db(dkvc, c + 'k_linear.bias', rows_c, 2 * d)
+            dcx = ws.get('b.dcx', (rows_c, d))
+            K.gemm(dkvc, P.w(c + 'k_linear.weight'), dcx, rows_c, d, 2 * d, b_t=True, epi=EPI_BF16)
+            dx1 = ws.get('b.dx1', (rows_q, d), f32)
+            gx1 = ws.get('b.gx1', (rows_q, d))
+            self._ln_bwd(pre + 'cross_attn_layer_norm', dhq, st['ln_cross'], rows_q, dxc, dx1, gx1)
+            self._ln_bwd(pre + 'context_layer_norm', dcx, st['ln_ctx'], rows_c, dctx, dctx)
+        # ---- self / learned-query attention (attention.py:51-105)
+        self._dw(gx1, st['O'], a + 'output_linear.weight', rows_q, d, d)
+        self._db(gx1, a + 'output_linear.bias', rows_q, d)
+        dO = ws.get('b.dO', (rows_q, d))
+        K.gemm(gx1, P.w(a + 'output_linear.weight'), dO, rows_q, d, d, b_t=True, epi=EPI_BF16)
+        delta = ws.get('b.delta', (B, heads, Lq), f32)
+        if st['learned']:
+            kv = st['kv']
+            dq32 = ws.get('b.dq32', (B * Lq, d), f32, zero=True)
+            dkv = ws.get('b.dkv', (rows_x, 2 * d))
+            K.attention(P.w(a + 'learned_queries').view(Lq, d), kv, kv[:, d:], st['O'], st['lse'], B=B, H=heads,
+                        Lq=Lq, Lk=Sx, hd=hd, sq=d, bq=0, sk=2 * d, sv=2 * d, bk=Sx * 2 * d, bv=Sx * 2 * d, so=d,
+                        bo=Lq * d, key_pad=st['pad_k'], causal=False, backward=True, dout=dO, sdo=d, bdo=Lq * d,
+                        delta=delta, dq=dq32, bdq=Lq * d, dk=dkv, dv=dkv[:, d:], sdk=2 * d, sdv=2 * d,
+                        bdk=Sx * 2 * d, bdv=Sx * 2 * d, rot=rot, rot_d=d)
+            K.colsum(dq32, B, Lq * d, Lq * d, P.g(a + 'learned_queries').view(-1))
+            self._dw(dkv, st['h'], a + 'k_linear.weight', rows_x, 2 * d, d)
+            self._db(dkv, a + 'k_linear.bias', rows_x, 2 * d)
+            dh = ws.get('b.dh', (rows_x, d))
+            K.gemm(dkv, P.w(a + 'k_linear.weight'), dh, rows_x, d, 2 * d, b_t=True, epi=EPI_BF16)
+        else:
+            qkv = st['qkv']
+            dq32 = ws.get('b.dq32', (rows_x, d), f32, zero=True)
+            dqkv = ws.get('b.dqkv', (rows_x, 3 * d))
+            K.attention(qkv, qkv[:, d:], qkv[:, 2 * d:], st['O'], st['lse'], B=B, H=heads, Lq=Lq, Lk=Sx, hd=hd,
+                        sq=3 * d, bq=Sx * 3 * d, sk=3 * d, sv=3 * d, bk=Sx * 3 * d, bv=Sx * 3 * d, so=d, bo=Lq * d,
+                        key_pad=st['pad_k'], causal=st['causal'], backward=True, dout=dO, sdo=d, bdo=Lq * d,
+                        delta=delta, dq=dq32, bdq=Sx * d, dk=dqkv[:, d:], dv=dqkv[:, 2 * d:], sdk=3 * d, sdv=3 * d,
+                        bdk=Sx * 3 * d, bdv=Sx * 3 * d, rot=rot, rot_d=d)
+            K.dq_finalize(dq32, dqkv, 3 * d, rows_x, d, rot, Sx)
+            self._dw(dqkv, st['h'], a + 'q_linear.weight', rows_x, 3 * d, d)
+            self._db(dqkv, a + 'q_linear.bias', rows_x, 3 * d)
+            dh = ws.get('b.dh', (rows_x, d))
+            K.gemm(dqkv, P.w(a + 'q_linear.weight'), dh, rows_x, d, 3 * d, b_t=True, epi=EPI_BF16)
+        if st['resid']:
+            self._ln_bwd(pre + 'attn_layer_norm', dh, st['ln_a'], rows_x, dx1, dx_out)
+            if dx_accumulate:
+                raise NotImplementedError('residual + accumulate is handled by the caller')
+        else:
+            self._ln_bwd(pre + 'attn_layer_norm', dh, st['ln_a'], rows_x, dx_out if dx_accumulate else None, dx_out)
+
+    # ------------------------------------------------------------------ full step
+    def forward(self, ids, ntok, *, pad=True, eps=None, seed=0, kl_weight=1.0, dropout=0.1, need_logits=False):
+        """TransformerVAE.training_step forward (transformer_vae.py:42-55). ids int [B, L] on the device."""
+        hp, d, ws, P = self.hp, self.d, self.ws, self.P
+        if not ids.is_cuda:
+            raise RuntimeError('VAEEngine needs device tensors (no CPU fallback)')
+        P.sync_shadow()
+        B, L = ids.shape
+        T, V, Z, N = B * L, hp.vocab_size, hp.latent_depth, hp.num_latents
+        ids32 = ws.get('ids', (B, L), torch.int32)
+        ids32.copy_(ids)
+        padm = None
+        if pad:
+            padm = ws.get('pad', (B, L), torch.uint8)
+            padm.copy_(ids.eq(0))
+        labels = ws.get('labels', (B, L), torch.int32)
+        labels[:, :-1].copy_(ids32[:, 1:])
+        labels[:, -1] = 0
+        ntok64 = ws.get('ntok', (B,), torch.int64)
+        ntok64.copy_(ntok)
+        sv = {'B': B, 'L': L, 'dropout': dropout, 'seed': seed}
+
+        x_emb = ws.get('x_emb', (T, d), f32)
+        K.embedding_fwd(ids32, P.f('input_layer.0.weight'), x_emb, T, d)
+
+        # ---- encoder (perceiver.py:39-50)
+        lay = []
+        z, st = self.layer_fwd('encoder.first_layer.', x_emb, B, L, L, padm, learned=N, heads=self.He, hd=64,
+                               drop_p=dropout, seed=_mix_seed(seed, 1000), tag='e0')
+        lay.append(st)
+        for j in range(hp.enc_layers - 2):
+            z, st = self.layer_fwd(f'encoder.middle_layers.{j}.', z, B, N, L, padm, cross=True, ctx=x_emb,
+                                   heads=self.He, hd=64, drop_p=dropout, seed=_mix_seed(seed, 1001 + j), tag=f'e{j + 1}')
+            lay.append(st)
+        enc, st = self.layer_fwd('encoder.bottleneck.', z, B, N, L, padm, learned=1, heads=self.He, hd=64,
+                                 drop_p=dropout, seed=_mix_seed(seed, 1999), tag='eb')
+        lay.append(st)
+        sv['enc_layers'] = lay
+
+        # ---- q(z|x) + reparameterise + KL (conditional_gaussian.py:18-28, continuous_autoencoder.py:42-52)
+        enc_bf = ws.get('enc_bf', (B, d))
+        K.cast_bf16(enc, enc_bf)
+        stats = ws.get('stats', (B, 2 * Z), f32)
+        K.gemm(enc_bf, P.w('q_of_z_given_x.linear.weight'), stats, B, 2 * Z, d, epi=EPI_F32,
+               bias=P.f('q_of_z_given_x.linear.bias'))
+        zf = ws.get('z', (B, Z), f32)
+        zb = ws.get('z_bf', (B, Z))
+        eps_buf = ws.get('eps', (B, Z), f32)
+        raw_kl = ws.get('raw_kl', (B,), f32)
+        kl = ws.get('kl', (2,), f32)
+        if eps is not None:
+            eps_buf.copy_(eps.reshape(B, Z))
+        K.reparam_fwd(stats, eps_buf if eps is not None else None, _mix_seed(seed, 7), ntok64, zf, zb, eps_buf,
+                      raw_kl, kl, B, Z)
+        sv.update(enc_bf=enc_bf, stats=stats, z_bf=zb, eps=eps_buf)
+
+        # ---- decoder (transformer_vae.py:85-93), position 0 replaced by z_projections[i](z) every layer
+        xs = ws.get('x_dec0', (T, d), f32)
+        xs.copy_(x_emb)
+        dec = []
+        for i in range(hp.num_layers):
+            K.gemm(zb, P.w(f'z_projections.{i}.weight'), xs, B, d, Z, ldc=L * d, epi=EPI_F32,
+                   bias=P.f(f'z_projections.{i}.bias'))
+            xs, st = self.layer_fwd(f'decoder_layers.{i}.', xs, B, L, L, padm, causal=True, heads=self.H,
+                                    hd=self.hd, drop_p=dropout, seed=_mix_seed(seed, i), tag=f'd{i}',
+                                    out=ws.get(f'x_dec{i + 1}', (T, d), f32))
+            dec.append(st)
+        sv['dec_layers'] = dec
+
+        # ---- output head + cross entropy (transformer_language_model.py:55-63, language_model.py:161-170)
+        xf = ws.get('xf_bf', (T, d))
+        K.cast_bf16(xs, xf)
+        pre0 = ws.get('h0_pre', (T, d))
+        h0 = ws.get('h0', (T, d))
+        K.gemm(xf, P.w('output_layer.0.weight'), h0, T, d, d, epi=EPI_GELU, bias=P.f('output_layer.0.bias'),
+               aux=pre0, ldaux=d)
+        hh, ln_h = self._ln_fwd('output_layer.2', h0, T, 'head.ln')
+        logits = ws.get('logits', (T, V))
+        ntile = -(-V // 128)
+        part = ws.get('ce.part', (T, ntile, 2), f32)
+        lab_logit = ws.get('ce.label_logit', (T,), f32)
+        K.gemm(hh, P.w('input_layer.0.weight'), logits, T, V, d, epi=EPI_CE_STATS, bias=P.f('output_layer.3.bias'),
+               aux=part, labels=labels, label_logit=lab_logit)
+        numel = B * (L - 1) * V
+        chunks = -(-numel // CE_CHUNK_NUMEL)
+        chunk_len = -(-(L - 1) // chunks)
+        nchunks = -(-(L - 1) // chunk_len)
+        lse = ws.get('ce.lse', (T,), f32)
+        row_loss = ws.get('ce.row_loss', (T,), f32)
+        chunk_w = ws.get('ce.chunk_w', (8,), f32)
+        nll = ws.get('nll', (1,), f32)
+        K.ce_finalize(part, ntile, lab_logit, labels, T, L, nchunks, chunk_len, lse, row_loss, chunk_w, nll)
+        sv.update(xf=xf, pre0=pre0, h0=h0, hh=hh, ln_h=ln_h, logits=logits, lse=lse, chunk_w=chunk_w,
+                  nchunks=nchunks, chunk_len=chunk_len, labels=labels, ids32=ids32, ntok=ntok64, x_emb=x_emb)
+        loss = nll[0] + kl_weight * kl[0]                                          # transformer_vae.py:55
+        self.saved = sv
+        return {'loss': loss, 'nll': nll[0], 'kl': kl[0], 'train_kl': kl[1], 'raw_kl': raw_kl,
+                'mu': stats[:, :Z], 'logvar': stats[:, Z:], 'z': zf, 'eps': eps_buf,
+                'logits': logits if need_logits else None}
+
+    def backward(self, gloss, kl_weight):
+        """Gradients of loss = nll + kl_weight * kl into the flat gradient arena (accumulating)."""
+        sv, hp, d, ws, P = self.saved, self.hp, self.d, self.ws, self.P
+        if sv is None:
+            raise RuntimeError('backward() without a saved forward')
+        B, L = sv['B'], sv['L']
+        T, V, Z, N = B * L, hp.vocab_size, hp.latent_depth, hp.num_latents
+        gs = ws.get('gscale', (2,), f32)
+        gs[0:1].copy_(gloss.reshape(1))
+        gs[1:2].copy_(gloss.reshape(1) * kl_weight)
+
+        # ---- head
+        logits = sv['logits']
+        K.ce_grad(logits, V, sv['lse'], sv['chunk_w'], sv['labels'], gs[0:1], T, V, L, sv['nchunks'], sv['chunk_len'])
+        self._dw(logits, sv['hh'], 'input_layer.0.weight', T, V, d)
+        self._db(logits, 'output_layer.3.bias', T, V)
+        dhh = ws.get('b.dhh', (T, d))
+        K.gemm(logits, P.w('input_layer.0.weight'), dhh, T, d, V, b_t=True, epi=EPI_BF16)
+        dh0 = ws.get('b.dh0', (T, d), f32)
+        self._ln_bwd('output_layer.2', dhh, sv['ln_h'], T, None, dh0)
+        dpre0 = ws.get('b.dpre0', (T, d))
+        K.gelu_bwd(dh0, sv['pre0'], dpre0, T * d)
+        self._dw(dpre0, sv['xf'], 'output_layer.0.weight', T, d, d)
+        self._db(dpre0, 'output_layer.0.bias', T, d)
+        dx = ws.get('b.dx_dec', (T, d), f32)
+        K.gemm(dpre0, P.w('output_layer.0.weight'), dx, T, d, d, b_t=True, epi=EPI_F32)
+
+        # ---- decoder layers, last to first
+        dz = ws.get('b.dz', (B, Z), f32, zero=True)
+        dzh = ws.get('b.dzh', (B, d), f32)
+        dzh_bf = ws.get('b.dzh_bf', (B, d))
+        dx_prev = ws.get('b.dx_prev', (T, d), f32)
+        for i in reversed(range(hp.num_layers)):
+            st = sv['dec_layers'][i]
+            self.layer_bwd(st, dx, dx_prev)
+            # position-0 splice: its gradient feeds z_projections[i]; earlier layers see zero there
+            K.extract_rows(dx_prev, d, T, L, d, dzh)
+            K.cast_bf16(dzh, dzh_bf)
+            self._dw(dzh_bf, sv['z_bf'], f'z_projections.{i}.weight', B, d, Z)
+            self._db(dzh, f'z_projections.{i}.bias', B, d)
+            K.gemm(dzh_bf, P.w(f'z_projections.{i}.weight'), dz, B, Z, d, b_t=True, epi=EPI_F32_ACC)
+            dx, dx_prev = dx_prev, dx
+        dx_emb = dx                                   # decoder part of d x_emb (rows 0 already zero)
+
+        # ---- reparameterise + q(z|x)
+        dstats = ws.get('b.dstats', (B, 2 * Z), f32)
+        K.reparam_bwd(sv['stats'], sv['eps'], dz, sv['ntok'], gs[1:2], dstats, B, Z)
+        dstats_bf = ws.get('b.dstats_bf', (B, 2 * Z))
+        K.cast_bf16(dstats, dstats_bf)
+        self._dw(dstats_bf, sv['enc_bf'], 'q_of_z_given_x.linear.weight', B, 2 * Z, d)
+        self._db(dstats, 'q_of_z_given_x.linear.bias', B, 2 * Z)
+        denc = ws.get('b.denc', (B, d), f32)
+        K.gemm(dstats_bf, P.w('q_of_z_given_x.linear.weight'), denc, B, d, 2 * Z, b_t=True, epi=EPI_F32)
+
+        # ---- encoder, bottleneck -> middle -> first
+        enc = sv['enc_layers']
+        dcur = denc
+        for k in reversed(range(1, len(enc))):
+            st = enc[k]
+            nxt = ws.get(f'b.denc{k}', (B * N, d), f32)
+            self.layer_bwd(st, dcur, nxt, dctx=dx_emb)
+            dcur = nxt
+        st0 = enc[0]
+        if st0['resid']:   # L == num_latents: the first layer keeps its residual (transformer_layer.py:49)
+            tmp = ws.get('b.dfirst', (T, d), f32)
+            self.layer_bwd(st0, dcur, tmp)
+            K.embedding_bwd(sv['ids32'], tmp, P.g('input_layer.0.weight'), T, d)
+        else:
+            self.layer_bwd(st0, dcur, dx_emb, dx_accumulate=True)
+
+        # ---- embedding (tied with the head weight)
+        K.embedding_bwd(sv['ids32'], dx_emb, P.g('input_layer.0.weight'), T, d)

@@ -1,0 +1,176 @@
+"""Typed wrappers over libsvae.so (include/svae.h). Tensor in, pointer out; every wrapper checks the
+arguments it relies on and raises on a non-zero status. All work is enqueued on torch's current HIP
+stream; nothing here synchronises."""
+import ctypes
+
+import torch
+
+from . import _native as N
+from ._native import lib, check, ptr, stream
+
+bf16, f32 = torch.bfloat16, torch.float32
+
+_gemm_desc = N.GemmDesc()
+
+
+def _dev(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError('libsvae kernels need device tensors (no CPU fallback)')
+
+
+def gemm(A, B, C, M, N_, K, *, a_t=False, b_t=False, lda=None, ldb=None, ldc=None, epi=N.EPI_BF16, bias=None,
+         resid=None, ldr=0, aux=None, ldaux=0, alpha=1.0, splits=1, drop_p=0.0, seed=0, rot=None, rot_cols=0,
+         rot_d=0, rot_seq=0, labels=None, label_logit=None, batch=1, sA=0, sB=0, sC=0):
+    """C = epi(alpha * A . B) with A [M,K] (a_t: stored [K,M]) and B [K,N] (b_t: stored [K,N], else [N,K])."""
+    _dev(A, B, C)
+    assert A.dtype == bf16 and B.dtype == bf16
+    d = _gemm_desc
+    d.A, d.B = A.data_ptr(), B.data_ptr()
+    d.lda = lda if lda is not None else (M if a_t else K)
+    d.ldb = ldb if ldb is not None else (N_ if b_t else K)
+    d.batch_stride_a, d.batch_stride_b = sA, sB
+    d.M, d.N, d.K = M, N_, K
+    d.batch, d.splits = batch, splits
+    d.a_t, d.b_t = int(a_t), int(b_t)
+    d.epi = epi
+    d.C = C.data_ptr()
+    d.ldc = ldc if ldc is not None else N_
+    d.batch_stride_c = sC
+    d.bias = ptr(bias)
+    d.resid = ptr(resid)
+    d.ldr = ldr
+    d.aux = ptr(aux)
+    d.ldaux = ldaux
+    d.alpha = alpha
+    d.drop_p = drop_p
+    d.seed = seed & 0xFFFFFFFFFFFFFFFF
+    d.rot_tab = ptr(rot)
+    d.rot_cols, d.rot_d, d.rot_seq = rot_cols, rot_d, rot_seq
+    d.labels = ptr(labels)
+    d.label_logit = ptr(label_logit)
+    check(lib.svae_gemm(ctypes.byref(d), stream()), 'svae_gemm')
+
+
+def auto_splits(M, N_, K, target=512):
+    tiles = -(-M // 128) * -(-N_ // 128)
+    if tiles >= 256 or K < 1024:
+        return 1
+    s = min(-(-target // tiles), K // 512)
+    return max(1, s)
+
+
+def linear_dw(dY, X, Wgrad, rows, n_out, n_in, ldy=None, ldx=None):
+    """Wgrad[n_out, n_in] += dY^T . X over `rows` rows (dY [rows, n_out] bf16, X [rows, n_in] bf16)."""
+    s = auto_splits(n_out, n_in, rows)
+    gemm(dY, X, Wgrad, n_out, n_in, rows, a_t=True, b_t=True, lda=ldy or n_out, ldb=ldx or n_in, ldc=n_in,
+         epi=N.EPI_F32_ATOMIC if s > 1 else N.EPI_F32_ACC, splits=s)
+
+
+def layernorm_fwd(x, w, b, y, mean, rstd, rows, D):
+    _dev(x, w, b, y, mean, rstd)
+    check(lib.svae_layernorm_fwd(x.data_ptr(), 0 if x.dtype == f32 else 1, w.data_ptr(), b.data_ptr(), y.data_ptr(),
+                                 mean.data_ptr(), rstd.data_ptr(), rows, D, stream()), 'svae_layernorm_fwd')
+
+
+def layernorm_bwd(dy, x, w, mean, rstd, dres, dx, dx_bf, wgrad2, rows, D, part_ws):
+    """dx = dres + LN'(dy); wgrad2 (the adjacent [weight | bias] grads, 2D floats) += sum of affine grads."""
+    nblk = lib.svae_layernorm_nblk(rows)
+    part = part_ws[: nblk * 2 * D]
+    check(lib.svae_layernorm_bwd(dy.data_ptr(), x.data_ptr(), 0 if x.dtype == f32 else 1, w.data_ptr(),
+                                 mean.data_ptr(), rstd.data_ptr(), ptr(dres), dx.data_ptr(), ptr(dx_bf),
+                                 part.data_ptr(), nblk, rows, D, 0, stream()), 'svae_layernorm_bwd')
+    colsum(part, nblk, 2 * D, 2 * D, wgrad2, accumulate=True)
+
+
+def colsum(inp, rows, cols, ld, out, accumulate=True):
+    check(lib.svae_colsum(inp.data_ptr(), 0 if inp.dtype == f32 else 1, rows, cols, ld, out.data_ptr(),
+                          int(accumulate), stream()), 'svae_colsum')
+
+
+_attn_desc = N.AttnDesc()
+
+
+def attention(q, k, v, o, lse, *, B, H, Lq, Lk, hd, sq, sk, sv, so, bq, bk, bv, bo, key_pad=None, causal=False,
+              scale=None, backward=False, dout=None, sdo=0, bdo=0, delta=None, dq=None, bdq=0, dk=None, dv=None,
+              sdk=0, sdv=0, bdk=0, bdv=0, rot=None, rot_d=0):
+    d = _attn_desc
+    d.q, d.k, d.v, d.o = q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr()
+    d.sq, d.sk, d.sv, d.so, d.bq, d.bk, d.bv, d.bo = sq, sk, sv, so, bq, bk, bv, bo
+    d.key_pad = ptr(key_pad)
+    d.lse = lse.data_ptr()
+    d.B, d.H, d.Lq, d.Lk, d.hd, d.causal = B, H, Lq, Lk, hd, int(causal)
+    d.scale = hd ** -0.5 if scale is None else scale
+    if backward:
+        d.dout, d.sdo, d.bdo = dout.data_ptr(), sdo, bdo
+        d.delta, d.dq, d.bdq = delta.data_ptr(), dq.data_ptr(), bdq
+        d.dk, d.dv, d.sdk, d.sdv, d.bdk, d.bdv = dk.data_ptr(), dv.data_ptr(), sdk, sdv, bdk, bdv
+        d.rot_tab, d.rot_d = ptr(rot), rot_d
+        check(lib.svae_attn_bwd(ctypes.byref(d), stream()), 'svae_attn_bwd')
+    else:
+        d.dout = None
+        check(lib.svae_attn_fwd(ctypes.byref(d), stream()), 'svae_attn_fwd')
+
+
+def dq_finalize(dq, out, ldo, rows, D, rot=None, seq=0):
+    check(lib.svae_dq_finalize(dq.data_ptr(), out.data_ptr(), ldo, rows, D, ptr(rot), seq, stream()),
+          'svae_dq_finalize')
+
+
+def embedding_fwd(ids, table, out, rows, D):
+    check(lib.svae_embedding_fwd(ids.data_ptr(), table.data_ptr(), out.data_ptr(), None, rows, D, stream()),
+          'svae_embedding_fwd')
+
+
+def embedding_bwd(ids, dout, dtable, rows, D):
+    check(lib.svae_embedding_bwd(ids.data_ptr(), dout.data_ptr(), dtable.data_ptr(), rows, D, stream()),
+          'svae_embedding_bwd')
+
+
+def reparam_fwd(stats, eps, seed, ntok, z, z_bf, eps_out, raw_kl, kl_out, B, Z):
+    check(lib.svae_reparam_kl_fwd(stats.data_ptr(), ptr(eps), seed & 0xFFFFFFFFFFFFFFFF, ntok.data_ptr(),
+                                  z.data_ptr(), ptr(z_bf), ptr(eps_out), raw_kl.data_ptr(), kl_out.data_ptr(), B, Z,
+                                  stream()), 'svae_reparam_kl_fwd')
+
+
+def reparam_bwd(stats, eps, dz, ntok, gkl, dstats, B, Z):
+    check(lib.svae_reparam_kl_bwd(stats.data_ptr(), eps.data_ptr(), ptr(dz), ntok.data_ptr(), gkl.data_ptr(),
+                                  dstats.data_ptr(), B, Z, stream()), 'svae_reparam_kl_bwd')
+
+
+def ce_finalize(part, ntile, label_logit, labels, rows, seq, nchunks, chunk_len, lse, row_loss, chunk_w, nll):
+    check(lib.svae_ce_finalize(part.data_ptr(), ntile, label_logit.data_ptr(), labels.data_ptr(), rows, seq,
+                               nchunks, chunk_len, lse.data_ptr(), row_loss.data_ptr(), chunk_w.data_ptr(),
+                               nll.data_ptr(), stream()), 'svae_ce_finalize')
+
+
+def ce_grad(logits, ld, lse, chunk_w, labels, gscale, rows, V, seq, nchunks, chunk_len):
+    check(lib.svae_ce_grad(logits.data_ptr(), ld, lse.data_ptr(), chunk_w.data_ptr(), labels.data_ptr(),
+                           gscale.data_ptr(), rows, V, seq, nchunks, chunk_len, stream()), 'svae_ce_grad')
+
+
+def dropout_bwd_cast(g, out, p, seed, rows, cols, ld_in=None):
+    check(lib.svae_dropout_bwd_cast(g.data_ptr(), out.data_ptr(), p, seed & 0xFFFFFFFFFFFFFFFF, rows * cols, cols,
+                                    ld_in or cols, stream()), 'svae_dropout_bwd_cast')
+
+
+def cast_bf16(x, out, n=None):
+    check(lib.svae_cast_bf16(x.data_ptr(), out.data_ptr(), n if n is not None else x.numel(), stream()),
+          'svae_cast_bf16')
+
+
+def gelu_bwd(dx, pre, out, n):
+    check(lib.svae_gelu_bwd(dx.data_ptr(), pre.data_ptr(), out.data_ptr(), n, stream()), 'svae_gelu_bwd')
+
+
+def extract_rows(x, ld, rows, mod, D, out):
+    check(lib.svae_extract_rows(x.data_ptr(), ld, rows, mod, D, out.data_ptr(), stream()), 'svae_extract_rows')
+
+
+def sumsq(g, n, part):
+    check(lib.svae_sumsq(g.data_ptr(), n, part.data_ptr(), part.numel(), stream()), 'svae_sumsq')
+
+
+def radam(p, pbf, g, m, v, n, part, scal, norm_out):
+    check(lib.svae_radam(p.data_ptr(), ptr(pbf), g.data_ptr(), m.data_ptr(), v.data_ptr(), n, part.data_ptr(),
+                         part.numel(), scal.data_ptr(), ptr(norm_out), stream()), 'svae_radam')

@@ -1,0 +1,64 @@
+"""Full training-step parity: the HIP engine (bf16 MFMA path) against the CPU fp32 oracle on the same seeded
+weights, tokens and injected noise (dropout off). The oracle is pinned to the reference by
+tests/test_oracle_golden.py. Tolerances: loss/ELBO 1e-3 rel (BASELINE.json north_star), KL and mu/logvar
+(kept f32 on the device) 2e-3 rel, gradients by cosine similarity and norm ratio per parameter."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+import oracle  # noqa: E402
+from golden_util import setup  # noqa: E402
+
+if torch.cuda.is_available():
+    from sparse_vae.engine import FlatParams, VAEEngine
+
+
+def _build(hp, params):
+    flat = FlatParams(hp, 'cuda')
+    for name in flat.offsets:
+        flat.view(name).copy_(params[name])
+    return flat, VAEEngine(hp, flat)
+
+
+@pytest.mark.parametrize('name', ['tiny_pad', 'small6_pad', 'hd96', 'c2shape'])
+def test_step_matches_oracle(name):
+    torch.set_num_threads(min(16, os.cpu_count()))
+    g, hp, params, ids = setup(name)
+    ntok = torch.from_numpy(g['lens'])
+    eps = torch.from_numpy(g['eps'])
+    kw = float(g['kl_weight'])
+    p = {k: v.clone().requires_grad_(True) for k, v in params.items()}
+    ref = oracle.training_step(p, hp, ids, ntok, eps, kl_weight=kw)
+    ref['loss'].backward()
+
+    flat, eng = _build(hp, params)
+    out = eng.forward(ids.cuda(), ntok.cuda(), eps=eps.cuda(), dropout=0.0, kl_weight=kw)
+    flat.grad.zero_()
+    eng.backward(torch.ones((), device='cuda'), kw)
+    torch.cuda.synchronize()
+
+    loss, nll, kl = out['loss'].item(), out['nll'].item(), out['kl'].item()
+    elbo_ref = -(ref['nll'].item() + ref['kl'].item())
+    assert abs(loss - ref['loss'].item()) / abs(ref['loss'].item()) < 1e-3
+    assert abs(-(nll + kl) - elbo_ref) / abs(elbo_ref) < 1e-3
+    assert abs(kl - ref['kl'].item()) / abs(ref['kl'].item()) < 2e-2
+    mu = out['mu'].cpu()
+    assert ((mu - ref['mu'].detach().view_as(mu)).norm() / ref['mu'].detach().norm()).item() < 2e-2
+
+    worst = []
+    for n in flat.live_names:
+        gr = p[n].grad
+        assert gr is not None, n
+        gg = flat.g(n).cpu().double().flatten()
+        gr = gr.double().flatten()
+        cos = (gg @ gr / (gg.norm() * gr.norm() + 1e-30)).item()
+        ratio = (gg.norm() / (gr.norm() + 1e-30)).item()
+        worst.append((cos, ratio, n))
+    worst.sort()
+    msg = '\n'.join(f'{c:.5f} {r:.4f} {n}' for c, r, n in worst[:8])
+    assert worst[0][0] > 0.98, msg
+    assert all(0.95 < r < 1.05 for _, r, _ in worst), msg

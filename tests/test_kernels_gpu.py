@@ -1,0 +1,301 @@
+"""Per-kernel numerics of libsvae.so against plain PyTorch fp32 references of the same ops (GPU only)."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+if torch.cuda.is_available():
+    from sparse_vae import kernels as K
+    from sparse_vae import _native as N
+    from sparse_vae.engine import rotary_table
+    import oracle
+
+dev = 'cuda'
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-30)).item()
+
+
+@pytest.mark.parametrize('M,Nn,Kk', [(128, 128, 64), (200, 136, 72), (512, 384, 1024), (64, 1536, 512)])
+@pytest.mark.parametrize('a_t,b_t', [(0, 0), (0, 1), (1, 1), (1, 0)])
+def test_gemm_layouts_exact(M, Nn, Kk, a_t, b_t):
+    g = torch.Generator(device=dev).manual_seed(M + Nn + Kk)
+    A = torch.randint(-3, 4, (M, Kk), device=dev, generator=g).float()
+    B = torch.randint(-3, 4, (Kk, Nn), device=dev, generator=g).float()
+    As = (A.t() if a_t else A).contiguous().bfloat16()
+    Bs = (B if b_t else B.t()).contiguous().bfloat16()
+    C = torch.zeros(M, Nn, device=dev)
+    K.gemm(As, Bs, C, M, Nn, Kk, a_t=bool(a_t), b_t=bool(b_t), epi=N.EPI_F32)
+    torch.cuda.synchronize()
+    assert torch.equal(C, A @ B)
+
+
+def test_gemm_split_k_atomic_and_acc():
+    A = torch.randint(-2, 3, (4096, 256), device=dev).float()
+    B = torch.randint(-2, 3, (4096, 384), device=dev).float()
+    C = torch.ones(256, 384, device=dev)
+    K.gemm(A.bfloat16(), B.bfloat16(), C, 256, 384, 4096, a_t=True, b_t=True, epi=N.EPI_F32_ATOMIC, splits=4)
+    assert torch.equal(C, 1 + A.t() @ B)
+    K.gemm(A.bfloat16(), B.bfloat16(), C, 256, 384, 4096, a_t=True, b_t=True, epi=N.EPI_F32_ACC)
+    assert torch.equal(C, 1 + 2 * (A.t() @ B))
+
+
+def test_gemm_epilogues():
+    torch.manual_seed(0)
+    M, Nn, Kk = 300, 256, 192
+    X = torch.randn(M, Kk, device=dev).bfloat16()
+    W = (torch.randn(Nn, Kk, device=dev) * 0.1).bfloat16()
+    b = torch.randn(Nn, device=dev)
+    ref = X.float() @ W.float().t() + b
+    C = torch.empty(M, Nn, device=dev, dtype=torch.bfloat16)
+    K.gemm(X, W, C, M, Nn, Kk, epi=N.EPI_BF16, bias=b)
+    assert _rel(C, ref) < 4e-3
+    # GELU
+    pre = torch.empty_like(C)
+    K.gemm(X, W, C, M, Nn, Kk, epi=N.EPI_GELU, bias=b, aux=pre, ldaux=Nn)
+    assert _rel(pre, ref) < 4e-3 and _rel(C, F.gelu(ref)) < 4e-3
+    # GELU backward: C = acc * gelu'(pre)
+    G = torch.empty_like(C)
+    K.gemm(X, W, G, M, Nn, Kk, epi=N.EPI_GELU_BWD, aux=pre, ldaux=Nn)
+    p = pre.float().requires_grad_()
+    F.gelu(p).backward(X.float() @ W.float().t())
+    assert _rel(G, p.grad) < 5e-3
+    # residual f32
+    R = torch.randn(M, Nn, device=dev)
+    C32 = torch.empty(M, Nn, device=dev)
+    K.gemm(X, W, C32, M, Nn, Kk, epi=N.EPI_F32, bias=b, resid=R, ldr=Nn)
+    assert _rel(C32, ref + R) < 1e-5
+    # dropout + residual: kept fraction ~ 0.9, kept values scaled by 1/0.9
+    K.gemm(X, W, C32, M, Nn, Kk, epi=N.EPI_DROPOUT_RESID, resid=R, ldr=Nn, drop_p=0.1, seed=123)
+    acc = X.float() @ W.float().t()
+    keep = (C32 - R).abs() > 1e-6
+    assert 0.87 < keep.float().mean().item() < 0.93
+    assert _rel((C32 - R)[keep], (acc / 0.9)[keep]) < 1e-5
+    # the backward cast regenerates the same mask
+    gb = torch.empty(M, Nn, device=dev, dtype=torch.bfloat16)
+    K.dropout_bwd_cast(torch.ones(M, Nn, device=dev), gb, 0.1, 123, M, Nn)
+    agree = ((gb.float() != 0) == keep) | (acc.abs() < 1e-4)
+    assert agree.all()
+
+
+def test_gemm_rotary_matches_reference_rotation():
+    torch.manual_seed(1)
+    B, L, d = 2, 96, 256
+    X = torch.randn(B * L, d, device=dev).bfloat16()
+    W = (torch.randn(3 * d, d, device=dev) * 0.05).bfloat16()
+    b = torch.randn(3 * d, device=dev) * 0.1
+    rot = rotary_table(L, d).to(dev)
+    C = torch.empty(B * L, 3 * d, device=dev, dtype=torch.bfloat16)
+    K.gemm(X, W, C, B * L, 3 * d, d, epi=N.EPI_ROTARY_BF16, bias=b, rot=rot, rot_cols=2 * d, rot_d=d, rot_seq=L)
+    y = (X.float() @ W.float().t() + b).view(B, L, 3 * d).cpu()
+    ref = torch.cat([oracle.rotary(y[..., :d]), oracle.rotary(y[..., d:2 * d]), y[..., 2 * d:]], -1)
+    assert _rel(C.view(B, L, 3 * d).cpu(), ref) < 4e-3
+
+
+def test_ce_stats_epilogue_and_finalize():
+    torch.manual_seed(2)
+    T, d, V, L = 256, 128, 32768, 128
+    X = torch.randn(T, d, device=dev).bfloat16()
+    W = (torch.randn(V, d, device=dev) * 0.1).bfloat16()
+    b = torch.randn(V, device=dev) * 0.1
+    labels = torch.randint(0, V, (T,), device=dev, dtype=torch.int32)
+    labels[::7] = 0
+    logits = torch.empty(T, V, device=dev, dtype=torch.bfloat16)
+    ntile = V // 128
+    part = torch.empty(T, ntile, 2, device=dev)
+    ll = torch.zeros(T, device=dev)
+    K.gemm(X, W, logits, T, V, d, epi=N.EPI_CE_STATS, bias=b, aux=part, labels=labels, label_logit=ll)
+    ref = X.float() @ W.float().t() + b
+    lse, rl, cw, nll = (torch.empty(T, device=dev), torch.empty(T, device=dev), torch.empty(8, device=dev),
+                        torch.empty(1, device=dev))
+    K.ce_finalize(part, ntile, ll, labels, T, L, 1, L, lse, rl, cw, nll)
+    assert _rel(lse, ref.logsumexp(-1)) < 1e-6
+    nll_ref = F.cross_entropy(ref, labels.long(), ignore_index=0)
+    assert abs(nll.item() - nll_ref.item()) / nll_ref.item() < 1e-5
+    gs = torch.ones(1, device=dev)
+    K.ce_grad(logits, V, lse, cw, labels, gs, T, V, L, 1, L)
+    r = ref.clone().requires_grad_()
+    F.cross_entropy(r, labels.long(), ignore_index=0).backward()
+    assert _rel(logits, r.grad) < 1e-2
+
+
+@pytest.mark.parametrize('D,xdt', [(128, torch.float32), (384, torch.float32), (512, torch.bfloat16), (768, torch.float32)])
+def test_layernorm(D, xdt):
+    torch.manual_seed(D)
+    rows = 333
+    x = (torch.randn(rows, D, device=dev) * 2 + 0.5).to(xdt)
+    w = torch.randn(D, device=dev) * 0.1 + 1
+    bb = torch.randn(D, device=dev) * 0.1
+    y = torch.empty(rows, D, device=dev, dtype=torch.bfloat16)
+    mean, rstd = torch.empty(rows, device=dev), torch.empty(rows, device=dev)
+    K.layernorm_fwd(x, w, bb, y, mean, rstd, rows, D)
+    xr = x.float().requires_grad_()
+    wr, br = w.clone().requires_grad_(), bb.clone().requires_grad_()
+    ref = F.layer_norm(xr, (D,), wr, br, 1e-5)
+    assert _rel(y, ref) < 4e-3
+    dy = torch.randn(rows, D, device=dev).bfloat16()
+    ref.backward(dy.float())
+    dres = torch.randn(rows, D, device=dev)
+    dx = torch.empty(rows, D, device=dev)
+    dxb = torch.empty(rows, D, device=dev, dtype=torch.bfloat16)
+    wg = torch.zeros(2 * D, device=dev)
+    part = torch.empty(1024 * 2 * D, device=dev)
+    K.layernorm_bwd(dy, x, w, mean, rstd, dres, dx, dxb, wg, rows, D, part)
+    assert _rel(dx, xr.grad + dres) < 1e-4
+    assert _rel(dxb, xr.grad + dres) < 4e-3
+    assert _rel(wg[:D], wr.grad) < 1e-4 and _rel(wg[D:], br.grad) < 1e-4
+
+
+def _attn_ref(q, k, v, pad, causal, scale):
+    s = q @ k.transpose(-1, -2) * scale
+    mask = None
+    if pad is not None:
+        mask = pad[:, None, None, :].bool()
+    if causal:
+        cm = torch.ones(q.shape[-2], k.shape[-2], device=q.device, dtype=torch.bool).triu(1)
+        mask = cm if mask is None else mask | cm
+    if mask is not None:
+        s = s - mask * 1e7
+    return s.softmax(-1) @ v
+
+
+@pytest.mark.parametrize('B,H,Lq,Lk,hd,causal,padded,learned', [
+    (2, 4, 128, 128, 64, True, True, False),
+    (2, 2, 192, 192, 64, True, False, False),
+    (2, 3, 64, 200, 64, False, True, True),
+    (3, 2, 1, 64, 64, False, False, True),
+    (2, 2, 96, 96, 96, True, True, False),
+    (1, 2, 130, 130, 32, True, False, False),
+    (2, 8, 64, 64, 16, False, False, False),
+])
+def test_attention_fwd_bwd(B, H, Lq, Lk, hd, causal, padded, learned):
+    torch.manual_seed(Lq * 7 + hd)
+    d = H * hd
+    q = torch.randn(1 if learned else B, Lq, d, device=dev).bfloat16()
+    k = torch.randn(B, Lk, d, device=dev).bfloat16()
+    v = torch.randn(B, Lk, d, device=dev).bfloat16()
+    pad = None
+    if padded:
+        pad = torch.zeros(B, Lk, device=dev, dtype=torch.uint8)
+        for b in range(B):
+            pad[b, Lk - 1 - 17 * b - 5:] = 1
+    o = torch.empty(B, Lq, d, device=dev, dtype=torch.bfloat16)
+    lse = torch.empty(B, H, Lq, device=dev)
+    scale = hd ** -0.5
+    common = dict(B=B, H=H, Lq=Lq, Lk=Lk, hd=hd, sq=d, bq=0 if learned else Lq * d, sk=d, sv=d, bk=Lk * d,
+                  bv=Lk * d, so=d, bo=Lq * d, key_pad=pad, causal=causal)
+    K.attention(q, k, v, o, lse, **common)
+
+    def heads(t):
+        return t.float().view(t.shape[0], t.shape[1], H, hd).transpose(1, 2)
+
+    qr = heads(q).expand(B, -1, -1, -1).clone().requires_grad_()
+    kr, vr = heads(k).requires_grad_(), heads(v).requires_grad_()
+    ref = _attn_ref(qr, kr, vr, pad, causal, scale)
+    ref_o = ref.transpose(1, 2).reshape(B, Lq, d)
+    assert _rel(o, ref_o) < 1e-2
+    do = torch.randn(B, Lq, d, device=dev).bfloat16()
+    ref_o.backward(do.float())
+    dq = torch.zeros(B, Lq, d, device=dev)
+    dk = torch.empty(B, Lk, d, device=dev, dtype=torch.bfloat16)
+    dv = torch.empty_like(dk)
+    delta = torch.empty(B, H, Lq, device=dev)
+    K.attention(q, k, v, o, lse, backward=True, dout=do, sdo=d, bdo=Lq * d, delta=delta, dq=dq, bdq=Lq * d,
+                dk=dk, dv=dv, sdk=d, sdv=d, bdk=Lk * d, bdv=Lk * d, **common)
+
+    def unheads(t):
+        return t.transpose(1, 2).reshape(t.shape[0], t.shape[2], d)
+
+    assert _rel(dq, unheads(qr.grad)) < 2e-2
+    assert _rel(dk, unheads(kr.grad)) < 2e-2
+    assert _rel(dv, unheads(vr.grad)) < 2e-2
+
+
+def test_attention_bwd_inverse_rotary_and_dq_finalize():
+    torch.manual_seed(5)
+    B, H, L, hd = 2, 2, 64, 64
+    d = H * hd
+    rot = rotary_table(L, d).to(dev)
+    g = torch.randn(B * L, d, device=dev)
+    out = torch.empty(B * L, d, device=dev, dtype=torch.bfloat16)
+    K.dq_finalize(g, out, d, B * L, d, rot, L)
+    # inverse rotary = gradient of the rotary map
+    x = torch.randn(B, L, d).requires_grad_()
+    oracle.rotary(x).backward(g.view(B, L, d).cpu())
+    assert _rel(out.view(B, L, d).cpu(), x.grad) < 4e-3
+
+
+def test_embedding_and_reparam():
+    torch.manual_seed(6)
+    V, D, T = 1000, 128, 300
+    table = torch.randn(V, D, device=dev)
+    ids = torch.randint(0, V, (T,), device=dev, dtype=torch.int32)
+    out = torch.empty(T, D, device=dev)
+    K.embedding_fwd(ids, table, out, T, D)
+    assert torch.equal(out, table[ids.long()])
+    dt = torch.zeros(V, D, device=dev)
+    g = torch.randn(T, D, device=dev)
+    K.embedding_bwd(ids, g, dt, T, D)
+    ref = torch.zeros(V, D, device=dev).index_add_(0, ids.long(), g)
+    assert _rel(dt, ref) < 1e-6
+    B, Z = 5, 64
+    stats = torch.randn(B, 2 * Z, device=dev) * 0.5
+    eps = torch.randn(B, Z, device=dev)
+    ntok = torch.tensor([100, 90, 80, 70, 60], device=dev)
+    z, zb, eo, raw, kl = (torch.empty(B, Z, device=dev), torch.empty(B, Z, device=dev, dtype=torch.bfloat16),
+                          torch.empty(B, Z, device=dev), torch.empty(B, device=dev), torch.empty(2, device=dev))
+    K.reparam_fwd(stats, eps, 0, ntok, z, zb, eo, raw, kl, B, Z)
+    s = stats.clone().requires_grad_()
+    mu, lv = s[:, :Z], s[:, Z:]
+    var = lv.exp()
+    zr = mu + eps * var.sqrt()
+    klr = 0.5 * (mu ** 2 + var - lv - 1.0)
+    rawr = klr.sum(-1)
+    assert _rel(z, zr) < 1e-6 and _rel(raw, rawr) < 1e-5
+    assert abs(kl[0].item() - (rawr / ntok).mean().item()) < 1e-5 * abs(kl[0].item()) + 1e-7
+    dz = torch.randn(B, Z, device=dev)
+    (zr * dz).sum().add((rawr / ntok).mean() * 0.7).backward()
+    gkl = torch.tensor([0.7], device=dev)
+    ds = torch.empty(B, 2 * Z, device=dev)
+    K.reparam_bwd(stats, eps, dz, ntok, gkl, ds, B, Z)
+    assert _rel(ds, s.grad) < 1e-5
+    # in-kernel noise: standard normal moments
+    K.reparam_fwd(torch.zeros(64, 2 * Z, device=dev), None, 99, torch.ones(64, device=dev, dtype=torch.int64),
+                  torch.empty(64, Z, device=dev), None, eo := torch.empty(64, Z, device=dev), torch.empty(64, device=dev),
+                  torch.empty(2, device=dev), 64, Z)
+    assert abs(eo.mean().item()) < 0.05 and abs(eo.std().item() - 1) < 0.05
+
+
+def test_radam_kernel_matches_oracle():
+    torch.manual_seed(7)
+    n = 10000
+    p = torch.randn(n, device=dev)
+    m, v = torch.zeros(n, device=dev), torch.zeros(n, device=dev)
+    pbf = torch.empty(n, device=dev, dtype=torch.bfloat16)
+    st = oracle.RAdamState()
+    ref = {'p': p.cpu().clone()}
+    part = torch.empty(64, device=dev)
+    norm = torch.empty(1, device=dev)
+    for s in range(7):
+        g = torch.randn(n, device=dev) * 3
+        lr, b1, b2, eps, wd, max_norm = 1e-2, 0.9, 0.999, 1e-6, 0.01, 150.0
+        step = st.step
+        b2t = b2 ** step
+        bcv = (1 - b2t) ** 0.5
+        rho_inf = 2 / (1 - b2) - 1
+        rho = rho_inf - 2 * step * b2t / (1 - b2t)
+        lr_eff = lr
+        if rho > 4:
+            lr_eff = lr * (((rho - 4) * (rho - 2) * rho_inf) / ((rho_inf - 4) * (rho_inf - 2) * rho)) ** 0.5 * bcv
+        scal = torch.tensor([lr_eff, 1 - b1 ** step, bcv, float(rho > 4), b1, b2, eps, wd, max_norm], device=dev)
+        K.sumsq(g, n, part)
+        K.radam(p, pbf, g, m, v, n, part, scal, norm)
+        total, (gc,) = oracle.clip_grad_norm([g.cpu()], max_norm)
+        ref = oracle.radam_step(ref, {'p': gc}, st, lr=lr, weight_decay=wd)
+        assert abs(norm.item() - total.item()) / total.item() < 1e-5
+        assert _rel(p, ref['p'].to(dev)) < 1e-6
+    assert torch.equal(pbf, p.bfloat16())
