@@ -110,6 +110,10 @@ typedef struct svae_attn_desc {
   int64_t sdk, sdv, bdk, bdv;
   const float* rot_tab;     /* inverse rotary applied to dk when non-NULL ([Lk][d/2] (cos, sin)) */
   int32_t rot_d;
+  /* optional f32 copy of O (forward writes it, backward's delta = rowsum(dO . O) reads it): keeps delta
+     free of the bf16 rounding of O, which otherwise cancels badly when the keys are nearly alike */
+  float* o32;
+  int64_t so32, bo32;
 } svae_attn_desc;
 
 int svae_attn_fwd(const svae_attn_desc* d, svae_stream_t stream);

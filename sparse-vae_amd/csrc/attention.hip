@@ -32,6 +32,7 @@ struct AP {
   float* dq; long long bdq;
   bf16* dk; bf16* dv; long long sdk, sdv, bdk, bdv;
   const float* rot; int rot_d;
+  float* o32; long long so32, bo32;
 };
 
 // [64 rows][HDP] bf16 tile in LDS, 16-B chunks XOR-swizzled by (row & (chunks-1)): conflict-free for the
@@ -199,6 +200,8 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AP p) {
       const int d = 16 * t + 4 * g;
       if (d < p.hd) {
         *(bf16x4*)(O + d) = (bf16x4){f2bf(o[t][0] * inv), f2bf(o[t][1] * inv), f2bf(o[t][2] * inv), f2bf(o[t][3] * inv)};
+        if (p.o32)
+          *(f32x4*)(p.o32 + b * p.bo32 + (long long)h * p.hd + (long long)qrow * p.so32 + d) = o[t] * inv;
       }
     }
     if (g == 0) p.lse[((long long)b * p.H + h) * p.Lq + qrow] = m + __logf(lsum);
@@ -213,13 +216,23 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(AP p) {
   const int total = p.B * p.Lq * p.H;
   if (gid >= total) return;
   const int h = gid % p.H, q = (gid / p.H) % p.Lq, b = gid / (p.H * p.Lq);
-  const bf16* O = p.o + b * p.bo + (long long)q * p.so + (long long)h * p.hd;
   const bf16* dO = p.dout + b * p.bdo + (long long)q * p.sdo + (long long)h * p.hd;
   float s = 0.f;
-  for (int d = li * 8; d < p.hd; d += 128) {
-    const bf16x8 a = *(const bf16x8*)(O + d), c = *(const bf16x8*)(dO + d);
+  if (p.o32) {
+    const float* O = p.o32 + b * p.bo32 + (long long)q * p.so32 + (long long)h * p.hd;
+    for (int d = li * 8; d < p.hd; d += 128) {
+      const bf16x8 c = *(const bf16x8*)(dO + d);
+      const f32x4 a0 = *(const f32x4*)(O + d), a1 = *(const f32x4*)(O + d + 4);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) s += (float)a[e] * (float)c[e];
+      for (int e = 0; e < 4; ++e) s += a0[e] * (float)c[e] + a1[e] * (float)c[e + 4];
+    }
+  } else {
+    const bf16* O = p.o + b * p.bo + (long long)q * p.so + (long long)h * p.hd;
+    for (int d = li * 8; d < p.hd; d += 128) {
+      const bf16x8 a = *(const bf16x8*)(O + d), c = *(const bf16x8*)(dO + d);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s += (float)a[e] * (float)c[e];
+    }
   }
 #pragma unroll
   for (int o = 8; o > 0; o >>= 1) s += __shfl_xor(s, o, 16);
@@ -409,6 +422,8 @@ bool fill(const svae_attn_desc* d, AP& p) {
   p.delta = d->delta; p.dq = d->dq; p.bdq = d->bdq;
   p.dk = (bf16*)d->dk; p.dv = (bf16*)d->dv; p.sdk = d->sdk; p.sdv = d->sdv; p.bdk = d->bdk; p.bdv = d->bdv;
   p.rot = d->rot_tab; p.rot_d = d->rot_d;
+  p.o32 = d->o32; p.so32 = d->so32; p.bo32 = d->bo32;
+  if (p.o32 && ((p.so32 | p.bo32) % 4)) return false;
   return true;
 }
 

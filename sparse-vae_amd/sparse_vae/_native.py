@@ -51,6 +51,7 @@ class AttnDesc(ctypes.Structure):
         ('dk', c_void_p), ('dv', c_void_p),
         ('sdk', c_int64), ('sdv', c_int64), ('bdk', c_int64), ('bdv', c_int64),
         ('rot_tab', c_void_p), ('rot_d', c_int32),
+        ('o32', c_void_p), ('so32', c_int64), ('bo32', c_int64),
     ]
 
 

@@ -234,10 +234,11 @@ class VAEEngine:
             st['qkv'] = qkv
         rows_q = B * Lq
         O = ws.get(tag + '.O', (rows_q, d))
+        O32 = ws.get(tag + '.O32', (rows_q, d), f32)
         lse = ws.get(tag + '.lse', (B, heads, Lq), f32)
         K.attention(q, kt, vt, O, lse, B=B, H=heads, Lq=Lq, Lk=Sx, hd=hd, so=d, bo=Lq * d, sk=sk, sv=sk,
-                    bk=Sx * sk, bv=Sx * sk, key_pad=pad_k, causal=causal, **qargs)
-        st.update(O=O, lse=lse, Lq=Lq, pad_k=pad_k)
+                    bk=Sx * sk, bv=Sx * sk, key_pad=pad_k, causal=causal, o32=O32, so32=d, bo32=Lq * d, **qargs)
+        st.update(O=O, O32=O32, lse=lse, Lq=Lq, pad_k=pad_k)
         resid = Lq == Sx                           # transformer_layer.py:49
         x1 = ws.get(tag + '.x1', (rows_q, d), f32)
         K.gemm(O, P.w(a + 'output_linear.weight'), x1, rows_q, d, d, epi=EPI_F32, bias=P.f(a + 'output_linear.bias'),
@@ -257,9 +258,12 @@ class VAEEngine:
             K.gemm(cx, P.w(c + 'k_linear.weight'), kvc, rows_c, 2 * d, d, epi=EPI_ROTARY_BF16,
                    bias=P.f(c + 'k_linear.bias'), rot=rot, rot_cols=d, rot_d=d, rot_seq=L)
             Oc = ws.get(tag + '.Oc', (rows_q, d))
+            Oc32 = ws.get(tag + '.Oc32', (rows_q, d), f32)
             lsec = ws.get(tag + '.lsec', (B, heads, Lq), f32)
             K.attention(qc, kvc, kvc[:, d:], Oc, lsec, B=B, H=heads, Lq=Lq, Lk=L, hd=hd, sq=d, bq=Lq * d, sk=2 * d,
-                        sv=2 * d, bk=L * 2 * d, bv=L * 2 * d, so=d, bo=Lq * d, key_pad=pad, causal=False)
+                        sv=2 * d, bk=L * 2 * d, bv=L * 2 * d, so=d, bo=Lq * d, key_pad=pad, causal=False, o32=Oc32,
+                        so32=d, bo32=Lq * d)
+            st['Oc32'] = Oc32
             x2 = ws.get(tag + '.x2', (rows_q, d), f32)
             K.gemm(Oc, P.w(c + 'output_linear.weight'), x2, rows_q, d, d, epi=EPI_F32,
                    bias=P.f(c + 'output_linear.bias'), resid=x1, ldr=d)
@@ -315,7 +319,8 @@ class VAEEngine:
                         hd=hd, sq=d, bq=Lq * d, sk=2 * d, sv=2 * d, bk=L * 2 * d, bv=L * 2 * d, so=d, bo=Lq * d,
                         key_pad=st['pad_ctx'], causal=False, backward=True,
                         dout=dOc, sdo=d, bdo=Lq * d, delta=delta, dq=dq32, bdq=Lq * d, dk=dkvc, dv=dkvc[:, d:],
-                        sdk=2 * d, sdv=2 * d, bdk=L * 2 * d, bdv=L * 2 * d, rot=rot, rot_d=d)
+                        sdk=2 * d, sdv=2 * d, bdk=L * 2 * d, bdv=L * 2 * d, rot=rot, rot_d=d, o32=st['Oc32'],
+                        so32=d, bo32=Lq * d)
             dqc = ws.get('b.dqc', (rows_q, d))
             K.dq_finalize(dq32, dqc, d, rows_q, d, rot, Lq)
             self._dw(dqc, st['hq'], c + 'q_linear.weight', rows_q, d, d)
@@ -344,7 +349,7 @@ class VAEEngine:
                         Lq=Lq, Lk=Sx, hd=hd, sq=d, bq=0, sk=2 * d, sv=2 * d, bk=Sx * 2 * d, bv=Sx * 2 * d, so=d,
                         bo=Lq * d, key_pad=st['pad_k'], causal=False, backward=True, dout=dO, sdo=d, bdo=Lq * d,
                         delta=delta, dq=dq32, bdq=Lq * d, dk=dkv, dv=dkv[:, d:], sdk=2 * d, sdv=2 * d,
-                        bdk=Sx * 2 * d, bdv=Sx * 2 * d, rot=rot, rot_d=d)
+                        bdk=Sx * 2 * d, bdv=Sx * 2 * d, rot=rot, rot_d=d, o32=st['O32'], so32=d, bo32=Lq * d)
             K.colsum(dq32, B, Lq * d, Lq * d, P.g(a + 'learned_queries').view(-1))
             self._dw(dkv, st['h'], a + 'k_linear.weight', rows_x, 2 * d, d)
             self._db(dkv, a + 'k_linear.bias', rows_x, 2 * d)
@@ -358,7 +363,7 @@ class VAEEngine:
                         sq=3 * d, bq=Sx * 3 * d, sk=3 * d, sv=3 * d, bk=Sx * 3 * d, bv=Sx * 3 * d, so=d, bo=Lq * d,
                         key_pad=st['pad_k'], causal=st['causal'], backward=True, dout=dO, sdo=d, bdo=Lq * d,
                         delta=delta, dq=dq32, bdq=Sx * d, dk=dqkv[:, d:], dv=dqkv[:, 2 * d:], sdk=3 * d, sdv=3 * d,
-                        bdk=Sx * 3 * d, bdv=Sx * 3 * d, rot=rot, rot_d=d)
+                        bdk=Sx * 3 * d, bdv=Sx * 3 * d, rot=rot, rot_d=d, o32=st['O32'], so32=d, bo32=Lq * d)
             K.dq_finalize(dq32, dqkv, 3 * d, rows_x, d, rot, Sx)
             self._dw(dqkv, st['h'], a + 'q_linear.weight', rows_x, 3 * d, d)
             self._db(dqkv, a + 'q_linear.bias', rows_x, 3 * d)

@@ -93,7 +93,7 @@ _attn_desc = N.AttnDesc()
 
 def attention(q, k, v, o, lse, *, B, H, Lq, Lk, hd, sq, sk, sv, so, bq, bk, bv, bo, key_pad=None, causal=False,
               scale=None, backward=False, dout=None, sdo=0, bdo=0, delta=None, dq=None, bdq=0, dk=None, dv=None,
-              sdk=0, sdv=0, bdk=0, bdv=0, rot=None, rot_d=0):
+              sdk=0, sdv=0, bdk=0, bdv=0, rot=None, rot_d=0, o32=None, so32=0, bo32=0):
     d = _attn_desc
     d.q, d.k, d.v, d.o = q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr()
     d.sq, d.sk, d.sv, d.so, d.bq, d.bk, d.bv, d.bo = sq, sk, sv, so, bq, bk, bv, bo
@@ -101,6 +101,7 @@ def attention(q, k, v, o, lse, *, B, H, Lq, Lk, hd, sq, sk, sv, so, bq, bk, bv, 
     d.lse = lse.data_ptr()
     d.B, d.H, d.Lq, d.Lk, d.hd, d.causal = B, H, Lq, Lk, hd, int(causal)
     d.scale = hd ** -0.5 if scale is None else scale
+    d.o32, d.so32, d.bo32 = ptr(o32), so32, bo32
     if backward:
         d.dout, d.sdo, d.bdo = dout.data_ptr(), sdo, bdo
         d.delta, d.dq, d.bdq = delta.data_ptr(), dq.data_ptr(), bdq

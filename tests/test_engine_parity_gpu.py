@@ -60,5 +60,6 @@ def test_step_matches_oracle(name):
         worst.append((cos, ratio, n))
     worst.sort()
     msg = '\n'.join(f'{c:.5f} {r:.4f} {n}' for c, r, n in worst[:8])
+    print(f'[{name}] loss {loss:.6f} ref {ref["loss"].item():.6f} kl {kl:.6f} ref {ref["kl"].item():.6f}\n' + msg)
     assert worst[0][0] > 0.98, msg
     assert all(0.95 < r < 1.05 for _, r, _ in worst), msg
