@@ -1,0 +1,226 @@
+"""Training-throughput benchmark of the MI355X TransformerVAE step (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c4|c5|tiny]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+A step = TransformerVAE.training_step (forward) + loss.backward() (engine backward with the bucketed RCCL
+gradient all-reduce overlapped) + on_after_backward (grad norm, KL anneal) + RAdam.step (fused clip +
+update) + LambdaLR.step, on a synthetic batch resident in HBM. Weak scaling: every rank runs the per-GPU
+batch of the config; value = all ranks' tokens / max-over-ranks wall time.
+
+Rank 0 prints ONE JSON line. At N=1 it also carries:
+  roofline     — the dominant kernel (the tied vocab-head GEMM, 2*T*d*V flops per launch) timed with HIP
+                 events on its own stream over the timed steps, against the dense bf16 MFMA peak;
+  cpu_baseline — the CPU fp32 oracle (oracle/, pinned to the reference by tests/golden) timed on this
+                 host's cores on a bounded sample of the same workload;
+  parity       — GPU step vs CPU oracle loss / ELBO on the C2 model at batch 2 (same weights, noise).
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, 'sparse-vae_amd'))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = 'training tokens/sec + ELBO match vs CPU ref, 512-tok seq, 1/2/4/8 MI355X'
+CONFIGS = {
+    'tiny': dict(layers=4, d=128, heads=8, L=128, B=64),
+    'c2': dict(layers=6, d=512, heads=8, L=512, B=64),
+    'c4': dict(layers=12, d=768, heads=8, L=1024, B=64),
+    'c5': dict(layers=12, d=768, heads=8, L=2048, B=32),
+}
+V, NLAT = 32768, 64
+PEAK_BF16_TFLOPS = 2500.0      # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def flops_per_token(nl, d, L, V=V, N=NLAT):
+    """F_train = 3 * F_fwd (dense count, verified against torch.utils.flop_counter)."""
+    f_enc = (4 * d * d + 4 * N * d + 18 * d * d * N / L) \
+        + (nl // 2 - 2) * (4 * d * d + 4 * N * d + (28 * d * d * N + 4 * N * N * d) / L) \
+        + (4 * d * d * N + 4 * N * d + 18 * d * d) / L
+    f_fwd = nl * (24 * d * d + 4 * L * d) + 2 * d * d + 2 * d * V + f_enc
+    return 3 * f_fwd
+
+
+def build(cfg, device):
+    from sparse_vae import TransformerVAE, TransformerVAEHparams, TextDataModule
+    hp = TransformerVAEHparams(d_model=cfg['d'], num_layers=cfg['layers'], num_heads=cfg['heads'], latent_depth=64,
+                               sparse_self_attention=False, grad_clip_threshold=150.0, init_scale=0.02,
+                               kl_weight_start=0.3, kl_weight_end=1.0, kl_annealing_steps=8000, lr=3e-4)
+    model = TransformerVAE(hp, device=device)
+    model.initialize_weights()
+    model.on_train_start()
+    dm = TextDataModule(dataset_name='synthetic', seq_len=cfg['L'], batch_size=cfg['B'],
+                        seed=7295 + 17 * int(os.environ.get('RANK', '0')))
+    batch = dm.synthetic_batch(0, device=device)                  # resident in HBM before timing
+    [opt], [sch] = model.configure_optimizers(cfg['B'] * cfg['L'], 1)
+    return model, opt, sch['scheduler'], batch
+
+
+def step(model, opt, sched, batch):
+    out = model.training_step(batch, 0)
+    out['loss'].backward()
+    model.on_after_backward()
+    opt.step()
+    sched.step()
+    opt.zero_grad()
+    return out
+
+
+def cpu_baseline(cfg, seconds_budget=25.0):
+    """The oracle's fp32 fwd+bwd on the host cores, on a bounded sample (batch 8 of the same model)."""
+    import oracle
+    from oracle.params import portable_ids
+    threads = min(len(os.sched_getaffinity(0)), 16)
+    torch.set_num_threads(threads)
+    hp = oracle.HParams(d_model=cfg['d'], num_heads=cfg['heads'], num_layers=cfg['layers'])
+    params = {k: v.requires_grad_(True) for k, v in oracle.init_params(hp, 0, test_init=False).items()}
+    B, L = 8, cfg['L']
+    ids = torch.from_numpy(portable_ids((B, L), 11))
+    ntok = torch.full((B,), L, dtype=torch.int64)
+    eps = torch.randn(B, 1, 64)
+    times = []
+    t_all = time.time()
+    for i in range(4):
+        t0 = time.time()
+        out = oracle.training_step(params, hp, ids, ntok, eps)
+        out['loss'].backward()
+        for p in params.values():
+            p.grad = None
+        times.append(time.time() - t0)
+        if time.time() - t_all > seconds_budget:
+            break
+    steady = times[1:] if len(times) > 1 else times
+    dt = sum(steady) / len(steady)
+    return {'value': round(B * L / dt, 1), 'unit': 'tokens/s', 'cores': threads, 'kind': 'port',
+            'sample': f'oracle/ (torch fp32 CPU restatement, golden-pinned) fwd+bwd of the {cfg["layers"]}L '
+                      f'd{cfg["d"]} model at batch {B} x {L} tokens, mean of {len(steady)} step(s) after 1 warmup '
+                      f'({dt:.2f} s/step)'}
+
+
+def parity_check(device):
+    """GPU engine vs CPU oracle on the C2 model at batch 2 (same portable weights and noise)."""
+    import oracle
+    from oracle.params import portable_ids, portable_normal
+    from sparse_vae.engine import FlatParams, VAEEngine
+    hp = oracle.HParams(d_model=512, num_heads=8, num_layers=6, kl_weight=0.7)
+    params = oracle.init_params(hp, 3)
+    B, L = 2, 512
+    ids = torch.from_numpy(portable_ids((B, L), 5))
+    ntok = torch.full((B,), L, dtype=torch.int64)
+    eps = torch.from_numpy(portable_normal(B * 64, 'eps', 3).reshape(B, 1, 64).astype('float32'))
+    with torch.no_grad():
+        ref = oracle.training_step(params, hp, ids, ntok, eps)
+    flat = FlatParams(hp, device)
+    for n in flat.offsets:
+        flat.view(n).copy_(params[n])
+    eng = VAEEngine(hp, flat)
+    out = eng.forward(ids.to(device), ntok.to(device), eps=eps.to(device), dropout=0.0, kl_weight=0.7)
+    loss, nll, kl = out['loss'].item(), out['nll'].item(), out['kl'].item()
+    elbo, elbo_ref = -(nll + kl), -(ref['nll'].item() + ref['kl'].item())
+    return {'config': 'C2 model (6L d512 L512) batch 2, dropout off, injected eps',
+            'loss_gpu': loss, 'loss_cpu_ref': ref['loss'].item(),
+            'loss_rel_err': abs(loss - ref['loss'].item()) / abs(ref['loss'].item()),
+            'elbo_rel_err': abs(elbo - elbo_ref) / abs(elbo_ref), 'tolerance': 1e-3}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=20)
+    ap.add_argument('--warmup', type=int, default=5)
+    ap.add_argument('--config', default=None)
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-parity', action='store_true')
+    args = ap.parse_args()
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    torch.cuda.set_device(local)
+    device = torch.device('cuda', local)
+    if world > 1:
+        dist.init_process_group('nccl', device_id=device)
+    cfg_name = args.config or 'c2'
+    cfg = CONFIGS[cfg_name]
+
+    model, opt, sched, batch = build(cfg, device)
+    if world > 1:
+        model.enable_data_parallel()
+    eng = model._engine
+
+    for _ in range(args.warmup):
+        step(model, opt, sched, batch)
+
+    # dominant-kernel timing: HIP events around every vocab-head GEMM launch of the timed steps
+    probes = []
+    eng.probe = probes
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(model, opt, sched, batch)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    eng.probe = None
+    if world > 1:
+        t = torch.tensor([dt], device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = t.item()
+    ms = dt / args.steps * 1e3
+    tokens = cfg['B'] * cfg['L'] * world * args.steps
+    value = tokens / dt
+    fpt = flops_per_token(cfg['layers'], cfg['d'], cfg['L'])
+    loss = model.logged.get('train_nll')
+
+    if rank == 0:
+        T = cfg['B'] * cfg['L']
+        head_ms = sum(a.elapsed_time(b) for a, b in probes) / max(1, len(probes))
+        head_flops = 2.0 * T * cfg['d'] * V
+        achieved = head_flops / (head_ms * 1e-3) / 1e12 if head_ms > 0 else None
+        traffic = None
+        pmc = os.path.join(ROOT, 'profiles', f'pmc_head_gemm_{cfg_name}.json')
+        if os.path.exists(pmc):
+            with open(pmc) as f:
+                traffic = json.load(f).get('hbm_bytes_per_launch')
+        res = {
+            'metric': METRIC, 'value': round(value, 1), 'unit': 'tokens/s', 'n_gpus': world, 'steps': args.steps,
+            'warmup': args.warmup, 'ms_per_step': round(ms, 3), 'higher_is_better': True, 'scaling': 'weak',
+            'vs_baseline': None, 'dtype': 'bf16', 'data': 'synthetic (uniform ids in [3, 32768), [CLS] first, no padding; random-init weights)',
+            'config': {'workload': f'{cfg_name}: TransformerVAE {cfg["layers"]}L d{cfg["d"]} heads {cfg["heads"]} seq {cfg["L"]}, '
+                                   f'batch {cfg["B"]}/GPU, dense attention, dropout 0.1, fwd+bwd+allreduce+clip+RAdam',
+                       'model': f'TransformerVAE-{cfg["layers"]}L-d{cfg["d"]}', 'global_batch': cfg['B'] * world,
+                       'seq_len': cfg['L'], 'parallelism': f'dp{world}'},
+            'model_tflops_per_gpu': round(value / world * fpt / 1e12, 1),
+            'step_mfu': round(value / world * fpt / (PEAK_BF16_TFLOPS * 1e12), 4),
+            'roofline': {'kernel': 'gemm_kernel<false,false,SVAE_EPI_CE_STATS> (vocab head + CE stats)',
+                         'bound': 'mfma', 'achieved': round(achieved, 1) if achieved else None,
+                         'peak': PEAK_BF16_TFLOPS, 'unit': 'TFLOP/s',
+                         'frac': round(achieved / PEAK_BF16_TFLOPS, 4) if achieved else None,
+                         'traffic': traffic, 'launch_ms': round(head_ms, 4), 'flops_per_launch': head_flops},
+            'final_train_nll': round(loss.item(), 5) if torch.is_tensor(loss) else None,
+        }
+        if world == 1 and not args.no_parity:
+            try:
+                res['parity'] = parity_check(device)
+            except Exception as e:  # parity is reported, never allowed to kill the throughput line
+                res['parity'] = {'error': repr(e)}
+        if world == 1 and not args.no_cpu_baseline:
+            res['cpu_baseline'] = cpu_baseline(cfg)
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

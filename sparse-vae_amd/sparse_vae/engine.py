@@ -102,6 +102,10 @@ class FlatParams:
         self.grad = torch.zeros(self.total, dtype=f32, device=self.device)
         self.shadow_version = -1
 
+    def end(self, name):
+        off, shape = self.offsets[name]
+        return off + -(-math.prod(shape) // ALIGN) * ALIGN
+
     def view(self, name, buf=None):
         off, shape = self.offsets[name]
         buf = self.master if buf is None else buf
@@ -170,6 +174,7 @@ class VAEEngine:
         self.hd = self.d // self.H
         self._rot = None
         self.saved = None
+        self.probe = None      # list -> HIP events around each vocab-head GEMM launch (bench roofline)
 
     # ------------------------------------------------------------------ helpers
     def rot(self, L):
@@ -388,9 +393,9 @@ class VAEEngine:
         ids32 = ws.get('ids', (B, L), torch.int32)
         ids32.copy_(ids)
         padm = None
-        if pad:
+        if pad is not None and pad is not False:
             padm = ws.get('pad', (B, L), torch.uint8)
-            padm.copy_(ids.eq(0))
+            padm.copy_(ids.eq(0) if pad is True else pad)
         labels = ws.get('labels', (B, L), torch.int32)
         labels[:, :-1].copy_(ids32[:, 1:])
         labels[:, -1] = 0
@@ -433,17 +438,7 @@ class VAEEngine:
         sv.update(enc_bf=enc_bf, stats=stats, z_bf=zb, eps=eps_buf)
 
         # ---- decoder (transformer_vae.py:85-93), position 0 replaced by z_projections[i](z) every layer
-        xs = ws.get('x_dec0', (T, d), f32)
-        xs.copy_(x_emb)
-        dec = []
-        for i in range(hp.num_layers):
-            K.gemm(zb, P.w(f'z_projections.{i}.weight'), xs, B, d, Z, ldc=L * d, epi=EPI_F32,
-                   bias=P.f(f'z_projections.{i}.bias'))
-            xs, st = self.layer_fwd(f'decoder_layers.{i}.', xs, B, L, L, padm, causal=True, heads=self.H,
-                                    hd=self.hd, drop_p=dropout, seed=_mix_seed(seed, i), tag=f'd{i}',
-                                    out=ws.get(f'x_dec{i + 1}', (T, d), f32))
-            dec.append(st)
-        sv['dec_layers'] = dec
+        xs, sv['dec_layers'] = self._decode(x_emb, zb, padm, B, L, dropout, seed)
 
         # ---- output head + cross entropy (transformer_language_model.py:55-63, language_model.py:161-170)
         xf = ws.get('xf_bf', (T, d))
@@ -457,8 +452,16 @@ class VAEEngine:
         ntile = -(-V // 128)
         part = ws.get('ce.part', (T, ntile, 2), f32)
         lab_logit = ws.get('ce.label_logit', (T,), f32)
+        probe = self.probe
+        if probe is not None:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e0.record()
         K.gemm(hh, P.w('input_layer.0.weight'), logits, T, V, d, epi=EPI_CE_STATS, bias=P.f('output_layer.3.bias'),
                aux=part, labels=labels, label_logit=lab_logit)
+        if probe is not None:
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record()
+            probe.append((e0, e1))
         numel = B * (L - 1) * V
         chunks = -(-numel // CE_CHUNK_NUMEL)
         chunk_len = -(-(L - 1) // chunks)
@@ -476,9 +479,51 @@ class VAEEngine:
                 'mu': stats[:, :Z], 'logvar': stats[:, Z:], 'z': zf, 'eps': eps_buf,
                 'logits': logits if need_logits else None}
 
-    def backward(self, gloss, kl_weight):
-        """Gradients of loss = nll + kl_weight * kl into the flat gradient arena (accumulating)."""
+    def _decode(self, x_emb, zb, padm, B, L, dropout, seed):
+        hp, d, ws, P = self.hp, self.d, self.ws, self.P
+        T, Z = B * L, hp.latent_depth
+        xs = ws.get('x_dec0', (T, d), f32)
+        xs.copy_(x_emb)
+        dec = []
+        for i in range(hp.num_layers):
+            K.gemm(zb, P.w(f'z_projections.{i}.weight'), xs, B, d, Z, ldc=L * d, epi=EPI_F32,
+                   bias=P.f(f'z_projections.{i}.bias'))
+            xs, st = self.layer_fwd(f'decoder_layers.{i}.', xs, B, L, L, padm, causal=True, heads=self.H,
+                                    hd=self.hd, drop_p=dropout, seed=_mix_seed(seed, i), tag=f'd{i}',
+                                    out=ws.get(f'x_dec{i + 1}', (T, d), f32))
+            dec.append(st)
+        return xs, dec
+
+    def reconstruct(self, x_emb, z, pad=None):
+        """TransformerVAE.reconstruct (transformer_vae.py:85-93): decoder + head logits [B, L, V] bf16 from
+        x_emb f32 [B, L, d] and z f32 [B, latent]; pad = [B, L] mask or None."""
+        hp, d, ws, P = self.hp, self.d, self.ws, self.P
+        P.sync_shadow()
+        B, L = x_emb.shape[0], x_emb.shape[1]
+        T, V, Z = B * L, hp.vocab_size, hp.latent_depth
+        padm = None
+        if pad is not None:
+            padm = ws.get('pad', (B, L), torch.uint8)
+            padm.copy_(pad)
+        zb = ws.get('z_bf', (B, Z))
+        K.cast_bf16(z, zb)
+        xs, _ = self._decode(x_emb.reshape(T, d), zb, padm, B, L, 0.0, 0)
+        xf = ws.get('xf_bf', (T, d))
+        K.cast_bf16(xs, xf)
+        pre0 = ws.get('h0_pre', (T, d))
+        h0 = ws.get('h0', (T, d))
+        K.gemm(xf, P.w('output_layer.0.weight'), h0, T, d, d, epi=EPI_GELU, bias=P.f('output_layer.0.bias'),
+               aux=pre0, ldaux=d)
+        hh, _ = self._ln_fwd('output_layer.2', h0, T, 'head.ln')
+        logits = torch.empty(B, L, V, dtype=bf16, device=P.device)
+        K.gemm(hh, P.w('input_layer.0.weight'), logits, T, V, d, epi=EPI_BF16, bias=P.f('output_layer.3.bias'))
+        return logits
+
+    def backward(self, gloss, kl_weight, ready=None):
+        """Gradients of loss = nll + kl_weight * kl into the flat gradient arena (accumulating). `ready(end)`
+        is called each time the arena prefix [0, end) holds final gradients (data-parallel bucketing)."""
         sv, hp, d, ws, P = self.saved, self.hp, self.d, self.ws, self.P
+        ready = ready or (lambda end: None)
         if sv is None:
             raise RuntimeError('backward() without a saved forward')
         B, L = sv['B'], sv['L']
@@ -502,6 +547,7 @@ class VAEEngine:
         self._db(dpre0, 'output_layer.0.bias', T, d)
         dx = ws.get('b.dx_dec', (T, d), f32)
         K.gemm(dpre0, P.w('output_layer.0.weight'), dx, T, d, d, b_t=True, epi=EPI_F32)
+        ready(P.end('output_layer.3.bias'))
 
         # ---- decoder layers, last to first
         dz = ws.get('b.dz', (B, Z), f32, zero=True)
@@ -517,6 +563,7 @@ class VAEEngine:
             self._dw(dzh_bf, sv['z_bf'], f'z_projections.{i}.weight', B, d, Z)
             self._db(dzh, f'z_projections.{i}.bias', B, d)
             K.gemm(dzh_bf, P.w(f'z_projections.{i}.weight'), dz, B, Z, d, b_t=True, epi=EPI_F32_ACC)
+            ready(P.end(f'z_projections.{i}.bias'))
             dx, dx_prev = dx_prev, dx
         dx_emb = dx                                   # decoder part of d x_emb (rows 0 already zero)
 
@@ -529,6 +576,7 @@ class VAEEngine:
         self._db(dstats, 'q_of_z_given_x.linear.bias', B, 2 * Z)
         denc = ws.get('b.denc', (B, d), f32)
         K.gemm(dstats_bf, P.w('q_of_z_given_x.linear.weight'), denc, B, d, 2 * Z, b_t=True, epi=EPI_F32)
+        ready(P.end('q_of_z_given_x.linear.bias'))
 
         # ---- encoder, bottleneck -> middle -> first
         enc = sv['enc_layers']
@@ -537,6 +585,7 @@ class VAEEngine:
             st = enc[k]
             nxt = ws.get(f'b.denc{k}', (B * N, d), f32)
             self.layer_bwd(st, dcur, nxt, dctx=dx_emb)
+            ready(P.end(st['pre'] + 'ffn_layer_norm.bias'))
             dcur = nxt
         st0 = enc[0]
         if st0['resid']:   # L == num_latents: the first layer keeps its residual (transformer_layer.py:49)
@@ -546,5 +595,7 @@ class VAEEngine:
         else:
             self.layer_bwd(st0, dcur, dx_emb, dx_accumulate=True)
 
+        ready(P.end('encoder.first_layer.ffn_layer_norm.bias'))
         # ---- embedding (tied with the head weight)
         K.embedding_bwd(sv['ids32'], dx_emb, P.g('input_layer.0.weight'), T, d)
+        ready(P.n_live)

@@ -1,0 +1,291 @@
+"""TransformerVAE (transformer_vae.py:16-128 in the reference) on MI355X.
+
+Same hparams dataclass, module tree and `state_dict` keys as the reference; the arithmetic of
+`training_step` / `reconstruct` runs in the fused HIP step engine (sparse_vae/engine.py). Parameters are
+views into one flat f32 arena (+ bf16 shadow, + flat grad arena) in gradient-ready order.
+
+Autograd compatibility: `training_step` returns a loss tensor whose `.backward()` runs the engine's
+explicit backward and leaves every parameter's `.grad` as a view of the gradient arena, so the reference's
+Lightning loop (training_step -> backward -> on_after_backward -> optimizer.step) works unchanged.
+"""
+from copy import deepcopy
+from dataclasses import dataclass
+from typing import Any, Dict, Optional
+
+import torch
+import torch.distributed as dist
+from torch import nn
+from torch.distributions.normal import Normal
+
+from .core import (ContinuousVAEHparams, ContinuousVAEHooks, ConditionalGaussian, LanguageModel, Perceiver,
+                   TransformerHparams, TransformerLayer, VOCAB_SIZE, marginal_kl)
+from .core.padded_tensor import PaddedTensor
+from .engine import FlatParams, VAEEngine
+from . import kernels as K
+from ._native import EPI_F32, EPI_BF16
+
+
+@dataclass
+class TransformerVAEHparams(TransformerHparams, ContinuousVAEHparams):
+    latent_depth: int = 64
+    pretrained_encoder: bool = False
+    pretrained_decoder: bool = False
+    use_gpt2: bool = False
+    early_stopping_metric: str = 'val_nll'
+
+
+class _EngineHP:
+    """The view of the hparams the engine reads."""
+
+    def __init__(self, hp):
+        self.d_model, self.num_heads, self.num_layers = hp.d_model, hp.num_heads, hp.num_layers
+        self.latent_depth, self.num_latents, self.vocab_size = hp.latent_depth, 64, VOCAB_SIZE
+        self.enc_layers = hp.num_layers // 2
+
+
+class _StepFn(torch.autograd.Function):
+    """One autograd node for the whole step: backward = the engine's explicit backward."""
+
+    @staticmethod
+    def forward(ctx, anchor, model, loss):
+        ctx.model = model
+        return loss.detach().clone()
+
+    @staticmethod
+    def backward(ctx, gloss):
+        ctx.model._run_backward(gloss)
+        return None, None, None
+
+
+class TransformerVAE(ContinuousVAEHooks, LanguageModel):
+    def __init__(self, hparams, device: Optional[str] = None):
+        super().__init__(hparams)
+        hp = self.hparams
+        d = hp.d_model
+        if (hp.get('d_embedding') or d) != d:
+            raise NotImplementedError('d_embedding != d_model (input projection) is not on the MI355X path')
+        if not hp.get('tie_embedding_weights', True):
+            raise NotImplementedError('untied embedding/head weights are not on the MI355X path')
+        if hp.get('cross_attention', False):
+            raise NotImplementedError('decoder cross-attention (transformer-lm context) is not on the VAE path')
+        if d % 64:
+            raise ValueError('d_model must be a multiple of 64 (Perceiver heads = d_model // 64, perceiver.py:13)')
+        # --- module tree in the reference's registration order (transformer_language_model.py:34-72,
+        #     transformer_vae.py:26-40) so state_dict keys and order match
+        self.input_layer = nn.Sequential(nn.Embedding(VOCAB_SIZE, d), nn.Dropout(p=hp.get('input_dropout', 0.0)))
+        self.context_layer = None
+        self.output_layer = nn.Sequential(nn.Linear(d, d), nn.GELU(), nn.LayerNorm(d), nn.Linear(d, VOCAB_SIZE))
+        self.output_layer[3].weight = self.input_layer[0].weight
+        sparse = hp.get('sparse_self_attention', True)
+        self.decoder_layers = nn.ModuleList([
+            TransformerLayer(d, hp.num_heads, causal=True, sparse_self_attention=False if not sparse else hp.attn_window_size)
+            for _ in range(hp.num_layers)])
+        self.example_input_array = None
+        self.encoder_input_layer = deepcopy(self.input_layer)
+        self.encoder_input_layer[0].weight = self.input_layer[0].weight
+        self.q_of_z_given_x = ConditionalGaussian(d, hp.latent_depth)
+        self.encoder = Perceiver(num_layers=hp.num_layers // 2, num_latents=64, d_model=d, bottleneck_width=1)
+        self.z_projections = nn.ModuleList([nn.Linear(hp.latent_depth, d) for _ in range(hp.num_layers)])
+        self._ehp = _EngineHP(hp)
+        if device is None:
+            device = 'cuda' if torch.cuda.is_available() else 'cpu'
+        self._flat = None
+        self._engine = None
+        self._bind_flat(torch.device(device))
+        self._norm_part = None
+        self._norm_valid = False
+        self._dp = None
+        self._step_seed = 7295
+
+    # ------------------------------------------------------------------ flat arena plumbing
+    def _bind_flat(self, device):
+        old = self._flat
+        flat = FlatParams(self._ehp, device)
+        with torch.no_grad():
+            for name in flat.offsets:
+                src = self.get_parameter(name)
+                flat.view(name).copy_(src.detach().to(device))
+        for name in flat.offsets:
+            mod_name, _, pname = name.rpartition('.')
+            mod = self.get_submodule(mod_name)
+            mod._parameters[pname] = nn.Parameter(flat.view(name), requires_grad=True)
+        emb = self.input_layer[0].weight
+        self.output_layer[3].weight = emb
+        self.encoder_input_layer[0].weight = emb
+        self._flat = flat
+        self._engine = VAEEngine(self._ehp, flat) if device.type == 'cuda' else None
+        self._grads_attached = False
+        del old
+
+    def _apply(self, fn, recurse=True):
+        probe = fn(torch.zeros(1, device=self._flat.device))
+        if probe.dtype != torch.float32:
+            raise RuntimeError('TransformerVAE keeps f32 master weights (bf16 copies are internal)')
+        if probe.device != self._flat.device:
+            self._bind_flat(probe.device)
+        return self
+
+    @property
+    def device(self):
+        return self._flat.device
+
+    def _require_engine(self):
+        if self._engine is None:
+            raise RuntimeError('TransformerVAE.training_step runs on the MI355X HIP kernels: move the model to a '
+                               'GPU (model.cuda()). There is no CPU fallback.')
+        return self._engine
+
+    def zero_grad_flat(self):
+        self._flat.grad.zero_()
+        self._attach_grads()
+        self._norm_valid = False
+
+    def zero_grad(self, set_to_none: bool = True):
+        self.zero_grad_flat()
+
+    def _attach_grads(self):
+        flat = self._flat
+        for name in flat.live_names:
+            p = self.get_parameter(name)
+            p.grad = flat.g(name)
+        self._grads_attached = True
+
+    @property
+    def _anchor(self):
+        return self.q_of_z_given_x.linear.bias
+
+    def _grads_alive(self):
+        p = self._anchor
+        return self._grads_attached and p.grad is not None and p.grad.data_ptr() == self._flat.g(
+            'q_of_z_given_x.linear.bias').data_ptr()
+
+    # ------------------------------------------------------------------ data parallel (RCCL over xGMI)
+    def enable_data_parallel(self, group=None, bucket_mb: float = 64.0):
+        """Pure DP: grads are averaged with bucketed async all-reduces launched while the
+        backward is still running (the arena is in gradient-ready order, so buckets are contiguous)."""
+        self._dp = {'group': group, 'bucket': int(bucket_mb * 2 ** 20 / 4), 'start': 0, 'works': []}
+        # identical initial weights on every rank
+        dist.broadcast(self._flat.master, 0, group=group)
+        self._flat.shadow_version = -1
+
+    def _dp_ready(self, end, final=False):
+        dp = self._dp
+        if dp is None:
+            return
+        if end - dp['start'] >= dp['bucket'] or (final and end > dp['start']):
+            seg = self._flat.grad[dp['start']:end]
+            dp['works'].append(dist.all_reduce(seg, op=dist.ReduceOp.AVG, group=dp['group'], async_op=True))
+            dp['start'] = end
+
+    def _dp_finish(self):
+        dp = self._dp
+        if dp is None:
+            return
+        self._dp_ready(self._flat.n_live, final=True)
+        for w in dp['works']:
+            w.wait()
+        dp['works'] = []
+        dp['start'] = 0
+
+    # ------------------------------------------------------------------ training step
+    def _batch_inputs(self, batch):
+        ids = batch['token_ids']
+        pad = getattr(ids, 'padding', None)
+        if isinstance(ids, PaddedTensor):
+            ids = ids.as_raw()
+        dev = self.device
+        ids = ids.to(dev, non_blocking=True)
+        if pad is not None:
+            pad = pad.to(dev, non_blocking=True)
+            if pad.shape != ids.shape:
+                pad = None
+        ntok = batch['num_tokens'].to(dev, non_blocking=True)
+        return ids, pad, ntok
+
+    def training_step(self, batch: Dict[str, Any], batch_index: int = 0, stage: str = 'train', eps=None,
+                      dropout: Optional[float] = None):
+        """transformer_vae.py:42-66. `eps` (injected N(0,1) noise [B,1,latent]) and `dropout` override the
+        in-kernel noise / the nn.Dropout(0.1) rate for parity runs."""
+        eng = self._require_engine()
+        ids, pad, ntok = self._batch_inputs(batch)
+        train = stage == 'train' and self.training
+        p = (0.1 if train else 0.0) if dropout is None else dropout
+        self._step_seed += 1
+        kw = float(self.hparams.kl_weight)
+        out = eng.forward(ids, ntok, pad=pad if pad is not None else False, eps=eps, seed=self._step_seed,
+                          kl_weight=kw, dropout=p)
+        self._last = out
+        self._kl_weight_used = kw
+        self.log(stage + '_kl', out['train_kl'])                       # continuous_autoencoder.py:50
+        self.log(stage + '_nll', out['nll'])                           # language_model.py:112
+        mu, logvar = out['mu'].view(-1, 1, self.hparams.latent_depth), out['logvar'].view(-1, 1, self.hparams.latent_depth)
+        scale = logvar.exp().sqrt()
+        if ids.shape[0] > 1 and self.hparams.get('log_mutual_info', True):
+            self.log(stage + '_mc_mutual_info', out['kl'] - marginal_kl(mu, scale))   # transformer_vae.py:59-61
+        if stage == 'train':
+            loss = _StepFn.apply(self._anchor, self, out['loss'])
+            return {'loss': loss, 'posterior': Normal(loc=mu.detach(), scale=scale.detach())}
+        if stage == 'val':
+            self.log('val_loss', out['nll'] + out['kl'])
+        return None
+
+    def validation_step(self, batch, batch_index: int = 0):
+        with torch.no_grad():
+            was = self.training
+            self.eval()
+            try:
+                return self.training_step(batch, batch_index, stage='val')
+            finally:
+                self.train(was)
+
+    def _run_backward(self, gloss):
+        eng = self._require_engine()
+        if not self._grads_alive():
+            self.zero_grad_flat()
+        eng.backward(gloss.reshape(()).to(torch.float32), self._kl_weight_used, ready=self._dp_ready)
+        self._dp_finish()
+        self._norm_valid = False
+
+    def _norm_partials(self, fresh=True):
+        if self._norm_part is None:
+            self._norm_part = torch.empty(1024, device=self.device)
+        if fresh or not self._norm_valid:
+            K.sumsq(self._flat.grad, self._flat.n_live, self._norm_part)
+            self._norm_valid = True
+        return self._norm_part
+
+    def grad_norm(self):
+        return self._norm_partials(fresh=True).sum().sqrt()
+
+    def on_after_backward(self):
+        super().on_after_backward()        # grad norm (+ clip inside the fused optimiser step)
+        self.anneal_kl()                   # continuous_autoencoder.py:28-39
+
+    # ------------------------------------------------------------------ inference-side helpers
+    @torch.no_grad()
+    def reconstruct(self, x, z):
+        """transformer_vae.py:85-93 on the device (no autograd): x = input_layer(ids) [B, L, d] f32 (a
+        PaddedTensor carrying the padding mask, or plain), z [B, 1, latent] -> logits [B, L, V] (bf16)."""
+        eng = self._require_engine()
+        pad = getattr(x, 'padding', None)
+        x = x.as_raw() if isinstance(x, PaddedTensor) else x
+        return eng.reconstruct(x.float().contiguous(), z.reshape(z.shape[0], -1).float().contiguous(), pad)
+
+    @torch.no_grad()
+    def embed(self, ids):
+        """input_layer(ids) as a PaddedTensor (the reference's x, transformer_vae.py:45)."""
+        pad = getattr(ids, 'padding', None)
+        raw = ids.as_raw() if isinstance(ids, PaddedTensor) else ids
+        raw = raw.to(self.device)
+        B, L = raw.shape
+        ids32 = raw.to(torch.int32).contiguous()
+        out = torch.empty(B, L, self.hparams.d_model, device=self.device)
+        K.embedding_fwd(ids32, self._flat.f('input_layer.0.weight'), out, B * L, self.hparams.d_model)
+        return PaddedTensor.from_raw(out, pad.to(self.device)) if pad is not None else out
+
+    @torch.no_grad()
+    def predict(self, batch, batch_idx: int = 0, dataloader_idx: Optional[int] = None):
+        """transformer_vae.py:81-83: q(z|x) for a batch."""
+        self.training_step(batch, stage='predict', dropout=0.0)
+        mu, logvar = self._last['mu'], self._last['logvar']
+        return Normal(mu.view(-1, 1, mu.shape[-1]).clone(), logvar.exp().sqrt().view(-1, 1, mu.shape[-1]))
