@@ -31,7 +31,7 @@ typedef void* svae_stream_t; /* hipStream_t */
  * a_t = 0: A stored [M][K] (lda >= K); a_t = 1: A stored [K][M] (lda >= M).
  * b_t = 0: B stored [N][K] (nn.Linear weight layout); b_t = 1: B stored [K][N].
  * Requirements: K % 8 == 0 unless a_t && b_t; for a_t: M % 8 == 0; for b_t: N % 8 == 0; lda, ldb % 8 == 0;
- * A, B 16-byte aligned. */
+ * A, B 16-byte aligned; N, ldc (and ldr, ldaux) % 4 == 0 and C 8-byte aligned (vectorised epilogue). */
 enum svae_epi {
   SVAE_EPI_BF16 = 0,          /* C bf16 = alpha*acc + bias                                            */
   SVAE_EPI_F32 = 1,           /* C f32  = alpha*acc + bias (+ resid)                                  */
@@ -67,6 +67,7 @@ typedef struct svae_gemm_desc {
   int32_t rot_cols, rot_d, rot_seq;
   const int32_t* labels;    /* CE_STATS: [M] target column per row (0 = ignored) */
   float* label_logit;       /* CE_STATS: [M] f32 out */
+  float* a_rowsum;          /* a_t only, optional: a_rowsum[m] += sum_k A[m][k] (bias grad of a dW GEMM) */
 } svae_gemm_desc;
 
 int svae_gemm(const svae_gemm_desc* d, svae_stream_t stream);
@@ -144,13 +145,13 @@ int svae_reparam_kl_bwd(const float* stats, const float* eps, const float* dz, c
  * into nchunks chunks of chunk_len (torch.chunk semantics) and nll = mean over chunks of the per-chunk
  * mean loss. finalize: lse[rows], row_loss[rows], chunk_w[nchunks] (= 1 / (count_c * nchunks)),
  * nll_out[1]. grad: in place, logits -> gscale[0] * chunk_w[c] * (softmax - onehot) in bf16 (0 for
- * ignored rows). nchunks <= 8. */
+ * ignored rows); dbias (optional, f32 [V]) += column sums of dlogits (output-bias gradient). nchunks <= 8. */
 int svae_ce_finalize(const float* part, int32_t ntile, const float* label_logit, const int32_t* labels,
                      int32_t rows, int32_t seq, int32_t nchunks, int32_t chunk_len, float* lse, float* row_loss,
                      float* chunk_w, float* nll_out, svae_stream_t stream);
 int svae_ce_grad(void* logits, int64_t ld, const float* lse, const float* chunk_w, const int32_t* labels,
-                 const float* gscale, int32_t rows, int32_t V, int32_t seq, int32_t nchunks, int32_t chunk_len,
-                 svae_stream_t stream);
+                 const float* gscale, float* dbias, int32_t rows, int32_t V, int32_t seq, int32_t nchunks,
+                 int32_t chunk_len, svae_stream_t stream);
 
 /* ---- elementwise helpers ------------------------------------------------------------------------ */
 /* dropout backward + cast: out bf16 = keep(seed, idx) * g / (1-p) (p = 0: plain cast). */

@@ -160,32 +160,42 @@ __global__ __launch_bounds__(1024) void ce_reduce_kernel(const float* __restrict
   }
 }
 
-// dlogits = g * w_row * (softmax - onehot), in place on bf16 logits; 8 elements per thread.
+// dlogits = g * w_chunk * (softmax - onehot), in place on bf16 logits, fused with the output-bias gradient
+// db[v] += sum_rows dlogits[row][v] (the reference's autograd sums it separately). Block = 256 threads x 8
+// columns = a 2048-column strip, walking `rows_per_block` rows: every row is one contiguous 4 KiB read+write.
 __global__ __launch_bounds__(256) void ce_grad_kernel(bf16* __restrict__ logits, long long ld, const float* __restrict__ lse,
                                                       const float* __restrict__ chunk_w, const int* __restrict__ labels,
-                                                      const float* __restrict__ gscale, int rows, int V, int seq,
-                                                      int nchunks, int chunk_len) {
-  const long long vec_per_row = V / 8;
-  const long long total = (long long)rows * vec_per_row;
+                                                      const float* __restrict__ gscale, float* __restrict__ dbias, int rows,
+                                                      int V, int seq, int nchunks, int chunk_len, int rows_per_block) {
+  const int c0 = (blockIdx.x * 256 + threadIdx.x) * 8;
+  const int r0 = blockIdx.y * rows_per_block;
+  const int r1 = min(rows, r0 + rows_per_block);
   const float g = gscale[0];
-  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
-    const int row = (int)(i / vec_per_row);
-    const int c0 = (int)(i % vec_per_row) * 8;
-    bf16x8* ptr = (bf16x8*)(logits + (long long)row * ld + c0);
-    const int lab = labels[row];
-    if (lab == 0) { *ptr = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0}; continue; }
-    const int ch = min((row % seq) / chunk_len, nchunks - 1);
-    const float w = g * chunk_w[ch];
-    const float l = lse[row];
-    bf16x8 v = *ptr;
-    bf16x8 o;
+  float db[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c0 < V) {
+    for (int row = r0; row < r1; ++row) {
+      bf16x8* ptr = (bf16x8*)(logits + (long long)row * ld + c0);
+      const int lab = labels[row];
+      if (lab == 0) { *ptr = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0}; continue; }
+      const int ch = min((row % seq) / chunk_len, nchunks - 1);
+      const float w = g * chunk_w[ch];
+      const float l = lse[row];
+      const bf16x8 v = *ptr;
+      bf16x8 o;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      float pr = __expf((float)v[e] - l);
-      if (c0 + e == lab) pr -= 1.0f;
-      o[e] = f2bf(w * pr);
+      for (int e = 0; e < 8; ++e) {
+        float pr = __expf((float)v[e] - l);
+        if (c0 + e == lab) pr -= 1.0f;
+        const float d = w * pr;
+        db[e] += d;
+        o[e] = f2bf(d);
+      }
+      *ptr = o;
     }
-    *ptr = o;
+    if (dbias) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) atomicAdd(dbias + c0 + e, db[e]);
+    }
   }
 }
 
@@ -369,12 +379,15 @@ SVAE_EXPORT int svae_ce_finalize(const float* part, int32_t ntile, const float* 
 }
 
 SVAE_EXPORT int svae_ce_grad(void* logits, int64_t ld, const float* lse, const float* chunk_w, const int32_t* labels,
-                             const float* gscale, int32_t rows, int32_t V, int32_t seq, int32_t nchunks,
+                             const float* gscale, float* dbias, int32_t rows, int32_t V, int32_t seq, int32_t nchunks,
                              int32_t chunk_len, svae_stream_t stream) {
   if (!logits || !lse || !chunk_w || !labels || !gscale || rows <= 0 || V % 8 || ld % 8) return SVAE_EINVAL;
-  const long long work = (long long)rows * (V / 8);
-  hipLaunchKernelGGL(ce_grad_kernel, dim3(grid_for(work, 256, 8192)), dim3(256), 0, (hipStream_t)stream, (bf16*)logits,
-                     ld, lse, chunk_w, labels, gscale, rows, V, seq, nchunks, chunk_len);
+  const int strips = (V + 2047) / 2048;
+  int rpb = 256;
+  while (rpb > 16 && (long long)strips * ((rows + rpb - 1) / rpb) < 1024) rpb /= 2;
+  dim3 grid(strips, (rows + rpb - 1) / rpb);
+  hipLaunchKernelGGL(ce_grad_kernel, grid, dim3(256), 0, (hipStream_t)stream, (bf16*)logits, ld, lse, chunk_w, labels,
+                     gscale, dbias, rows, V, seq, nchunks, chunk_len, rpb);
   SVAE_LAUNCH_CHECK();
   return SVAE_OK;
 }

@@ -30,6 +30,7 @@ struct GP {
   unsigned long long seed;
   const float* rot_tab; int rot_cols, rot_d, rot_seq;
   const int* labels; float* label_logit;
+  float* a_rowsum;   // optional: += sum_k A[m][k] (bias gradient fused into the dW GEMM); a_t layout only
   int epi;
 };
 
@@ -90,6 +91,9 @@ __device__ __forceinline__ bf16x8 read_frag(const char* lds, int base, int kk, i
   }
 }
 
+// f32 staging tile [128][128] for the epilogue: 16-B unit index XOR ((row >> 2) & 3) << 2
+__device__ __forceinline__ int cs_swz(int row, int col) { return (((col >> 2) ^ (((row >> 2) & 3) << 2)) << 2) | (col & 3); }
+
 template <bool AT, bool BT, int EPI>
 __global__ __launch_bounds__(256, 2) void gemm_kernel(GP p) {
   __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];
@@ -114,6 +118,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GP p) {
     for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
   const int nk = (kend - kbeg + BK - 1) / BK;
+  float rsum[4] = {0.f, 0.f, 0.f, 0.f};
   u32x4 ra[4], rb[4];
   if (nk > 0) {
     load_tile<AT>(A, p.lda, m0, p.M, kbeg, kend, ra, tid);
@@ -145,6 +150,18 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GP p) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
     }
+    if constexpr (AT) {
+      if (p.a_rowsum && bn == 0) {   // this block's share of sum_k A[m][k]: 4 columns x 8 k-rows per thread
+        const int mu = tid & 31, kg = tid >> 5;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          const short4v v = *(const short4v*)(la + mn_off(kg * 8 + r, mu));
+          const bf16x4 b = __builtin_bit_cast(bf16x4, v);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) rsum[e] += (float)b[e];
+        }
+      }
+    }
     if (more) {
       char* nb = smem + (cur ^ 1) * 2 * TILE_BYTES;
       store_tile<AT>(nb, ra, tid);
@@ -153,56 +170,87 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GP p) {
     __syncthreads();
   }
 
-  // ---------------------------------------------------------------- epilogue
-  const long long cofs = (long long)batch * p.sC;
-  if constexpr (EPI == SVAE_EPI_CE_STATS) {
-    // logits tile -> bf16 store, per-row (max, sumexp) over this block's 128 columns, label logit.
-    // Each wave covers 64 columns; reduce the 2 waves (wn) through LDS.
-    float* red = (float*)smem;  // [2 wn][128 rows][2]
+  if constexpr (AT) {
+    if (p.a_rowsum && bn == 0) {
+      const int m = m0 + (tid & 31) * 4;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+      for (int e = 0; e < 4; ++e)
+        if (m + e < p.M) atomicAdd(p.a_rowsum + m + e, rsum[e]);
+    }
+  }
+  // ---------------------------------------------------------------- epilogue
+  // Stage the 128x128 f32 tile through LDS (16-B units XOR-swizzled by row so the fragment writes spread
+  // over the banks), then every thread owns a fixed 4-column slice and walks 16 rows: all global traffic
+  // of the epilogue is 16-B (f32) / 8-B (bf16) vectors, two full rows per wave instruction.
+  float* cs = (float*)smem;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int ml = wm * 64 + i * 16 + 4 * (lane >> 4) + r;
-        const int m = m0 + ml;
-        float mx = -INFINITY;
-        float v[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int n = n0 + wn * 64 + j * 16 + (lane & 15);
-          float x = -INFINITY;
-          if (n < p.N) {
-            x = p.alpha * acc[i][j][r] + (p.bias ? p.bias[n] : 0.f);
-            if (m < p.M) {
-              ((bf16*)p.C)[cofs + (long long)m * p.ldc + n] = f2bf(x);
-              if (p.labels[m] == n) p.label_logit[m] = x;
-            }
-          }
-          v[j] = x;
-          mx = fmaxf(mx, x);
-        }
-        // reduce over the 16 lanes sharing this row (lane & 15 varies)
-#pragma unroll
-        for (int o = 8; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
-        float se = 0.f;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) se += (v[j] == -INFINITY) ? 0.f : __expf(v[j] - mx);
-#pragma unroll
-        for (int o = 8; o > 0; o >>= 1) se += __shfl_xor(se, o, 64);
-        if ((lane & 15) == 0) {
-          red[(wn * 128 + ml) * 2 + 0] = mx;
-          red[(wn * 128 + ml) * 2 + 1] = se;
-        }
+        const int row = wm * 64 + i * 16 + 4 * (lane >> 4) + r;
+        const int col = wn * 64 + j * 16 + (lane & 15);
+        cs[row * 128 + cs_swz(row, col)] = p.alpha * acc[i][j][r];
+      }
+  __syncthreads();
+  const long long cofs = (long long)batch * p.sC;
+  if constexpr (EPI == SVAE_EPI_F32_ATOMIC) {
+    // one column per lane: each wave-wide atomic covers 256 contiguous bytes (the full-rate shape)
+    const int col = tid & 127, n = n0 + col;
+    if (n < p.N) {
+      for (int it = 0; it < 64; ++it) {
+        const int row = (tid >> 7) + 2 * it, m = m0 + row;
+        if (m < p.M) atomicAdd((float*)p.C + cofs + (long long)m * p.ldc + n, cs[row * 128 + cs_swz(row, col)]);
       }
     }
-    __syncthreads();
-    if (tid < 128) {
-      const int m = m0 + tid;
-      if (m < p.M) {
-        const float a0 = red[tid * 2], s0 = red[tid * 2 + 1];
-        const float a1 = red[(128 + tid) * 2], s1 = red[(128 + tid) * 2 + 1];
-        const float mx = fmaxf(a0, a1);
-        const float se = (a0 == -INFINITY ? 0.f : s0 * __expf(a0 - mx)) + (a1 == -INFINITY ? 0.f : s1 * __expf(a1 - mx));
+    return;
+  }
+  const int cc = (tid & 31) * 4;          // this thread's 4 columns within the tile
+  const int n = n0 + cc;
+  const bool ncol = n < p.N;              // N % 4 == 0 (checked on the host)
+  f32x4 bias = {0.f, 0.f, 0.f, 0.f};
+  if (p.bias && ncol) bias = *(const f32x4*)(p.bias + n);
+
+  if constexpr (EPI == SVAE_EPI_CE_STATS) {
+    // (a) bf16 logits, coalesced
+#pragma unroll 4
+    for (int it = 0; it < 16; ++it) {
+      const int row = (tid >> 5) + 8 * it, m = m0 + row;
+      if (m >= p.M || !ncol) continue;
+      const f32x4 v = *(const f32x4*)(cs + row * 128 + cs_swz(row, cc)) + bias;
+      *(bf16x4*)((bf16*)p.C + cofs + (long long)m * p.ldc + n) = (bf16x4){f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
+    }
+    // (b) per-row online (max, sumexp) over the tile's columns: thread = (row, half)
+    const int row = tid >> 1, half = tid & 1, m = m0 + row;
+    float v[64];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int c = half * 64 + 4 * u;
+      f32x4 x = *(const f32x4*)(cs + row * 128 + cs_swz(row, c));
+      if (p.bias) x += (n0 + c < p.N) ? *(const f32x4*)(p.bias + n0 + c) : (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float y = (n0 + c + e < p.N) ? x[e] : -INFINITY;
+        v[4 * u + e] = y;
+        mx = fmaxf(mx, y);
+      }
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 1, 64));
+    float se = 0.f;
+#pragma unroll
+    for (int e = 0; e < 64; ++e) se += __expf(v[e] - mx);
+    se += __shfl_xor(se, 1, 64);
+    if (m < p.M) {
+      const int lab = p.labels[m];
+      const int lc = lab - n0 - half * 64;
+      if (lc >= 0 && lc < 64) {
+#pragma unroll
+        for (int e = 0; e < 64; ++e)
+          if (e == lc) p.label_logit[m] = v[e];
+      }
+      if (half == 0) {
         float* part = (float*)p.aux + ((long long)m * p.tiles_n + bn) * 2;
         part[0] = mx;
         part[1] = se;
@@ -211,56 +259,52 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GP p) {
     return;
   }
 
+#pragma unroll 4
+  for (int it = 0; it < 16; ++it) {
+    const int row = (tid >> 5) + 8 * it, m = m0 + row;
+    if (m >= p.M || !ncol) continue;
+    f32x4 x = *(const f32x4*)(cs + row * 128 + cs_swz(row, cc));
+    const long long ci = cofs + (long long)m * p.ldc + n;
+    if constexpr (EPI == SVAE_EPI_BF16) {
+      x += bias;
+      *(bf16x4*)((bf16*)p.C + ci) = (bf16x4){f2bf(x[0]), f2bf(x[1]), f2bf(x[2]), f2bf(x[3])};
+    } else if constexpr (EPI == SVAE_EPI_ROTARY_BF16) {
+      x += bias;
+      if (n < p.rot_cols) {   // pairs (n, n+1), (n+2, n+3): (a, b) -> (a c - b s, b c + a s)
+        const int pos = m % p.rot_seq;
+        const int pair = (n % p.rot_d) >> 1;
+        const f32x4 cs2 = *(const f32x4*)(p.rot_tab + ((long long)pos * (p.rot_d >> 1) + pair) * 2);
+        const float a0 = x[0], b0 = x[1], a1 = x[2], b1 = x[3];
+        x[0] = a0 * cs2[0] + (-b0) * cs2[1];
+        x[1] = b0 * cs2[0] + a0 * cs2[1];
+        x[2] = a1 * cs2[2] + (-b1) * cs2[3];
+        x[3] = b1 * cs2[2] + a1 * cs2[3];
+      }
+      *(bf16x4*)((bf16*)p.C + ci) = (bf16x4){f2bf(x[0]), f2bf(x[1]), f2bf(x[2]), f2bf(x[3])};
+    } else if constexpr (EPI == SVAE_EPI_F32) {
+      x += bias;
+      if (p.resid) x += *(const f32x4*)(p.resid + (long long)m * p.ldr + n);
+      *(f32x4*)((float*)p.C + ci) = x;
+    } else if constexpr (EPI == SVAE_EPI_F32_ACC) {
+      *(f32x4*)((float*)p.C + ci) = *(const f32x4*)((float*)p.C + ci) + x;
+    } else if constexpr (EPI == SVAE_EPI_GELU) {
+      x += bias;
+      *(bf16x4*)((bf16*)p.aux + (long long)m * p.ldaux + n) = (bf16x4){f2bf(x[0]), f2bf(x[1]), f2bf(x[2]), f2bf(x[3])};
+      *(bf16x4*)((bf16*)p.C + ci) = (bf16x4){f2bf(gelu_f(x[0])), f2bf(gelu_f(x[1])), f2bf(gelu_f(x[2])), f2bf(gelu_f(x[3]))};
+    } else if constexpr (EPI == SVAE_EPI_GELU_BWD) {
+      const bf16x4 pre = *(const bf16x4*)((const bf16*)p.aux + (long long)m * p.ldaux + n);
+      *(bf16x4*)((bf16*)p.C + ci) = (bf16x4){f2bf(x[0] * gelu_grad_f((float)pre[0])), f2bf(x[1] * gelu_grad_f((float)pre[1])),
+                                              f2bf(x[2] * gelu_grad_f((float)pre[2])), f2bf(x[3] * gelu_grad_f((float)pre[3]))};
+    } else if constexpr (EPI == SVAE_EPI_DROPOUT_RESID) {
+      if (p.drop_p > 0.f) {
+        const float sc = 1.0f / (1.0f - p.drop_p);
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int n = n0 + wn * 64 + j * 16 + (lane & 15);
-      const float bias = (p.bias && n < p.N) ? p.bias[n] : 0.f;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wm * 64 + i * 16 + 4 * (lane >> 4) + r;
-        float x = p.alpha * acc[i][j][r];
-        if constexpr (EPI == SVAE_EPI_ROTARY_BF16) {
-          x += bias;
-          const float partner = __shfl_xor(x, 1, 64);
-          if (n < p.rot_cols && m < p.M) {
-            const int pair = (n % p.rot_d) >> 1;
-            const int pos = m % p.rot_seq;
-            const float2 cs = ((const float2*)p.rot_tab)[(long long)pos * (p.rot_d >> 1) + pair];
-            x = (n & 1) ? (x * cs.x + partner * cs.y) : (x * cs.x + (-partner) * cs.y);
-          }
-        }
-        if (m >= p.M || n >= p.N) continue;
-        const long long ci = cofs + (long long)m * p.ldc + n;
-        if constexpr (EPI == SVAE_EPI_BF16) {
-          ((bf16*)p.C)[ci] = f2bf(x + bias);
-        } else if constexpr (EPI == SVAE_EPI_ROTARY_BF16) {
-          ((bf16*)p.C)[ci] = f2bf(x);
-        } else if constexpr (EPI == SVAE_EPI_F32) {
-          float y = x + bias;
-          if (p.resid) y += p.resid[(long long)m * p.ldr + n];
-          ((float*)p.C)[ci] = y;
-        } else if constexpr (EPI == SVAE_EPI_F32_ACC) {
-          ((float*)p.C)[ci] += x;
-        } else if constexpr (EPI == SVAE_EPI_F32_ATOMIC) {
-          atomicAdd(&((float*)p.C)[ci], x);
-        } else if constexpr (EPI == SVAE_EPI_GELU) {
-          const float pre = x + bias;
-          ((bf16*)p.aux)[(long long)m * p.ldaux + n] = f2bf(pre);
-          ((bf16*)p.C)[ci] = f2bf(gelu_f(pre));
-        } else if constexpr (EPI == SVAE_EPI_GELU_BWD) {
-          const float pre = bf2f(((const bf16*)p.aux)[(long long)m * p.ldaux + n]);
-          ((bf16*)p.C)[ci] = f2bf(x * gelu_grad_f(pre));
-        } else if constexpr (EPI == SVAE_EPI_DROPOUT_RESID) {
-          float y = x;
-          if (p.drop_p > 0.f) {
-            const float u = rand_uniform(p.seed, (unsigned long long)m * p.N + n);
-            y = (u >= p.drop_p) ? y * (1.0f / (1.0f - p.drop_p)) : 0.f;
-          }
-          ((float*)p.C)[ci] = p.resid[(long long)m * p.ldr + n] + y;
+        for (int e = 0; e < 4; ++e) {
+          const float u = rand_uniform(p.seed, (unsigned long long)m * p.N + n + e);
+          x[e] = (u >= p.drop_p) ? x[e] * sc : 0.f;
         }
       }
+      *(f32x4*)((float*)p.C + ci) = *(const f32x4*)(p.resid + (long long)m * p.ldr + n) + x;
     }
   }
 }
@@ -282,6 +326,10 @@ SVAE_EXPORT int svae_gemm(const svae_gemm_desc* d, svae_stream_t stream) {
   if (d->epi == SVAE_EPI_DROPOUT_RESID && !d->resid) return SVAE_EINVAL;
   if (d->epi == SVAE_EPI_CE_STATS && (!d->labels || !d->label_logit || d->splits != 1)) return SVAE_EINVAL;
   if (d->splits > 1 && d->epi != SVAE_EPI_F32_ATOMIC) return SVAE_EINVAL;
+  if (d->a_rowsum && !d->a_t) return SVAE_EINVAL;
+  if (d->N % 4 || d->ldc % 4 || ((uintptr_t)d->C & 7) || (d->resid && (d->ldr % 4)) || (d->aux && d->ldaux % 4))
+    return SVAE_EINVAL;   // vectorised epilogue
+  if (d->epi == SVAE_EPI_ROTARY_BF16 && (d->rot_d % 4 || d->rot_cols % 4)) return SVAE_EINVAL;
 
   GP p;
   p.A = (const bf16*)d->A; p.B = (const bf16*)d->B;
@@ -298,6 +346,7 @@ SVAE_EXPORT int svae_gemm(const svae_gemm_desc* d, svae_stream_t stream) {
   p.alpha = d->alpha; p.drop_p = d->drop_p; p.seed = d->seed;
   p.rot_tab = d->rot_tab; p.rot_cols = d->rot_cols; p.rot_d = d->rot_d; p.rot_seq = d->rot_seq;
   p.labels = d->labels; p.label_logit = d->label_logit;
+  p.a_rowsum = d->a_rowsum;
   p.epi = d->epi;
 
   dim3 grid(p.tiles_n * p.tiles_m, 1, d->batch * d->splits);

@@ -35,6 +35,7 @@ class GemmDesc(ctypes.Structure):
         ('alpha', c_float), ('drop_p', c_float), ('seed', c_uint64),
         ('rot_tab', c_void_p), ('rot_cols', c_int32), ('rot_d', c_int32), ('rot_seq', c_int32),
         ('labels', c_void_p), ('label_logit', c_void_p),
+        ('a_rowsum', c_void_p),
     ]
 
 
@@ -73,8 +74,8 @@ _SIGS = {
     'svae_reparam_kl_bwd': [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p],
     'svae_ce_finalize': [c_void_p, c_int32, c_void_p, c_void_p, c_int32, c_int32, c_int32, c_int32, c_void_p,
                          c_void_p, c_void_p, c_void_p, c_void_p],
-    'svae_ce_grad': [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_int32, c_int32,
-                     c_int32, c_void_p],
+    'svae_ce_grad': [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_int32,
+                     c_int32, c_int32, c_void_p],
     'svae_dropout_bwd_cast': [c_void_p, c_void_p, c_float, c_uint64, c_int64, c_int32, c_int64, c_void_p],
     'svae_gelu_bwd': [c_void_p, c_void_p, c_void_p, c_int64, c_void_p],
     'svae_cast_bf16': [c_void_p, c_void_p, c_int64, c_void_p],

@@ -198,8 +198,12 @@ class VAEEngine:
         wg = self.P.grad[self.P.offsets[name + '.weight'][0]:][:2 * D]   # [weight | bias] grads (adjacent)
         K.layernorm_bwd(dy, x, self.P.f(name + '.weight'), mean, rstd, dres, dx, dx_bf, wg, rows, D, part)
 
-    def _dw(self, dY, X, wname, rows, n_out, n_in, ldy=None, ldx=None):
-        K.linear_dw(dY, X, self.P.g(wname), rows, n_out, n_in, ldy, ldx)
+    def _dw(self, dY, X, wname, rows, n_out, n_in, ldy=None, ldx=None, bias=None):
+        bg = None
+        if bias is not None:
+            off = self.P.offsets[bias][0]
+            bg = self.P.grad[off:off + n_out]
+        K.linear_dw(dY, X, self.P.g(wname), rows, n_out, n_in, ldy, ldx, bgrad=bg)
 
     def _db(self, dY, bname, rows, cols, ld=None):
         off = self.P.offsets[bname][0]
@@ -302,8 +306,7 @@ class VAEEngine:
         dpre = ws.get('b.dpre', (rows_q, 4 * d))
         K.gemm(g2, P.w(pre + 'ffn.2.weight'), dpre, rows_q, 4 * d, d, b_t=True, epi=EPI_GELU_BWD, aux=st['preact'],
                ldaux=4 * d)
-        self._dw(dpre, st['h2'], pre + 'ffn.0.weight', rows_q, 4 * d, d)
-        self._db(dpre, pre + 'ffn.0.bias', rows_q, 4 * d)
+        self._dw(dpre, st['h2'], pre + 'ffn.0.weight', rows_q, 4 * d, d, bias=pre + 'ffn.0.bias')
         dh2 = ws.get('b.dh2', (rows_q, d))
         K.gemm(dpre, P.w(pre + 'ffn.0.weight'), dh2, rows_q, d, 4 * d, b_t=True, epi=EPI_BF16)
         dxc = ws.get('b.dxc', (rows_q, d), f32)
@@ -313,8 +316,7 @@ class VAEEngine:
         if st['cross']:
             c = pre + 'cross_attention.'
             rows_c = B * L
-            self._dw(gxc, st['Oc'], c + 'output_linear.weight', rows_q, d, d)
-            self._db(gxc, c + 'output_linear.bias', rows_q, d)
+            self._dw(gxc, st['Oc'], c + 'output_linear.weight', rows_q, d, d, bias=c + 'output_linear.bias')
             dOc = ws.get('b.dO', (rows_q, d))
             K.gemm(gxc, P.w(c + 'output_linear.weight'), dOc, rows_q, d, d, b_t=True, epi=EPI_BF16)
             dq32 = ws.get('b.dq32', (rows_q, d), f32, zero=True)
@@ -328,12 +330,10 @@ class VAEEngine:
                         so32=d, bo32=Lq * d)
             dqc = ws.get('b.dqc', (rows_q, d))
             K.dq_finalize(dq32, dqc, d, rows_q, d, rot, Lq)
-            self._dw(dqc, st['hq'], c + 'q_linear.weight', rows_q, d, d)
-            self._db(dqc, c + 'q_linear.bias', rows_q, d)
+            self._dw(dqc, st['hq'], c + 'q_linear.weight', rows_q, d, d, bias=c + 'q_linear.bias')
             dhq = ws.get('b.dhq', (rows_q, d))
             K.gemm(dqc, P.w(c + 'q_linear.weight'), dhq, rows_q, d, d, b_t=True, epi=EPI_BF16)
-            self._dw(dkvc, st['cx'], c + 'k_linear.weight', rows_c, 2 * d, d)
-            self._db(dkvc, c + 'k_linear.bias', rows_c, 2 * d)
+            self._dw(dkvc, st['cx'], c + 'k_linear.weight', rows_c, 2 * d, d, bias=c + 'k_linear.bias')
             dcx = ws.get('b.dcx', (rows_c, d))
             K.gemm(dkvc, P.w(c + 'k_linear.weight'), dcx, rows_c, d, 2 * d, b_t=True, epi=EPI_BF16)
             dx1 = ws.get('b.dx1', (rows_q, d), f32)
@@ -341,8 +341,7 @@ class VAEEngine:
             self._ln_bwd(pre + 'cross_attn_layer_norm', dhq, st['ln_cross'], rows_q, dxc, dx1, gx1)
             self._ln_bwd(pre + 'context_layer_norm', dcx, st['ln_ctx'], rows_c, dctx, dctx)
         # ---- self / learned-query attention (attention.py:51-105)
-        self._dw(gx1, st['O'], a + 'output_linear.weight', rows_q, d, d)
-        self._db(gx1, a + 'output_linear.bias', rows_q, d)
+        self._dw(gx1, st['O'], a + 'output_linear.weight', rows_q, d, d, bias=a + 'output_linear.bias')
         dO = ws.get('b.dO', (rows_q, d))
         K.gemm(gx1, P.w(a + 'output_linear.weight'), dO, rows_q, d, d, b_t=True, epi=EPI_BF16)
         delta = ws.get('b.delta', (B, heads, Lq), f32)
@@ -356,8 +355,7 @@ class VAEEngine:
                         delta=delta, dq=dq32, bdq=Lq * d, dk=dkv, dv=dkv[:, d:], sdk=2 * d, sdv=2 * d,
                         bdk=Sx * 2 * d, bdv=Sx * 2 * d, rot=rot, rot_d=d, o32=st['O32'], so32=d, bo32=Lq * d)
             K.colsum(dq32, B, Lq * d, Lq * d, P.g(a + 'learned_queries').view(-1))
-            self._dw(dkv, st['h'], a + 'k_linear.weight', rows_x, 2 * d, d)
-            self._db(dkv, a + 'k_linear.bias', rows_x, 2 * d)
+            self._dw(dkv, st['h'], a + 'k_linear.weight', rows_x, 2 * d, d, bias=a + 'k_linear.bias')
             dh = ws.get('b.dh', (rows_x, d))
             K.gemm(dkv, P.w(a + 'k_linear.weight'), dh, rows_x, d, 2 * d, b_t=True, epi=EPI_BF16)
         else:
@@ -370,8 +368,7 @@ class VAEEngine:
                         delta=delta, dq=dq32, bdq=Sx * d, dk=dqkv[:, d:], dv=dqkv[:, 2 * d:], sdk=3 * d, sdv=3 * d,
                         bdk=Sx * 3 * d, bdv=Sx * 3 * d, rot=rot, rot_d=d, o32=st['O32'], so32=d, bo32=Lq * d)
             K.dq_finalize(dq32, dqkv, 3 * d, rows_x, d, rot, Sx)
-            self._dw(dqkv, st['h'], a + 'q_linear.weight', rows_x, 3 * d, d)
-            self._db(dqkv, a + 'q_linear.bias', rows_x, 3 * d)
+            self._dw(dqkv, st['h'], a + 'q_linear.weight', rows_x, 3 * d, d, bias=a + 'q_linear.bias')
             dh = ws.get('b.dh', (rows_x, d))
             K.gemm(dqkv, P.w(a + 'q_linear.weight'), dh, rows_x, d, 3 * d, b_t=True, epi=EPI_BF16)
         if st['resid']:
@@ -535,16 +532,14 @@ class VAEEngine:
         # ---- head
         logits = sv['logits']
         K.ce_grad(logits, V, sv['lse'], sv['chunk_w'], sv['labels'], gs[0:1], T, V, L, sv['nchunks'], sv['chunk_len'])
-        self._dw(logits, sv['hh'], 'input_layer.0.weight', T, V, d)
-        self._db(logits, 'output_layer.3.bias', T, V)
+        self._dw(logits, sv['hh'], 'input_layer.0.weight', T, V, d, bias='output_layer.3.bias')
         dhh = ws.get('b.dhh', (T, d))
         K.gemm(logits, P.w('input_layer.0.weight'), dhh, T, d, V, b_t=True, epi=EPI_BF16)
         dh0 = ws.get('b.dh0', (T, d), f32)
         self._ln_bwd('output_layer.2', dhh, sv['ln_h'], T, None, dh0)
         dpre0 = ws.get('b.dpre0', (T, d))
         K.gelu_bwd(dh0, sv['pre0'], dpre0, T * d)
-        self._dw(dpre0, sv['xf'], 'output_layer.0.weight', T, d, d)
-        self._db(dpre0, 'output_layer.0.bias', T, d)
+        self._dw(dpre0, sv['xf'], 'output_layer.0.weight', T, d, d, bias='output_layer.0.bias')
         dx = ws.get('b.dx_dec', (T, d), f32)
         K.gemm(dpre0, P.w('output_layer.0.weight'), dx, T, d, d, b_t=True, epi=EPI_F32)
         ready(P.end('output_layer.3.bias'))

@@ -21,7 +21,7 @@ def _dev(*ts):
 
 def gemm(A, B, C, M, N_, K, *, a_t=False, b_t=False, lda=None, ldb=None, ldc=None, epi=N.EPI_BF16, bias=None,
          resid=None, ldr=0, aux=None, ldaux=0, alpha=1.0, splits=1, drop_p=0.0, seed=0, rot=None, rot_cols=0,
-         rot_d=0, rot_seq=0, labels=None, label_logit=None, batch=1, sA=0, sB=0, sC=0):
+         rot_d=0, rot_seq=0, labels=None, label_logit=None, batch=1, sA=0, sB=0, sC=0, a_rowsum=None):
     """C = epi(alpha * A . B) with A [M,K] (a_t: stored [K,M]) and B [K,N] (b_t: stored [K,N], else [N,K])."""
     _dev(A, B, C)
     assert A.dtype == bf16 and B.dtype == bf16
@@ -49,6 +49,7 @@ def gemm(A, B, C, M, N_, K, *, a_t=False, b_t=False, lda=None, ldb=None, ldc=Non
     d.rot_cols, d.rot_d, d.rot_seq = rot_cols, rot_d, rot_seq
     d.labels = ptr(labels)
     d.label_logit = ptr(label_logit)
+    d.a_rowsum = ptr(a_rowsum)
     check(lib.svae_gemm(ctypes.byref(d), stream()), 'svae_gemm')
 
 
@@ -60,11 +61,12 @@ def auto_splits(M, N_, K, target=512):
     return max(1, s)
 
 
-def linear_dw(dY, X, Wgrad, rows, n_out, n_in, ldy=None, ldx=None):
-    """Wgrad[n_out, n_in] += dY^T . X over `rows` rows (dY [rows, n_out] bf16, X [rows, n_in] bf16)."""
+def linear_dw(dY, X, Wgrad, rows, n_out, n_in, ldy=None, ldx=None, bgrad=None):
+    """Wgrad[n_out, n_in] += dY^T . X over `rows` rows (dY [rows, n_out] bf16, X [rows, n_in] bf16); with
+    bgrad, also bgrad[n_out] += column sums of dY (the bias gradient, fused into the same pass over dY)."""
     s = auto_splits(n_out, n_in, rows)
     gemm(dY, X, Wgrad, n_out, n_in, rows, a_t=True, b_t=True, lda=ldy or n_out, ldb=ldx or n_in, ldc=n_in,
-         epi=N.EPI_F32_ATOMIC if s > 1 else N.EPI_F32_ACC, splits=s)
+         epi=N.EPI_F32_ATOMIC if s > 1 else N.EPI_F32_ACC, splits=s, a_rowsum=bgrad)
 
 
 def layernorm_fwd(x, w, b, y, mean, rstd, rows, D):
@@ -145,9 +147,9 @@ def ce_finalize(part, ntile, label_logit, labels, rows, seq, nchunks, chunk_len,
                                nll.data_ptr(), stream()), 'svae_ce_finalize')
 
 
-def ce_grad(logits, ld, lse, chunk_w, labels, gscale, rows, V, seq, nchunks, chunk_len):
+def ce_grad(logits, ld, lse, chunk_w, labels, gscale, rows, V, seq, nchunks, chunk_len, dbias=None):
     check(lib.svae_ce_grad(logits.data_ptr(), ld, lse.data_ptr(), chunk_w.data_ptr(), labels.data_ptr(),
-                           gscale.data_ptr(), rows, V, seq, nchunks, chunk_len, stream()), 'svae_ce_grad')
+                           gscale.data_ptr(), ptr(dbias), rows, V, seq, nchunks, chunk_len, stream()), 'svae_ce_grad')
 
 
 def dropout_bwd_cast(g, out, p, seed, rows, cols, ld_in=None):

@@ -163,18 +163,21 @@ class TransformerVAE(ContinuousVAEHooks, LanguageModel):
     def enable_data_parallel(self, group=None, bucket_mb: float = 64.0):
         """Pure DP: grads are averaged with bucketed async all-reduces launched while the
         backward is still running (the arena is in gradient-ready order, so buckets are contiguous)."""
-        self._dp = {'group': group, 'bucket': int(bucket_mb * 2 ** 20 / 4), 'start': 0, 'works': []}
+        self._dp = {'group': group, 'bucket': int(bucket_mb * 2 ** 20 / 4), 'start': 0, 'works': [],
+                    'world': dist.get_world_size(group)}
         # identical initial weights on every rank
         dist.broadcast(self._flat.master, 0, group=group)
         self._flat.shadow_version = -1
 
     def _dp_ready(self, end, final=False):
+        """Called by the engine backward each time the arena prefix [0, end) holds final gradients."""
         dp = self._dp
         if dp is None:
             return
         if end - dp['start'] >= dp['bucket'] or (final and end > dp['start']):
             seg = self._flat.grad[dp['start']:end]
-            dp['works'].append(dist.all_reduce(seg, op=dist.ReduceOp.AVG, group=dp['group'], async_op=True))
+            # the backward ran on loss / world, so a SUM all-reduce leaves the average (no extra pass)
+            dp['works'].append(dist.all_reduce(seg, op=dist.ReduceOp.SUM, group=dp['group'], async_op=True))
             dp['start'] = end
 
     def _dp_finish(self):
@@ -242,7 +245,10 @@ class TransformerVAE(ContinuousVAEHooks, LanguageModel):
         eng = self._require_engine()
         if not self._grads_alive():
             self.zero_grad_flat()
-        eng.backward(gloss.reshape(()).to(torch.float32), self._kl_weight_used, ready=self._dp_ready)
+        g = gloss.reshape(()).to(torch.float32)
+        if self._dp is not None:
+            g = g / self._dp['world']
+        eng.backward(g, self._kl_weight_used, ready=self._dp_ready)
         self._dp_finish()
         self._norm_valid = False
 

@@ -1,0 +1,73 @@
+"""Data-parallel gradient averaging over world_size 2 on CPU (gloo): the model's real bucketing code
+(_dp_ready / _dp_finish over the gradient-ready flat arena), driven by the same ready() sequence the engine
+backward emits. On the GPU the backend is 'nccl' (RCCL) and the engine calls ready() itself."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _ready_sequence(flat, hp):
+    ends = [flat.end('output_layer.3.bias')]
+    ends += [flat.end(f'z_projections.{i}.bias') for i in reversed(range(hp.num_layers))]
+    ends.append(flat.end('q_of_z_given_x.linear.bias'))
+    ends.append(flat.end('encoder.bottleneck.ffn_layer_norm.bias'))
+    ends += [flat.end(f'encoder.middle_layers.{j}.ffn_layer_norm.bias') for j in reversed(range(hp.num_layers // 2 - 2))]
+    ends.append(flat.end('encoder.first_layer.ffn_layer_norm.bias'))
+    ends.append(flat.n_live)
+    return ends
+
+
+def _worker(rank, world, port, bucket_mb, q):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'sparse-vae_amd'))
+    from sparse_vae import TransformerVAE, TransformerVAEHparams
+    torch.manual_seed(100 + rank)                       # different init per rank: broadcast must unify
+    hp = TransformerVAEHparams(d_model=128, num_layers=6, num_heads=8, sparse_self_attention=False)
+    m = TransformerVAE(hp, device='cpu')
+    m.enable_data_parallel(bucket_mb=bucket_mb)
+    flat = m._flat
+    g = torch.arange(flat.total, dtype=torch.float32) * 1e-6 + rank
+    flat.grad.copy_(g / world)                         # the engine backward runs on loss / world
+    for end in _ready_sequence(flat, m._ehp):
+        m._dp_ready(end)
+    m._dp_finish()
+    live = flat.n_live
+    q.put((rank, flat.master[:1000].numpy().copy(), flat.grad[:live].numpy().copy(), flat.grad[live:].numpy().copy()))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('bucket_mb', [0.5, 64.0])
+def test_gradients_are_averaged_and_weights_broadcast(bucket_mb):
+    world = 2
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, bucket_mb, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda r: r[0])
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (_, w0, g0, d0), (_, w1, g1, d1) = [(r, *(torch.from_numpy(a) for a in t)) for r, *t in res]
+    assert torch.equal(w0, w1)                         # rank 0's weights everywhere
+    n = g0.numel()
+    expect = torch.arange(n, dtype=torch.float32) * 1e-6 + 0.5      # mean over ranks of (base + rank)
+    torch.testing.assert_close(g0, expect, rtol=1e-6, atol=1e-6)
+    assert torch.equal(g0, g1)
+    # gradients of parameters that never receive one (pos_linear) are not communicated
+    assert not torch.equal(d0, d1)

@@ -38,8 +38,11 @@ def test_gemm_split_k_atomic_and_acc():
     A = torch.randint(-2, 3, (4096, 256), device=dev).float()
     B = torch.randint(-2, 3, (4096, 384), device=dev).float()
     C = torch.ones(256, 384, device=dev)
-    K.gemm(A.bfloat16(), B.bfloat16(), C, 256, 384, 4096, a_t=True, b_t=True, epi=N.EPI_F32_ATOMIC, splits=4)
+    rs = torch.full((256,), 2.0, device=dev)
+    K.gemm(A.bfloat16(), B.bfloat16(), C, 256, 384, 4096, a_t=True, b_t=True, epi=N.EPI_F32_ATOMIC, splits=4,
+           a_rowsum=rs)
     assert torch.equal(C, 1 + A.t() @ B)
+    assert torch.equal(rs, 2 + A.sum(0))
     K.gemm(A.bfloat16(), B.bfloat16(), C, 256, 384, 4096, a_t=True, b_t=True, epi=N.EPI_F32_ACC)
     assert torch.equal(C, 1 + 2 * (A.t() @ B))
 
@@ -117,10 +120,12 @@ def test_ce_stats_epilogue_and_finalize():
     nll_ref = F.cross_entropy(ref, labels.long(), ignore_index=0)
     assert abs(nll.item() - nll_ref.item()) / nll_ref.item() < 1e-5
     gs = torch.ones(1, device=dev)
-    K.ce_grad(logits, V, lse, cw, labels, gs, T, V, L, 1, L)
+    db = torch.zeros(V, device=dev)
+    K.ce_grad(logits, V, lse, cw, labels, gs, T, V, L, 1, L, dbias=db)
     r = ref.clone().requires_grad_()
     F.cross_entropy(r, labels.long(), ignore_index=0).backward()
     assert _rel(logits, r.grad) < 1e-2
+    assert _rel(db, r.grad.sum(0)) < 1e-2
 
 
 @pytest.mark.parametrize('D,xdt', [(128, torch.float32), (384, torch.float32), (512, torch.bfloat16), (768, torch.float32)])
