@@ -10,6 +10,7 @@
 // b128 lane groups); M/N-contiguous tiles with ds_read_b64_tr_b16 (XOR-swizzled 8-B units).
 #include "common.h"
 #include "../../include/svae.h"
+#include <stdlib.h>
 
 using namespace svae;
 
@@ -100,8 +101,13 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GP p) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
 
-  // tile coordinates: consecutive blocks walk N first (A panel reuse in L2)
-  const int bid = blockIdx.x;
+  // tile coordinates: XCD-aware remap (see gemm_glds_kernel), then N first inside an XCD's range
+  const int nwg = p.tiles_n * p.tiles_m;
+  int bid = blockIdx.x;
+  if (nwg >= 16) {
+    const int q = nwg / 8, r = nwg % 8, xcd = bid % 8, idx = bid / 8;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+  }
   const int bn = bid % p.tiles_n, bm = bid / p.tiles_n;
   const int z = blockIdx.z;
   const int batch = z / p.splits, split = z % p.splits;
@@ -309,6 +315,283 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GP p) {
   }
 }
 
+// ===================================================================================================
+// gemm_glds: same contract, deeper pipeline. BK = 32, a 3-stage LDS ring filled by LDS-DMA
+// (buffer_load ... lds, 16 B per lane; out-of-range lanes read zeros from the buffer range check), so two
+// K-tiles are in flight while a third is consumed, with no staging registers and no ds_write pass.
+// 48 KiB of LDS and <= 168 VGPRs per block -> 3 blocks (12 waves) per CU overlap each other's prologue and
+// epilogue. The LDS image is lane-linear per wave instruction (1 KiB); the bank swizzle is applied on the
+// SOURCE address and undone on the fragment reads (K-contiguous: 64-B rows, chunk ^ ((row >> 1) & 3);
+// M/N-contiguous: 256-B rows, 16-B chunk ^ 2 s(k)).
+constexpr int BK2 = 32;
+constexpr int T2 = 128 * BK2 * 2;          // 8 KiB per operand tile
+constexpr int STAGE2 = 2 * T2;             // A + B
+constexpr int NSTAGE = 3;
+
+__device__ __forceinline__ int kc2_off(int row, int c) { return row * 64 + ((c ^ ((row >> 1) & 3)) << 4); }
+
+template <bool TRANS>
+__device__ __forceinline__ void issue_tile2(const bf16* __restrict__ g, long long ld, int row0, int nrows, int k0,
+                                            int kend, char* lds_tile, int wave, int lane) {
+  const bf16* base = TRANS ? g + (long long)k0 * ld + row0 : g + (long long)row0 * ld + k0;
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, 0x7FFFFFF0, 0x00020000);
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int inst = wave * 2 + j;
+    const int slot = inst * 64 + lane;
+    int off;
+    bool ok;
+    if (!TRANS) {
+      const int row = slot >> 2, c = (slot & 3) ^ ((row >> 1) & 3);
+      off = (row * (int)ld + c * 8) * 2;
+      ok = (row0 + row < nrows) && (k0 + c * 8 < kend);
+    } else {
+      const int kr = slot >> 4;
+      const int sk = (kr & 3) | (((kr >> 3) & 1) << 2);
+      const int v = (slot & 15) ^ (sk << 1);
+      off = (kr * (int)ld + v * 8) * 2;
+      ok = (k0 + kr < kend) && (row0 + v * 8 < nrows);
+    }
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void*)(lds_tile + inst * 1024), 16,
+                                             ok ? off : 0x7FFFFFF0, 0, 0, 0);
+  }
+}
+
+template <bool TRANS>
+__device__ __forceinline__ bf16x8 read_frag2(const char* lds, int base, int lane) {
+  if (!TRANS) {
+    return *(const bf16x8*)(lds + kc2_off(base + (lane & 15), lane >> 4));
+  } else {
+    const int q = (lane & 15) >> 2, p = lane & 3;
+    const int kb = 8 * (lane >> 4) + q;
+    const int u = (base >> 2) + p;
+    return cat44(lds_read_tr(lds + mn_off(kb, u)), lds_read_tr(lds + mn_off(kb + 4, u)));
+  }
+}
+
+// f32 staging rows for the epilogue (64 rows x 128 cols per half)
+template <int EPI>
+__device__ __forceinline__ void epilogue_half(const GP& p, const float* cs, int m0, int n0, int bn, int rbase,
+                                              long long cofs, int tid) {
+  if constexpr (EPI == SVAE_EPI_F32_ATOMIC) {
+    const int col = tid & 127, n = n0 + col;
+    if (n < p.N) {
+      for (int it = 0; it < 32; ++it) {
+        const int row = (tid >> 7) + 2 * it, m = m0 + rbase + row;
+        if (m < p.M) atomicAdd((float*)p.C + cofs + (long long)m * p.ldc + n, cs[row * 128 + cs_swz(row, col)]);
+      }
+    }
+    return;
+  }
+  const int cc = (tid & 31) * 4;
+  const int n = n0 + cc;
+  const bool ncol = n < p.N;
+  f32x4 bias = {0.f, 0.f, 0.f, 0.f};
+  if (p.bias && ncol) bias = *(const f32x4*)(p.bias + n);
+  if constexpr (EPI == SVAE_EPI_CE_STATS) {
+#pragma unroll 4
+    for (int it = 0; it < 8; ++it) {
+      const int row = (tid >> 5) + 8 * it, m = m0 + rbase + row;
+      if (m >= p.M || !ncol) continue;
+      const f32x4 v = *(const f32x4*)(cs + row * 128 + cs_swz(row, cc)) + bias;
+      *(bf16x4*)((bf16*)p.C + cofs + (long long)m * p.ldc + n) = (bf16x4){f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
+    }
+    // per row: 4 threads x 32 columns -> (max, sumexp), label logit
+    const int row = tid >> 2, qd = tid & 3, m = m0 + rbase + row;
+    float v[32];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int c = qd * 32 + 4 * u;
+      f32x4 x = *(const f32x4*)(cs + row * 128 + cs_swz(row, c));
+      if (p.bias) x += (n0 + c < p.N) ? *(const f32x4*)(p.bias + n0 + c) : (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float y = (n0 + c + e < p.N) ? x[e] : -INFINITY;
+        v[4 * u + e] = y;
+        mx = fmaxf(mx, y);
+      }
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 1, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 2, 64));
+    float se = 0.f;
+#pragma unroll
+    for (int e = 0; e < 32; ++e) se += __expf(v[e] - mx);
+    se += __shfl_xor(se, 1, 64);
+    se += __shfl_xor(se, 2, 64);
+    if (m < p.M) {
+      const int lc = p.labels[m] - n0 - qd * 32;
+      if (lc >= 0 && lc < 32) {
+#pragma unroll
+        for (int e = 0; e < 32; ++e)
+          if (e == lc) p.label_logit[m] = v[e];
+      }
+      if (qd == 0) {
+        float* part = (float*)p.aux + ((long long)m * p.tiles_n + bn) * 2;
+        part[0] = mx;
+        part[1] = se;
+      }
+    }
+    return;
+  }
+#pragma unroll 4
+  for (int it = 0; it < 8; ++it) {
+    const int row = (tid >> 5) + 8 * it, m = m0 + rbase + row;
+    if (m >= p.M || !ncol) continue;
+    f32x4 x = *(const f32x4*)(cs + row * 128 + cs_swz(row, cc));
+    const long long ci = cofs + (long long)m * p.ldc + n;
+    if constexpr (EPI == SVAE_EPI_BF16) {
+      x += bias;
+      *(bf16x4*)((bf16*)p.C + ci) = (bf16x4){f2bf(x[0]), f2bf(x[1]), f2bf(x[2]), f2bf(x[3])};
+    } else if constexpr (EPI == SVAE_EPI_ROTARY_BF16) {
+      x += bias;
+      if (n < p.rot_cols) {
+        const int pos = m % p.rot_seq;
+        const int pair = (n % p.rot_d) >> 1;
+        const f32x4 cs2 = *(const f32x4*)(p.rot_tab + ((long long)pos * (p.rot_d >> 1) + pair) * 2);
+        const float a0 = x[0], b0 = x[1], a1 = x[2], b1 = x[3];
+        x[0] = a0 * cs2[0] + (-b0) * cs2[1];
+        x[1] = b0 * cs2[0] + a0 * cs2[1];
+        x[2] = a1 * cs2[2] + (-b1) * cs2[3];
+        x[3] = b1 * cs2[2] + a1 * cs2[3];
+      }
+      *(bf16x4*)((bf16*)p.C + ci) = (bf16x4){f2bf(x[0]), f2bf(x[1]), f2bf(x[2]), f2bf(x[3])};
+    } else if constexpr (EPI == SVAE_EPI_F32) {
+      x += bias;
+      if (p.resid) x += *(const f32x4*)(p.resid + (long long)m * p.ldr + n);
+      *(f32x4*)((float*)p.C + ci) = x;
+    } else if constexpr (EPI == SVAE_EPI_F32_ACC) {
+      *(f32x4*)((float*)p.C + ci) = *(const f32x4*)((float*)p.C + ci) + x;
+    } else if constexpr (EPI == SVAE_EPI_GELU) {
+      x += bias;
+      *(bf16x4*)((bf16*)p.aux + (long long)m * p.ldaux + n) = (bf16x4){f2bf(x[0]), f2bf(x[1]), f2bf(x[2]), f2bf(x[3])};
+      *(bf16x4*)((bf16*)p.C + ci) = (bf16x4){f2bf(gelu_f(x[0])), f2bf(gelu_f(x[1])), f2bf(gelu_f(x[2])), f2bf(gelu_f(x[3]))};
+    } else if constexpr (EPI == SVAE_EPI_GELU_BWD) {
+      const bf16x4 pre = *(const bf16x4*)((const bf16*)p.aux + (long long)m * p.ldaux + n);
+      *(bf16x4*)((bf16*)p.C + ci) = (bf16x4){f2bf(x[0] * gelu_grad_f((float)pre[0])), f2bf(x[1] * gelu_grad_f((float)pre[1])),
+                                              f2bf(x[2] * gelu_grad_f((float)pre[2])), f2bf(x[3] * gelu_grad_f((float)pre[3]))};
+    } else if constexpr (EPI == SVAE_EPI_DROPOUT_RESID) {
+      if (p.drop_p > 0.f) {
+        const float sc = 1.0f / (1.0f - p.drop_p);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float u = rand_uniform(p.seed, (unsigned long long)m * p.N + n + e);
+          x[e] = (u >= p.drop_p) ? x[e] * sc : 0.f;
+        }
+      }
+      *(f32x4*)((float*)p.C + ci) = *(const f32x4*)(p.resid + (long long)m * p.ldr + n) + x;
+    }
+  }
+}
+
+template <bool AT, bool BT, int EPI>
+__global__ __launch_bounds__(256, 3) void gemm_glds_kernel(GP p) {
+  __shared__ __attribute__((aligned(16))) char smem[NSTAGE * STAGE2];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int nwg = p.tiles_n * p.tiles_m;
+  int bid = blockIdx.x;
+  if (nwg >= 16) {
+    const int q = nwg / 8, r = nwg % 8, xcd = bid % 8, idx = bid / 8;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+  }
+  const int bn = bid % p.tiles_n, bm = bid / p.tiles_n;
+  const int z = blockIdx.z;
+  const int batch = z / p.splits, split = z % p.splits;
+  const int m0 = bm * BM, n0 = bn * BN;
+  const int kbeg = split * p.kchunk;
+  const int kend = min(p.K, kbeg + p.kchunk);
+  const bf16* A = p.A + batch * p.sA;
+  const bf16* B = p.B + batch * p.sB;
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float rsum[4] = {0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (kend - kbeg + BK2 - 1) / BK2;
+  if (nk > 0) {
+    issue_tile2<AT>(A, p.lda, m0, p.M, kbeg, kend, smem, wave, lane);
+    issue_tile2<BT>(B, p.ldb, n0, p.N, kbeg, kend, smem + T2, wave, lane);
+  }
+  if (nk > 1) {
+    issue_tile2<AT>(A, p.lda, m0, p.M, kbeg + BK2, kend, smem + STAGE2, wave, lane);
+    issue_tile2<BT>(B, p.ldb, n0, p.N, kbeg + BK2, kend, smem + STAGE2 + T2, wave, lane);
+  }
+  int stage = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    // tile kt landed (this wave's 4 DMA pieces of tile kt+1 may still fly), then everyone's pieces + the
+    // ring slot of tile kt+2 (last read in iteration kt-1) is free
+    if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (kt + 2 < nk) {
+      int s2 = stage + 2;
+      if (s2 >= NSTAGE) s2 -= NSTAGE;
+      char* st2 = smem + s2 * STAGE2;
+      issue_tile2<AT>(A, p.lda, m0, p.M, kbeg + (kt + 2) * BK2, kend, st2, wave, lane);
+      issue_tile2<BT>(B, p.ldb, n0, p.N, kbeg + (kt + 2) * BK2, kend, st2 + T2, wave, lane);
+    }
+    const char* la = smem + stage * STAGE2;
+    const char* lb = la + T2;
+    bf16x8 af[4], bfr[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) af[i] = read_frag2<AT>(la, wm * 64 + i * 16, lane);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bfr[j] = read_frag2<BT>(lb, wn * 64 + j * 16, lane);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+    if constexpr (AT) {
+      if (p.a_rowsum && bn == 0) {   // sum_k A[m][k]: 4 columns x 4 k-rows per thread
+        const int mu = tid & 31, kg = tid >> 5;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const short4v v = *(const short4v*)(la + mn_off(kg * 4 + r, mu));
+          const bf16x4 b = __builtin_bit_cast(bf16x4, v);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) rsum[e] += (float)b[e];
+        }
+      }
+    }
+    stage = stage + 1 == NSTAGE ? 0 : stage + 1;
+  }
+  if constexpr (AT) {
+    if (p.a_rowsum && bn == 0) {
+      const int m = m0 + (tid & 31) * 4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (m + e < p.M) atomicAdd(p.a_rowsum + m + e, rsum[e]);
+    }
+  }
+  __syncthreads();
+  // epilogue in two halves of 64 rows (the ring holds 48 KiB; a half tile of f32 is 32 KiB)
+  float* cs = (float*)smem;
+  const long long cofs = (long long)batch * p.sC;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    if (wm == h) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = i * 16 + 4 * (lane >> 4) + r;
+            const int col = wn * 64 + j * 16 + (lane & 15);
+            cs[row * 128 + cs_swz(row, col)] = p.alpha * acc[i][j][r];
+          }
+    }
+    __syncthreads();
+    epilogue_half<EPI>(p, cs, m0, n0, bn, h * 64, cofs, tid);
+    __syncthreads();
+  }
+}
+
 }  // namespace
 
 SVAE_EXPORT int svae_gemm(const svae_gemm_desc* d, svae_stream_t stream) {
@@ -352,6 +635,37 @@ SVAE_EXPORT int svae_gemm(const svae_gemm_desc* d, svae_stream_t stream) {
   dim3 grid(p.tiles_n * p.tiles_m, 1, d->batch * d->splits);
   hipStream_t s = (hipStream_t)stream;
   const int lay = (d->a_t ? 2 : 0) | (d->b_t ? 1 : 0);
+  // short-K GEMMs: the 3-stage LDS-DMA kernel (3 blocks/CU overlap prologues/epilogues); long-K GEMMs: the
+  // BK=64 register-staged kernel (half the barriers per MFMA). SVAE_GEMM_IMPL=1/2 forces one (A/B runs).
+  static const int forced = [] { const char* e = getenv("SVAE_GEMM_IMPL"); return e ? atoi(e) : 0; }();
+  const int kslice = (d->K + d->splits - 1) / d->splits;
+  const int impl = forced ? forced : ((kslice <= 2048 && !(d->a_t && d->b_t)) ? 2 : 1);
+  if (impl == 2) {
+    int kchunk2 = (d->K + d->splits - 1) / d->splits;
+    p.kchunk = (kchunk2 + BK2 - 1) / BK2 * BK2;
+#define SVAE_GEMM2_CASE(E)                                                                             \
+  case E:                                                                                              \
+    if (lay == 0) hipLaunchKernelGGL((gemm_glds_kernel<false, false, E>), grid, dim3(256), 0, s, p);    \
+    else if (lay == 1) hipLaunchKernelGGL((gemm_glds_kernel<false, true, E>), grid, dim3(256), 0, s, p); \
+    else if (lay == 2) hipLaunchKernelGGL((gemm_glds_kernel<true, false, E>), grid, dim3(256), 0, s, p); \
+    else hipLaunchKernelGGL((gemm_glds_kernel<true, true, E>), grid, dim3(256), 0, s, p);                \
+    break;
+    switch (d->epi) {
+      SVAE_GEMM2_CASE(SVAE_EPI_BF16)
+      SVAE_GEMM2_CASE(SVAE_EPI_F32)
+      SVAE_GEMM2_CASE(SVAE_EPI_F32_ACC)
+      SVAE_GEMM2_CASE(SVAE_EPI_F32_ATOMIC)
+      SVAE_GEMM2_CASE(SVAE_EPI_GELU)
+      SVAE_GEMM2_CASE(SVAE_EPI_GELU_BWD)
+      SVAE_GEMM2_CASE(SVAE_EPI_DROPOUT_RESID)
+      SVAE_GEMM2_CASE(SVAE_EPI_ROTARY_BF16)
+      SVAE_GEMM2_CASE(SVAE_EPI_CE_STATS)
+      default: return SVAE_EINVAL;
+    }
+#undef SVAE_GEMM2_CASE
+    SVAE_LAUNCH_CHECK();
+    return SVAE_OK;
+  }
 #define SVAE_GEMM_CASE(E)                                                                             \
   case E:                                                                                             \
     if (lay == 0) hipLaunchKernelGGL((gemm_kernel<false, false, E>), grid, dim3(256), 0, s, p);        \
