@@ -125,10 +125,20 @@ def parity_check(device):
     out = eng.forward(ids.to(device), ntok.to(device), eps=eps.to(device), dropout=0.0, kl_weight=0.7)
     loss, nll, kl = out['loss'].item(), out['nll'].item(), out['kl'].item()
     elbo, elbo_ref = -(nll + kl), -(ref['nll'].item() + ref['kl'].item())
+    # argmax reconstructions at z = mu: fp32 kernel mode vs the CPU fp32 path
+    from sparse_vae import kernels as K
+    x = torch.empty(B * L, 512, device=device)
+    K.embedding_fwd(ids.to(torch.int32).to(device), flat.f('input_layer.0.weight'), x, B * L, 512)
+    mu = out['mu'].clone()
+    am_gpu = eng.reconstruct_f32(x.view(B, L, 512), mu)[:, :-1].argmax(-1).cpu()
+    with torch.no_grad():
+        xr = torch.nn.functional.embedding(ids, params['input_layer.0.weight'])
+        am_ref = oracle.reconstruct(params, xr, mu.cpu().view(B, 1, 64), ids.eq(0), hp)[:, :-1].argmax(-1)
     return {'config': 'C2 model (6L d512 L512) batch 2, dropout off, injected eps',
             'loss_gpu': loss, 'loss_cpu_ref': ref['loss'].item(),
             'loss_rel_err': abs(loss - ref['loss'].item()) / abs(ref['loss'].item()),
-            'elbo_rel_err': abs(elbo - elbo_ref) / abs(elbo_ref), 'tolerance': 1e-3}
+            'elbo_rel_err': abs(elbo - elbo_ref) / abs(elbo_ref), 'tolerance': 1e-3,
+            'argmax_fp32_mode_agreement': (am_gpu == am_ref).float().mean().item()}
 
 
 def main():

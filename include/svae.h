@@ -174,6 +174,21 @@ int svae_sumsq(const float* g, int64_t n, float* part, int32_t nblk, svae_stream
 int svae_radam(float* p, void* pbf, const float* g, float* m, float* v, int64_t n, const float* part,
                int32_t nblk, const float* scal, float* norm_out, svae_stream_t stream);
 
+/* ---- fp32 kernel mode (argmax-reconstruction parity; TransformerVAE.reconstruct in exact f32) ---------
+ * svae_gemm_f32: C[M,N] = epi(A[M,K] . W[N,K]^T) on f32-input MFMA; epi in {SVAE_EPI_F32 (+bias, +resid),
+ * SVAE_EPI_ROTARY_BF16 (rotary on cols < rot_cols, f32 out), SVAE_EPI_GELU (f32 out)}.
+ * svae_attn_fwd_f32: dense attention forward in f32 (same strides / masks as svae_attn_desc).
+ * svae_layernorm_fwd_f32: LayerNorm with f32 output. */
+int svae_gemm_f32(const float* A, const float* W, float* C, int32_t M, int32_t N, int32_t K, int64_t lda, int64_t ldw,
+                  int64_t ldc, const float* bias, const float* resid, int64_t ldr, int32_t epi, const float* rot_tab,
+                  int32_t rot_cols, int32_t rot_d, int32_t rot_seq, svae_stream_t stream);
+int svae_attn_fwd_f32(const float* q, const float* k, const float* v, float* o, int64_t sq, int64_t sk, int64_t sv,
+                      int64_t so, int64_t bq, int64_t bk, int64_t bv, int64_t bo, const uint8_t* key_pad, int32_t B,
+                      int32_t H, int32_t Lq, int32_t Lk, int32_t hd, int32_t causal, float scale,
+                      svae_stream_t stream);
+int svae_layernorm_fwd_f32(const float* x, const float* w, const float* b, float* y, int32_t rows, int32_t D,
+                           svae_stream_t stream);
+
 /* library identification: returns a static string (build id, target arch). */
 const char* svae_version(void);
 

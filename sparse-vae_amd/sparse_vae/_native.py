@@ -83,6 +83,12 @@ _SIGS = {
     'svae_sumsq': [c_void_p, c_int64, c_void_p, c_int32, c_void_p],
     'svae_radam': [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_int32, c_void_p,
                    c_void_p, c_void_p],
+    'svae_gemm_f32': [c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_int32, c_int64, c_int64, c_int64, c_void_p,
+                      c_void_p, c_int64, c_int32, c_void_p, c_int32, c_int32, c_int32, c_void_p],
+    'svae_attn_fwd_f32': [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_int64, c_int64, c_int64,
+                          c_int64, c_int64, c_void_p, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, c_float,
+                          c_void_p],
+    'svae_layernorm_fwd_f32': [c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p],
     'svae_version': [],
 }
 

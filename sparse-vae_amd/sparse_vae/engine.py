@@ -491,6 +491,45 @@ class VAEEngine:
             dec.append(st)
         return xs, dec
 
+    def reconstruct_f32(self, x_emb, z, pad=None):
+        """reconstruct() in the fp32 kernel mode (f32-input MFMA GEMMs, f32 attention / LayerNorm): logits
+        [B, L, V] f32 for the bit-exact argmax check against the fp32 reference."""
+        hp, d, P = self.hp, self.d, self.P
+        dev = P.device
+        B, L = x_emb.shape[0], x_emb.shape[1]
+        T, V, Z, H, hd = B * L, hp.vocab_size, hp.latent_depth, self.H, self.hd
+        rot = self.rot(L)
+        padm = None
+        if pad is not None:
+            padm = torch.empty(B, L, dtype=torch.uint8, device=dev)
+            padm.copy_(pad)
+        x = x_emb.reshape(T, d).clone()
+        h = torch.empty(T, d, device=dev)
+        qkv = torch.empty(T, 3 * d, device=dev)
+        o = torch.empty(T, d, device=dev)
+        x1 = torch.empty(T, d, device=dev)
+        f = torch.empty(T, 4 * d, device=dev)
+        for i in range(hp.num_layers):
+            pre = f'decoder_layers.{i}.'
+            a = pre + 'attention.'
+            # position 0 <- z_projections[i](z)   (transformer_vae.py:89-90)
+            K.gemm_f32(z, P.f(f'z_projections.{i}.weight'), x, B, d, Z, ldc=L * d, bias=P.f(f'z_projections.{i}.bias'))
+            K.layernorm_fwd_f32(x, P.f(pre + 'attn_layer_norm.weight'), P.f(pre + 'attn_layer_norm.bias'), h, T, d)
+            K.gemm_f32(h, P.f(a + 'q_linear.weight'), qkv, T, 3 * d, d, epi=EPI_ROTARY_BF16, bias=P.f(a + 'q_linear.bias'),
+                       rot=rot, rot_cols=2 * d, rot_d=d, rot_seq=L)
+            K.attention_f32(qkv, qkv[:, d:], qkv[:, 2 * d:], o, B=B, H=H, Lq=L, Lk=L, hd=hd, sq=3 * d, sk=3 * d,
+                            sv=3 * d, so=d, bq=L * 3 * d, bk=L * 3 * d, bv=L * 3 * d, bo=L * d, key_pad=padm, causal=True)
+            K.gemm_f32(o, P.f(a + 'output_linear.weight'), x1, T, d, d, bias=P.f(a + 'output_linear.bias'), resid=x, ldr=d)
+            K.layernorm_fwd_f32(x1, P.f(pre + 'ffn_layer_norm.weight'), P.f(pre + 'ffn_layer_norm.bias'), h, T, d)
+            K.gemm_f32(h, P.f(pre + 'ffn.0.weight'), f, T, 4 * d, d, epi=EPI_GELU, bias=P.f(pre + 'ffn.0.bias'))
+            K.gemm_f32(f, P.f(pre + 'ffn.2.weight'), x, T, d, 4 * d, resid=x1, ldr=d)
+        h0 = torch.empty(T, d, device=dev)
+        K.gemm_f32(x, P.f('output_layer.0.weight'), h0, T, d, d, epi=EPI_GELU, bias=P.f('output_layer.0.bias'))
+        K.layernorm_fwd_f32(h0, P.f('output_layer.2.weight'), P.f('output_layer.2.bias'), h, T, d)
+        logits = torch.empty(B, L, V, device=dev)
+        K.gemm_f32(h, P.f('input_layer.0.weight'), logits, T, V, d, bias=P.f('output_layer.3.bias'))
+        return logits
+
     def reconstruct(self, x_emb, z, pad=None):
         """TransformerVAE.reconstruct (transformer_vae.py:85-93): decoder + head logits [B, L, V] bf16 from
         x_emb f32 [B, L, d] and z f32 [B, latent]; pad = [B, L] mask or None."""

@@ -177,3 +177,22 @@ def sumsq(g, n, part):
 def radam(p, pbf, g, m, v, n, part, scal, norm_out):
     check(lib.svae_radam(p.data_ptr(), ptr(pbf), g.data_ptr(), m.data_ptr(), v.data_ptr(), n, part.data_ptr(),
                          part.numel(), scal.data_ptr(), ptr(norm_out), stream()), 'svae_radam')
+
+
+# ---- fp32 kernel mode (argmax-reconstruction parity)
+def gemm_f32(A, W, C, M, N_, K_, *, lda=None, ldw=None, ldc=None, epi=N.EPI_F32, bias=None, resid=None, ldr=0,
+             rot=None, rot_cols=0, rot_d=0, rot_seq=0):
+    _dev(A, W, C)
+    check(lib.svae_gemm_f32(A.data_ptr(), W.data_ptr(), C.data_ptr(), M, N_, K_, lda or K_, ldw or K_, ldc or N_,
+                            ptr(bias), ptr(resid), ldr, epi, ptr(rot), rot_cols, rot_d, rot_seq, stream()),
+          'svae_gemm_f32')
+
+
+def attention_f32(q, k, v, o, *, B, H, Lq, Lk, hd, sq, sk, sv, so, bq, bk, bv, bo, key_pad=None, causal=False):
+    check(lib.svae_attn_fwd_f32(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), sq, sk, sv, so, bq, bk, bv, bo,
+                                ptr(key_pad), B, H, Lq, Lk, hd, int(causal), hd ** -0.5, stream()), 'svae_attn_fwd_f32')
+
+
+def layernorm_fwd_f32(x, w, b, y, rows, D):
+    check(lib.svae_layernorm_fwd_f32(x.data_ptr(), w.data_ptr(), b.data_ptr(), y.data_ptr(), rows, D, stream()),
+          'svae_layernorm_fwd_f32')

@@ -269,13 +269,18 @@ class TransformerVAE(ContinuousVAEHooks, LanguageModel):
 
     # ------------------------------------------------------------------ inference-side helpers
     @torch.no_grad()
-    def reconstruct(self, x, z):
+    def reconstruct(self, x, z, precision: str = 'bf16'):
         """transformer_vae.py:85-93 on the device (no autograd): x = input_layer(ids) [B, L, d] f32 (a
-        PaddedTensor carrying the padding mask, or plain), z [B, 1, latent] -> logits [B, L, V] (bf16)."""
+        PaddedTensor carrying the padding mask, or plain), z [B, 1, latent] -> logits [B, L, V]: bf16 from the
+        training kernels, or f32 from the fp32 kernel mode (precision='fp32', the argmax-parity mode)."""
         eng = self._require_engine()
         pad = getattr(x, 'padding', None)
         x = x.as_raw() if isinstance(x, PaddedTensor) else x
-        return eng.reconstruct(x.float().contiguous(), z.reshape(z.shape[0], -1).float().contiguous(), pad)
+        x = x.float().contiguous()
+        z = z.reshape(z.shape[0], -1).float().contiguous()
+        if precision == 'fp32':
+            return eng.reconstruct_f32(x, z, pad)
+        return eng.reconstruct(x, z, pad)
 
     @torch.no_grad()
     def embed(self, ids):
