@@ -37,8 +37,8 @@ enum svae_epi {
   SVAE_EPI_F32 = 1,           /* C f32  = alpha*acc + bias (+ resid)                                  */
   SVAE_EPI_F32_ACC = 2,       /* C f32 += alpha*acc                                                   */
   SVAE_EPI_F32_ATOMIC = 3,    /* atomicAdd(C f32, alpha*acc)   (split-K / shared destinations)        */
-  SVAE_EPI_GELU = 4,          /* aux bf16 = acc + bias;  C bf16 = gelu(acc + bias)                     */
-  SVAE_EPI_GELU_BWD = 5,      /* C bf16 = acc * gelu'(aux)                                             */
+  SVAE_EPI_GELU = 4,          /* C bf16 = gelu(acc + bias);  aux bf16 = gelu'(acc + bias)              */
+  SVAE_EPI_GELU_BWD = 5,      /* C bf16 = acc * aux  (aux = the gelu' saved by SVAE_EPI_GELU)          */
   SVAE_EPI_DROPOUT_RESID = 6, /* C f32 = resid + keep(seed, m*N+n) * acc / (1 - p)                     */
   SVAE_EPI_ROTARY_BF16 = 7,   /* C bf16 = rotary(acc + bias) on cols < rot_cols (attention.py:194-208) */
   SVAE_EPI_CE_STATS = 8       /* C bf16 = acc + bias; per (row, 128-col tile) online (max, sumexp) to
@@ -157,8 +157,9 @@ int svae_ce_grad(void* logits, int64_t ld, const float* lse, const float* chunk_
 /* dropout backward + cast: out bf16 = keep(seed, idx) * g / (1-p) (p = 0: plain cast). */
 int svae_dropout_bwd_cast(const float* g, void* out, float p, uint64_t seed, int64_t n, int32_t cols,
                           int64_t ld_in, svae_stream_t stream);
-/* GELU backward (transformer_language_model.py:57 head GELU): out bf16 = dx * gelu'(pre). */
-int svae_gelu_bwd(const float* dx, const void* pre, void* out, int64_t n, svae_stream_t stream);
+/* GELU backward (transformer_language_model.py:57 head GELU): out bf16 = dx * gp, gp = gelu' saved by the
+   forward's SVAE_EPI_GELU epilogue. */
+int svae_gelu_bwd(const float* dx, const void* gp, void* out, int64_t n, svae_stream_t stream);
 /* cast f32 -> bf16 (n elements). */
 int svae_cast_bf16(const float* in, void* out, int64_t n, svae_stream_t stream);
 /* rows of x (f32 [rows][D], stride ld) whose (row % mod == 0) are copied to out [rows/mod][D] and zeroed

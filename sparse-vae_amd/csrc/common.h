@@ -58,6 +58,21 @@ __device__ __forceinline__ float gelu_grad_f(float x) {
   return cdf + x * pdf;
 }
 
+// GELU and GELU' together for the GEMM epilogues: Phi(x) from erfc(|x|/sqrt2) by Abramowitz-Stegun 7.1.26
+// (|erf error| <= 1.5e-7, branchless: one v_rcp, one v_exp, 7 FMAs), and phi(x) = exp(-x^2/2)/sqrt(2 pi)
+// reusing the same exponential. ~1/5 of the instructions of the erff-based pair above.
+__device__ __forceinline__ void gelu_pair(float x, float& g, float& gp) {
+  const float z = fabsf(x) * 0.70710678118654752f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.0f));
+  const float poly =
+      t * fmaf(t, fmaf(t, fmaf(t, fmaf(t, 1.061405429f, -1.453152027f), 1.421413741f), -0.284496736f), 0.254829592f);
+  const float e = __expf(-z * z);             // exp(-x^2 / 2)
+  const float half_erfc = 0.5f * poly * e;    // Phi(-|x|)
+  const float cdf = x >= 0.f ? 1.0f - half_erfc : half_erfc;
+  g = x * cdf;
+  gp = fmaf(x * 0.3989422804014327f, e, cdf);
+}
+
 // Counter-based RNG (splitmix64 finaliser over (seed, counter)): stateless, so the backward pass
 // regenerates exactly the forward's dropout mask / noise from the same (seed, index).
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
@@ -68,6 +83,17 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
 __device__ __forceinline__ float rand_uniform(uint64_t seed, uint64_t idx) {
   uint64_t r = mix64(seed * 0x9E3779B97F4A7C15ull + idx + 0x632BE59BD9B4E019ull);
   return ((uint32_t)(r >> 40) + 0.5f) * (1.0f / 16777216.0f);
+}
+// Dropout: the four uniforms of elements 4q..4q+3 (row-major index / 4) from ONE hash, 16 bits each
+// (keep-probability resolution 2^-16). Shared by the forward epilogue and the backward mask kernel.
+__device__ __forceinline__ void rand_uniform4(uint64_t seed, uint64_t q, float (&u)[4]) {
+  const uint64_t r = mix64(seed * 0x9E3779B97F4A7C15ull + q + 0x632BE59BD9B4E019ull);
+  const uint32_t lo = (uint32_t)r, hi = (uint32_t)(r >> 32);
+  const float s = 1.0f / 65536.0f;
+  u[0] = ((lo & 0xffffu) + 0.5f) * s;
+  u[1] = ((lo >> 16) + 0.5f) * s;
+  u[2] = ((hi & 0xffffu) + 0.5f) * s;
+  u[3] = ((hi >> 16) + 0.5f) * s;
 }
 
 }  // namespace svae

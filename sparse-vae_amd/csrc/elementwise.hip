@@ -208,20 +208,22 @@ __global__ __launch_bounds__(256) void dropout_bwd_cast_kernel(const float* __re
     const int c = (int)(i % cols);
     const f32x4 v = *(const f32x4*)(g + r * ld_in + c);
     bf16x4 o;
+    float u[4] = {1.f, 1.f, 1.f, 1.f};
+    if (p > 0.f) rand_uniform4(seed, (unsigned long long)i >> 2, u);
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       float x = v[e];
-      if (p > 0.f) x = (rand_uniform(seed, (unsigned long long)(i + e)) >= p) ? x * scale : 0.f;
+      if (p > 0.f) x = (u[e] >= p) ? x * scale : 0.f;
       o[e] = f2bf(x);
     }
     *(bf16x4*)(out + i) = o;
   }
 }
 
-__global__ __launch_bounds__(256) void gelu_bwd_kernel(const float* __restrict__ dx, const bf16* __restrict__ pre,
+__global__ __launch_bounds__(256) void gelu_bwd_kernel(const float* __restrict__ dx, const bf16* __restrict__ gp,
                                                        bf16* __restrict__ out, long long n) {
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256)
-    out[i] = f2bf(dx[i] * gelu_grad_f((float)pre[i]));
+    out[i] = f2bf(dx[i] * (float)gp[i]);
 }
 
 __global__ __launch_bounds__(256) void cast_kernel(const float* __restrict__ in, bf16* __restrict__ out, long long n) {
@@ -401,9 +403,9 @@ SVAE_EXPORT int svae_dropout_bwd_cast(const float* g, void* out, float p, uint64
   return SVAE_OK;
 }
 
-SVAE_EXPORT int svae_gelu_bwd(const float* dx, const void* pre, void* out, int64_t n, svae_stream_t stream) {
-  if (!dx || !pre || !out || n <= 0) return SVAE_EINVAL;
-  hipLaunchKernelGGL(gelu_bwd_kernel, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream, dx, (const bf16*)pre,
+SVAE_EXPORT int svae_gelu_bwd(const float* dx, const void* gp, void* out, int64_t n, svae_stream_t stream) {
+  if (!dx || !gp || !out || n <= 0) return SVAE_EINVAL;
+  hipLaunchKernelGGL(gelu_bwd_kernel, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream, dx, (const bf16*)gp,
                      (bf16*)out, n);
   SVAE_LAUNCH_CHECK();
   return SVAE_OK;

@@ -95,6 +95,182 @@ __device__ __forceinline__ bf16x8 read_frag(const char* lds, int base, int kk, i
 // f32 staging tile [128][128] for the epilogue: 16-B unit index XOR ((row >> 2) & 3) << 2
 __device__ __forceinline__ int cs_swz(int row, int col) { return (((col >> 2) ^ (((row >> 2) & 3) << 2)) << 2) | (col & 3); }
 
+__device__ __forceinline__ void store_bf16(bf16* dst, const f32x4& a, const f32x4& b, bool full) {
+  if (full)
+    *(bf16x8*)dst = (bf16x8){f2bf(a[0]), f2bf(a[1]), f2bf(a[2]), f2bf(a[3]), f2bf(b[0]), f2bf(b[1]), f2bf(b[2]), f2bf(b[3])};
+  else
+    *(bf16x4*)dst = (bf16x4){f2bf(a[0]), f2bf(a[1]), f2bf(a[2]), f2bf(a[3])};
+}
+
+// rotary on the interleaved pairs (n, n+1), (n+2, n+3) of 4 columns: (a, b) -> (a c - b s, b c + a s)
+__device__ __forceinline__ void rotary4(const GP& p, f32x4& x, int m, int n) {
+  if (n >= p.rot_cols) return;
+  const int pos = m % p.rot_seq;
+  const int pair = (n % p.rot_d) >> 1;
+  const f32x4 cs2 = *(const f32x4*)(p.rot_tab + ((long long)pos * (p.rot_d >> 1) + pair) * 2);
+  const float a0 = x[0], b0 = x[1], a1 = x[2], b1 = x[3];
+  x[0] = a0 * cs2[0] + (-b0) * cs2[1];
+  x[1] = b0 * cs2[0] + a0 * cs2[1];
+  x[2] = a1 * cs2[2] + (-b1) * cs2[3];
+  x[3] = b1 * cs2[2] + a1 * cs2[3];
+}
+
+__device__ __forceinline__ void dropout4(const GP& p, f32x4& x, int m, int n) {
+  const float sc = 1.0f / (1.0f - p.drop_p);
+  float u[4];
+  rand_uniform4(p.seed, ((unsigned long long)m * p.N + n) >> 2, u);   // n % 4 == 0, N % 4 == 0
+#pragma unroll
+  for (int e = 0; e < 4; ++e) x[e] = (u[e] >= p.drop_p) ? x[e] * sc : 0.f;
+}
+
+// Epilogue over 64 rows x 128 columns of the f32 staging tile cs (local rows; global row m0 + rbase + row).
+// Thread = 8 consecutive columns x 4 rows (16 threads per row): 16-B bf16 / 2 x 16-B f32 global vectors.
+// N % 4 == 0, so a thread's group is either fully inside N or holds exactly 4 valid columns ("full").
+template <int EPI>
+__device__ __forceinline__ void epilogue_half(const GP& p, const float* cs, int m0, int n0, int bn, int rbase,
+                                              long long cofs, int tid) {
+  if constexpr (EPI == SVAE_EPI_F32_ATOMIC) {
+    // one column per lane: each wave-wide atomic covers 256 contiguous bytes (the full-rate shape)
+    const int col = tid & 127, n = n0 + col;
+    if (n < p.N) {
+      for (int it = 0; it < 32; ++it) {
+        const int row = (tid >> 7) + 2 * it, m = m0 + rbase + row;
+        if (m < p.M) atomicAdd((float*)p.C + cofs + (long long)m * p.ldc + n, cs[row * 128 + cs_swz(row, col)]);
+      }
+    }
+    return;
+  }
+  const int cc = (tid & 15) * 8, n = n0 + cc;
+  const bool ncol = n < p.N, full = n + 8 <= p.N;
+  const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+  f32x4 b0 = zero, b1 = zero;
+  if (p.bias && ncol) {
+    b0 = *(const f32x4*)(p.bias + n);
+    if (full) b1 = *(const f32x4*)(p.bias + n + 4);
+  }
+  if constexpr (EPI == SVAE_EPI_CE_STATS) {
+    // (a) bf16 logits
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int row = (tid >> 4) + 16 * it, m = m0 + rbase + row;
+      if (m >= p.M || !ncol) continue;
+      const f32x4 x0 = *(const f32x4*)(cs + row * 128 + cs_swz(row, cc)) + b0;
+      const f32x4 x1 = *(const f32x4*)(cs + row * 128 + cs_swz(row, cc + 4)) + b1;
+      store_bf16((bf16*)p.C + cofs + (long long)m * p.ldc + n, x0, x1, full);
+    }
+    // (b) per row: 4 threads x 32 columns -> (max, sumexp), label logit
+    const int row = tid >> 2, qd = tid & 3, m = m0 + rbase + row;
+    float v[32];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int c = qd * 32 + 4 * u;
+      f32x4 x = *(const f32x4*)(cs + row * 128 + cs_swz(row, c));
+      if (p.bias) x += (n0 + c < p.N) ? *(const f32x4*)(p.bias + n0 + c) : zero;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float y = (n0 + c + e < p.N) ? x[e] : -INFINITY;
+        v[4 * u + e] = y;
+        mx = fmaxf(mx, y);
+      }
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 1, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 2, 64));
+    float se = 0.f;
+#pragma unroll
+    for (int e = 0; e < 32; ++e) se += __expf(v[e] - mx);
+    se += __shfl_xor(se, 1, 64);
+    se += __shfl_xor(se, 2, 64);
+    if (m < p.M) {
+      const int lc = p.labels[m] - n0 - qd * 32;
+      if (lc >= 0 && lc < 32) {
+#pragma unroll
+        for (int e = 0; e < 32; ++e)
+          if (e == lc) p.label_logit[m] = v[e];
+      }
+      if (qd == 0) {
+        float* part = (float*)p.aux + ((long long)m * p.tiles_n + bn) * 2;
+        part[0] = mx;
+        part[1] = se;
+      }
+    }
+    return;
+  }
+  if (!ncol) return;
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
+    const int row = (tid >> 4) + 16 * it, m = m0 + rbase + row;
+    if (m >= p.M) break;
+    f32x4 x0 = *(const f32x4*)(cs + row * 128 + cs_swz(row, cc));
+    f32x4 x1 = full ? *(const f32x4*)(cs + row * 128 + cs_swz(row, cc + 4)) : zero;
+    const long long ci = cofs + (long long)m * p.ldc + n;
+    if constexpr (EPI == SVAE_EPI_BF16) {
+      store_bf16((bf16*)p.C + ci, x0 + b0, x1 + b1, full);
+    } else if constexpr (EPI == SVAE_EPI_ROTARY_BF16) {
+      x0 += b0;
+      x1 += b1;
+      rotary4(p, x0, m, n);
+      if (full) rotary4(p, x1, m, n + 4);
+      store_bf16((bf16*)p.C + ci, x0, x1, full);
+    } else if constexpr (EPI == SVAE_EPI_F32 || EPI == SVAE_EPI_F32_ACC || EPI == SVAE_EPI_DROPOUT_RESID) {
+      float* c = (float*)p.C + ci;
+      if constexpr (EPI == SVAE_EPI_F32) {
+        x0 += b0;
+        x1 += b1;
+        if (p.resid) {
+          const float* r = p.resid + (long long)m * p.ldr + n;
+          x0 += *(const f32x4*)r;
+          if (full) x1 += *(const f32x4*)(r + 4);
+        }
+      } else if constexpr (EPI == SVAE_EPI_F32_ACC) {
+        x0 += *(const f32x4*)c;
+        if (full) x1 += *(const f32x4*)(c + 4);
+      } else {
+        if (p.drop_p > 0.f) {
+          dropout4(p, x0, m, n);
+          if (full) dropout4(p, x1, m, n + 4);
+        }
+        const float* r = p.resid + (long long)m * p.ldr + n;
+        x0 += *(const f32x4*)r;
+        if (full) x1 += *(const f32x4*)(r + 4);
+      }
+      *(f32x4*)c = x0;
+      if (full) *(f32x4*)(c + 4) = x1;
+    } else if constexpr (EPI == SVAE_EPI_GELU) {
+      // C = gelu(acc + bias), aux = gelu'(acc + bias): the backward multiplies by aux, no erf recomputed
+      x0 += b0;
+      x1 += b1;
+      f32x4 g0, g1, d0, d1;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float g, dg;
+        gelu_pair(x0[e], g, dg);
+        g0[e] = g;
+        d0[e] = dg;
+        gelu_pair(x1[e], g, dg);
+        g1[e] = g;
+        d1[e] = dg;
+      }
+      store_bf16((bf16*)p.C + ci, g0, g1, full);
+      store_bf16((bf16*)p.aux + (long long)m * p.ldaux + n, d0, d1, full);
+    } else if constexpr (EPI == SVAE_EPI_GELU_BWD) {
+      const bf16* a = (const bf16*)p.aux + (long long)m * p.ldaux + n;
+      bf16x8 d;
+      if (full) d = *(const bf16x8*)a;
+      else {
+        const bf16x4 h = *(const bf16x4*)a;
+        d = (bf16x8){h[0], h[1], h[2], h[3], h[0], h[1], h[2], h[3]};
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        x0[e] *= (float)d[e];
+        x1[e] *= (float)d[e + 4];
+      }
+      store_bf16((bf16*)p.C + ci, x0, x1, full);
+    }
+  }
+}
+
 template <bool AT, bool BT, int EPI>
 __global__ __launch_bounds__(256, 2) void gemm_kernel(GP p) {
   __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];
@@ -185,9 +361,8 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GP p) {
     }
   }
   // ---------------------------------------------------------------- epilogue
-  // Stage the 128x128 f32 tile through LDS (16-B units XOR-swizzled by row so the fragment writes spread
-  // over the banks), then every thread owns a fixed 4-column slice and walks 16 rows: all global traffic
-  // of the epilogue is 16-B (f32) / 8-B (bf16) vectors, two full rows per wave instruction.
+  // Stage the 128x128 f32 tile through LDS (16-B units XOR-swizzled by row so the fragment writes spread over
+  // the banks), then run the shared vectorised epilogue on each 64-row half.
   float* cs = (float*)smem;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -201,118 +376,8 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GP p) {
       }
   __syncthreads();
   const long long cofs = (long long)batch * p.sC;
-  if constexpr (EPI == SVAE_EPI_F32_ATOMIC) {
-    // one column per lane: each wave-wide atomic covers 256 contiguous bytes (the full-rate shape)
-    const int col = tid & 127, n = n0 + col;
-    if (n < p.N) {
-      for (int it = 0; it < 64; ++it) {
-        const int row = (tid >> 7) + 2 * it, m = m0 + row;
-        if (m < p.M) atomicAdd((float*)p.C + cofs + (long long)m * p.ldc + n, cs[row * 128 + cs_swz(row, col)]);
-      }
-    }
-    return;
-  }
-  const int cc = (tid & 31) * 4;          // this thread's 4 columns within the tile
-  const int n = n0 + cc;
-  const bool ncol = n < p.N;              // N % 4 == 0 (checked on the host)
-  f32x4 bias = {0.f, 0.f, 0.f, 0.f};
-  if (p.bias && ncol) bias = *(const f32x4*)(p.bias + n);
-
-  if constexpr (EPI == SVAE_EPI_CE_STATS) {
-    // (a) bf16 logits, coalesced
-#pragma unroll 4
-    for (int it = 0; it < 16; ++it) {
-      const int row = (tid >> 5) + 8 * it, m = m0 + row;
-      if (m >= p.M || !ncol) continue;
-      const f32x4 v = *(const f32x4*)(cs + row * 128 + cs_swz(row, cc)) + bias;
-      *(bf16x4*)((bf16*)p.C + cofs + (long long)m * p.ldc + n) = (bf16x4){f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
-    }
-    // (b) per-row online (max, sumexp) over the tile's columns: thread = (row, half)
-    const int row = tid >> 1, half = tid & 1, m = m0 + row;
-    float v[64];
-    float mx = -INFINITY;
-#pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      const int c = half * 64 + 4 * u;
-      f32x4 x = *(const f32x4*)(cs + row * 128 + cs_swz(row, c));
-      if (p.bias) x += (n0 + c < p.N) ? *(const f32x4*)(p.bias + n0 + c) : (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float y = (n0 + c + e < p.N) ? x[e] : -INFINITY;
-        v[4 * u + e] = y;
-        mx = fmaxf(mx, y);
-      }
-    }
-    mx = fmaxf(mx, __shfl_xor(mx, 1, 64));
-    float se = 0.f;
-#pragma unroll
-    for (int e = 0; e < 64; ++e) se += __expf(v[e] - mx);
-    se += __shfl_xor(se, 1, 64);
-    if (m < p.M) {
-      const int lab = p.labels[m];
-      const int lc = lab - n0 - half * 64;
-      if (lc >= 0 && lc < 64) {
-#pragma unroll
-        for (int e = 0; e < 64; ++e)
-          if (e == lc) p.label_logit[m] = v[e];
-      }
-      if (half == 0) {
-        float* part = (float*)p.aux + ((long long)m * p.tiles_n + bn) * 2;
-        part[0] = mx;
-        part[1] = se;
-      }
-    }
-    return;
-  }
-
-#pragma unroll 4
-  for (int it = 0; it < 16; ++it) {
-    const int row = (tid >> 5) + 8 * it, m = m0 + row;
-    if (m >= p.M || !ncol) continue;
-    f32x4 x = *(const f32x4*)(cs + row * 128 + cs_swz(row, cc));
-    const long long ci = cofs + (long long)m * p.ldc + n;
-    if constexpr (EPI == SVAE_EPI_BF16) {
-      x += bias;
-      *(bf16x4*)((bf16*)p.C + ci) = (bf16x4){f2bf(x[0]), f2bf(x[1]), f2bf(x[2]), f2bf(x[3])};
-    } else if constexpr (EPI == SVAE_EPI_ROTARY_BF16) {
-      x += bias;
-      if (n < p.rot_cols) {   // pairs (n, n+1), (n+2, n+3): (a, b) -> (a c - b s, b c + a s)
-        const int pos = m % p.rot_seq;
-        const int pair = (n % p.rot_d) >> 1;
-        const f32x4 cs2 = *(const f32x4*)(p.rot_tab + ((long long)pos * (p.rot_d >> 1) + pair) * 2);
-        const float a0 = x[0], b0 = x[1], a1 = x[2], b1 = x[3];
-        x[0] = a0 * cs2[0] + (-b0) * cs2[1];
-        x[1] = b0 * cs2[0] + a0 * cs2[1];
-        x[2] = a1 * cs2[2] + (-b1) * cs2[3];
-        x[3] = b1 * cs2[2] + a1 * cs2[3];
-      }
-      *(bf16x4*)((bf16*)p.C + ci) = (bf16x4){f2bf(x[0]), f2bf(x[1]), f2bf(x[2]), f2bf(x[3])};
-    } else if constexpr (EPI == SVAE_EPI_F32) {
-      x += bias;
-      if (p.resid) x += *(const f32x4*)(p.resid + (long long)m * p.ldr + n);
-      *(f32x4*)((float*)p.C + ci) = x;
-    } else if constexpr (EPI == SVAE_EPI_F32_ACC) {
-      *(f32x4*)((float*)p.C + ci) = *(const f32x4*)((float*)p.C + ci) + x;
-    } else if constexpr (EPI == SVAE_EPI_GELU) {
-      x += bias;
-      *(bf16x4*)((bf16*)p.aux + (long long)m * p.ldaux + n) = (bf16x4){f2bf(x[0]), f2bf(x[1]), f2bf(x[2]), f2bf(x[3])};
-      *(bf16x4*)((bf16*)p.C + ci) = (bf16x4){f2bf(gelu_f(x[0])), f2bf(gelu_f(x[1])), f2bf(gelu_f(x[2])), f2bf(gelu_f(x[3]))};
-    } else if constexpr (EPI == SVAE_EPI_GELU_BWD) {
-      const bf16x4 pre = *(const bf16x4*)((const bf16*)p.aux + (long long)m * p.ldaux + n);
-      *(bf16x4*)((bf16*)p.C + ci) = (bf16x4){f2bf(x[0] * gelu_grad_f((float)pre[0])), f2bf(x[1] * gelu_grad_f((float)pre[1])),
-                                              f2bf(x[2] * gelu_grad_f((float)pre[2])), f2bf(x[3] * gelu_grad_f((float)pre[3]))};
-    } else if constexpr (EPI == SVAE_EPI_DROPOUT_RESID) {
-      if (p.drop_p > 0.f) {
-        const float sc = 1.0f / (1.0f - p.drop_p);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float u = rand_uniform(p.seed, (unsigned long long)m * p.N + n + e);
-          x[e] = (u >= p.drop_p) ? x[e] * sc : 0.f;
-        }
-      }
-      *(f32x4*)((float*)p.C + ci) = *(const f32x4*)(p.resid + (long long)m * p.ldr + n) + x;
-    }
-  }
+  epilogue_half<EPI>(p, cs, m0, n0, bn, 0, cofs, tid);
+  epilogue_half<EPI>(p, cs + 64 * 128, m0, n0, bn, 64, cofs, tid);
 }
 
 // ===================================================================================================
@@ -366,121 +431,6 @@ __device__ __forceinline__ bf16x8 read_frag2(const char* lds, int base, int lane
     const int kb = 8 * (lane >> 4) + q;
     const int u = (base >> 2) + p;
     return cat44(lds_read_tr(lds + mn_off(kb, u)), lds_read_tr(lds + mn_off(kb + 4, u)));
-  }
-}
-
-// f32 staging rows for the epilogue (64 rows x 128 cols per half)
-template <int EPI>
-__device__ __forceinline__ void epilogue_half(const GP& p, const float* cs, int m0, int n0, int bn, int rbase,
-                                              long long cofs, int tid) {
-  if constexpr (EPI == SVAE_EPI_F32_ATOMIC) {
-    const int col = tid & 127, n = n0 + col;
-    if (n < p.N) {
-      for (int it = 0; it < 32; ++it) {
-        const int row = (tid >> 7) + 2 * it, m = m0 + rbase + row;
-        if (m < p.M) atomicAdd((float*)p.C + cofs + (long long)m * p.ldc + n, cs[row * 128 + cs_swz(row, col)]);
-      }
-    }
-    return;
-  }
-  const int cc = (tid & 31) * 4;
-  const int n = n0 + cc;
-  const bool ncol = n < p.N;
-  f32x4 bias = {0.f, 0.f, 0.f, 0.f};
-  if (p.bias && ncol) bias = *(const f32x4*)(p.bias + n);
-  if constexpr (EPI == SVAE_EPI_CE_STATS) {
-#pragma unroll 4
-    for (int it = 0; it < 8; ++it) {
-      const int row = (tid >> 5) + 8 * it, m = m0 + rbase + row;
-      if (m >= p.M || !ncol) continue;
-      const f32x4 v = *(const f32x4*)(cs + row * 128 + cs_swz(row, cc)) + bias;
-      *(bf16x4*)((bf16*)p.C + cofs + (long long)m * p.ldc + n) = (bf16x4){f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
-    }
-    // per row: 4 threads x 32 columns -> (max, sumexp), label logit
-    const int row = tid >> 2, qd = tid & 3, m = m0 + rbase + row;
-    float v[32];
-    float mx = -INFINITY;
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int c = qd * 32 + 4 * u;
-      f32x4 x = *(const f32x4*)(cs + row * 128 + cs_swz(row, c));
-      if (p.bias) x += (n0 + c < p.N) ? *(const f32x4*)(p.bias + n0 + c) : (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float y = (n0 + c + e < p.N) ? x[e] : -INFINITY;
-        v[4 * u + e] = y;
-        mx = fmaxf(mx, y);
-      }
-    }
-    mx = fmaxf(mx, __shfl_xor(mx, 1, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 2, 64));
-    float se = 0.f;
-#pragma unroll
-    for (int e = 0; e < 32; ++e) se += __expf(v[e] - mx);
-    se += __shfl_xor(se, 1, 64);
-    se += __shfl_xor(se, 2, 64);
-    if (m < p.M) {
-      const int lc = p.labels[m] - n0 - qd * 32;
-      if (lc >= 0 && lc < 32) {
-#pragma unroll
-        for (int e = 0; e < 32; ++e)
-          if (e == lc) p.label_logit[m] = v[e];
-      }
-      if (qd == 0) {
-        float* part = (float*)p.aux + ((long long)m * p.tiles_n + bn) * 2;
-        part[0] = mx;
-        part[1] = se;
-      }
-    }
-    return;
-  }
-#pragma unroll 4
-  for (int it = 0; it < 8; ++it) {
-    const int row = (tid >> 5) + 8 * it, m = m0 + rbase + row;
-    if (m >= p.M || !ncol) continue;
-    f32x4 x = *(const f32x4*)(cs + row * 128 + cs_swz(row, cc));
-    const long long ci = cofs + (long long)m * p.ldc + n;
-    if constexpr (EPI == SVAE_EPI_BF16) {
-      x += bias;
-      *(bf16x4*)((bf16*)p.C + ci) = (bf16x4){f2bf(x[0]), f2bf(x[1]), f2bf(x[2]), f2bf(x[3])};
-    } else if constexpr (EPI == SVAE_EPI_ROTARY_BF16) {
-      x += bias;
-      if (n < p.rot_cols) {
-        const int pos = m % p.rot_seq;
-        const int pair = (n % p.rot_d) >> 1;
-        const f32x4 cs2 = *(const f32x4*)(p.rot_tab + ((long long)pos * (p.rot_d >> 1) + pair) * 2);
-        const float a0 = x[0], b0 = x[1], a1 = x[2], b1 = x[3];
-        x[0] = a0 * cs2[0] + (-b0) * cs2[1];
-        x[1] = b0 * cs2[0] + a0 * cs2[1];
-        x[2] = a1 * cs2[2] + (-b1) * cs2[3];
-        x[3] = b1 * cs2[2] + a1 * cs2[3];
-      }
-      *(bf16x4*)((bf16*)p.C + ci) = (bf16x4){f2bf(x[0]), f2bf(x[1]), f2bf(x[2]), f2bf(x[3])};
-    } else if constexpr (EPI == SVAE_EPI_F32) {
-      x += bias;
-      if (p.resid) x += *(const f32x4*)(p.resid + (long long)m * p.ldr + n);
-      *(f32x4*)((float*)p.C + ci) = x;
-    } else if constexpr (EPI == SVAE_EPI_F32_ACC) {
-      *(f32x4*)((float*)p.C + ci) = *(const f32x4*)((float*)p.C + ci) + x;
-    } else if constexpr (EPI == SVAE_EPI_GELU) {
-      x += bias;
-      *(bf16x4*)((bf16*)p.aux + (long long)m * p.ldaux + n) = (bf16x4){f2bf(x[0]), f2bf(x[1]), f2bf(x[2]), f2bf(x[3])};
-      *(bf16x4*)((bf16*)p.C + ci) = (bf16x4){f2bf(gelu_f(x[0])), f2bf(gelu_f(x[1])), f2bf(gelu_f(x[2])), f2bf(gelu_f(x[3]))};
-    } else if constexpr (EPI == SVAE_EPI_GELU_BWD) {
-      const bf16x4 pre = *(const bf16x4*)((const bf16*)p.aux + (long long)m * p.ldaux + n);
-      *(bf16x4*)((bf16*)p.C + ci) = (bf16x4){f2bf(x[0] * gelu_grad_f((float)pre[0])), f2bf(x[1] * gelu_grad_f((float)pre[1])),
-                                              f2bf(x[2] * gelu_grad_f((float)pre[2])), f2bf(x[3] * gelu_grad_f((float)pre[3]))};
-    } else if constexpr (EPI == SVAE_EPI_DROPOUT_RESID) {
-      if (p.drop_p > 0.f) {
-        const float sc = 1.0f / (1.0f - p.drop_p);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float u = rand_uniform(p.seed, (unsigned long long)m * p.N + n + e);
-          x[e] = (u >= p.drop_p) ? x[e] * sc : 0.f;
-        }
-      }
-      *(f32x4*)((float*)p.C + ci) = *(const f32x4*)(p.resid + (long long)m * p.ldr + n) + x;
-    }
   }
 }
 
@@ -610,8 +560,11 @@ SVAE_EXPORT int svae_gemm(const svae_gemm_desc* d, svae_stream_t stream) {
   if (d->epi == SVAE_EPI_CE_STATS && (!d->labels || !d->label_logit || d->splits != 1)) return SVAE_EINVAL;
   if (d->splits > 1 && d->epi != SVAE_EPI_F32_ATOMIC) return SVAE_EINVAL;
   if (d->a_rowsum && !d->a_t) return SVAE_EINVAL;
-  if (d->N % 4 || d->ldc % 4 || ((uintptr_t)d->C & 7) || (d->resid && (d->ldr % 4)) || (d->aux && d->ldaux % 4))
-    return SVAE_EINVAL;   // vectorised epilogue
+  // vectorised epilogue: 16-B aligned rows of C / resid / aux
+  if (d->N % 4 || d->ldc % 8 || ((uintptr_t)d->C & 15) || (d->resid && (d->ldr % 4 || ((uintptr_t)d->resid & 15))))
+    return SVAE_EINVAL;
+  if ((d->epi == SVAE_EPI_GELU || d->epi == SVAE_EPI_GELU_BWD) && (d->ldaux % 8 || ((uintptr_t)d->aux & 15)))
+    return SVAE_EINVAL;
   if (d->epi == SVAE_EPI_ROTARY_BF16 && (d->rot_d % 4 || d->rot_cols % 4)) return SVAE_EINVAL;
 
   GP p;

@@ -279,14 +279,14 @@ class VAEEngine:
             st.update(cx=cx, hq=hq, qc=qc, kvc=kvc, Oc=Oc, lsec=lsec, x2=x2, pad_ctx=pad)
             xc = x2
         h2, st['ln_f'] = self._ln_fwd(pre + 'ffn_layer_norm', xc, rows_q, tag + '.ln_f')
-        preact = ws.get(tag + '.pre', (rows_q, 4 * d))
+        gprime = ws.get(tag + '.gprime', (rows_q, 4 * d))   # gelu'(pre-activation), saved by the epilogue
         f = ws.get(tag + '.f', (rows_q, 4 * d))
         K.gemm(h2, P.w(pre + 'ffn.0.weight'), f, rows_q, 4 * d, d, epi=EPI_GELU, bias=P.f(pre + 'ffn.0.bias'),
-               aux=preact, ldaux=4 * d)
+               aux=gprime, ldaux=4 * d)
         out = ws.get(tag + '.out', (rows_q, d), f32) if out is None else out
         K.gemm(f, P.w(pre + 'ffn.2.weight'), out, rows_q, d, 4 * d, epi=EPI_DROPOUT_RESID, resid=xc, ldr=d,
                drop_p=drop_p, seed=seed)
-        st.update(h2=h2, preact=preact, f=f, xc=xc, rows_q=rows_q)
+        st.update(h2=h2, gprime=gprime, f=f, xc=xc, rows_q=rows_q)
         return out, st
 
     def layer_bwd(self, st, dout, dx_out, *, dx_accumulate=False, dctx=None):
@@ -304,7 +304,7 @@ class VAEEngine:
         K.dropout_bwd_cast(dout, g2, st['drop_p'], st['seed'], rows_q, d)
         self._dw(g2, st['f'], pre + 'ffn.2.weight', rows_q, d, 4 * d)
         dpre = ws.get('b.dpre', (rows_q, 4 * d))
-        K.gemm(g2, P.w(pre + 'ffn.2.weight'), dpre, rows_q, 4 * d, d, b_t=True, epi=EPI_GELU_BWD, aux=st['preact'],
+        K.gemm(g2, P.w(pre + 'ffn.2.weight'), dpre, rows_q, 4 * d, d, b_t=True, epi=EPI_GELU_BWD, aux=st['gprime'],
                ldaux=4 * d)
         self._dw(dpre, st['h2'], pre + 'ffn.0.weight', rows_q, 4 * d, d, bias=pre + 'ffn.0.bias')
         dh2 = ws.get('b.dh2', (rows_q, d))
@@ -440,10 +440,10 @@ class VAEEngine:
         # ---- output head + cross entropy (transformer_language_model.py:55-63, language_model.py:161-170)
         xf = ws.get('xf_bf', (T, d))
         K.cast_bf16(xs, xf)
-        pre0 = ws.get('h0_pre', (T, d))
+        gp0 = ws.get('h0_gprime', (T, d))
         h0 = ws.get('h0', (T, d))
         K.gemm(xf, P.w('output_layer.0.weight'), h0, T, d, d, epi=EPI_GELU, bias=P.f('output_layer.0.bias'),
-               aux=pre0, ldaux=d)
+               aux=gp0, ldaux=d)
         hh, ln_h = self._ln_fwd('output_layer.2', h0, T, 'head.ln')
         logits = ws.get('logits', (T, V))
         ntile = -(-V // 128)
@@ -468,7 +468,7 @@ class VAEEngine:
         chunk_w = ws.get('ce.chunk_w', (8,), f32)
         nll = ws.get('nll', (1,), f32)
         K.ce_finalize(part, ntile, lab_logit, labels, T, L, nchunks, chunk_len, lse, row_loss, chunk_w, nll)
-        sv.update(xf=xf, pre0=pre0, h0=h0, hh=hh, ln_h=ln_h, logits=logits, lse=lse, chunk_w=chunk_w,
+        sv.update(xf=xf, gp0=gp0, h0=h0, hh=hh, ln_h=ln_h, logits=logits, lse=lse, chunk_w=chunk_w,
                   nchunks=nchunks, chunk_len=chunk_len, labels=labels, ids32=ids32, ntok=ntok64, x_emb=x_emb)
         loss = nll[0] + kl_weight * kl[0]                                          # transformer_vae.py:55
         self.saved = sv
@@ -546,10 +546,10 @@ class VAEEngine:
         xs, _ = self._decode(x_emb.reshape(T, d), zb, padm, B, L, 0.0, 0)
         xf = ws.get('xf_bf', (T, d))
         K.cast_bf16(xs, xf)
-        pre0 = ws.get('h0_pre', (T, d))
+        gp0 = ws.get('h0_gprime', (T, d))
         h0 = ws.get('h0', (T, d))
         K.gemm(xf, P.w('output_layer.0.weight'), h0, T, d, d, epi=EPI_GELU, bias=P.f('output_layer.0.bias'),
-               aux=pre0, ldaux=d)
+               aux=gp0, ldaux=d)
         hh, _ = self._ln_fwd('output_layer.2', h0, T, 'head.ln')
         logits = torch.empty(B, L, V, dtype=bf16, device=P.device)
         K.gemm(hh, P.w('input_layer.0.weight'), logits, T, V, d, epi=EPI_BF16, bias=P.f('output_layer.3.bias'))
@@ -577,7 +577,7 @@ class VAEEngine:
         dh0 = ws.get('b.dh0', (T, d), f32)
         self._ln_bwd('output_layer.2', dhh, sv['ln_h'], T, None, dh0)
         dpre0 = ws.get('b.dpre0', (T, d))
-        K.gelu_bwd(dh0, sv['pre0'], dpre0, T * d)
+        K.gelu_bwd(dh0, sv['gp0'], dpre0, T * d)
         self._dw(dpre0, sv['xf'], 'output_layer.0.weight', T, d, d, bias='output_layer.0.bias')
         dx = ws.get('b.dx_dec', (T, d), f32)
         K.gemm(dpre0, P.w('output_layer.0.weight'), dx, T, d, d, b_t=True, epi=EPI_F32)

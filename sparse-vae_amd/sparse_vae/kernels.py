@@ -162,8 +162,8 @@ def cast_bf16(x, out, n=None):
           'svae_cast_bf16')
 
 
-def gelu_bwd(dx, pre, out, n):
-    check(lib.svae_gelu_bwd(dx.data_ptr(), pre.data_ptr(), out.data_ptr(), n, stream()), 'svae_gelu_bwd')
+def gelu_bwd(dx, gp, out, n):
+    check(lib.svae_gelu_bwd(dx.data_ptr(), gp.data_ptr(), out.data_ptr(), n, stream()), 'svae_gelu_bwd')
 
 
 def extract_rows(x, ld, rows, mod, D, out):

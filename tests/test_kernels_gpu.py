@@ -57,16 +57,31 @@ def test_gemm_epilogues():
     C = torch.empty(M, Nn, device=dev, dtype=torch.bfloat16)
     K.gemm(X, W, C, M, Nn, Kk, epi=N.EPI_BF16, bias=b)
     assert _rel(C, ref) < 4e-3
-    # GELU
-    pre = torch.empty_like(C)
-    K.gemm(X, W, C, M, Nn, Kk, epi=N.EPI_GELU, bias=b, aux=pre, ldaux=Nn)
-    assert _rel(pre, ref) < 4e-3 and _rel(C, F.gelu(ref)) < 4e-3
-    # GELU backward: C = acc * gelu'(pre)
+    # GELU: C = gelu(acc + b), aux = gelu'(acc + b) (erf-exact reference; epilogue erf error <= 1.5e-7)
+    gp = torch.empty_like(C)
+    K.gemm(X, W, C, M, Nn, Kk, epi=N.EPI_GELU, bias=b, aux=gp, ldaux=Nn)
+    r = ref.clone().requires_grad_()
+    F.gelu(r).backward(torch.ones_like(r))
+    assert _rel(C, F.gelu(ref)) < 4e-3 and _rel(gp, r.grad) < 4e-3
+    # GELU backward: C = acc * aux
     G = torch.empty_like(C)
-    K.gemm(X, W, G, M, Nn, Kk, epi=N.EPI_GELU_BWD, aux=pre, ldaux=Nn)
-    p = pre.float().requires_grad_()
-    F.gelu(p).backward(X.float() @ W.float().t())
-    assert _rel(G, p.grad) < 5e-3
+    K.gemm(X, W, G, M, Nn, Kk, epi=N.EPI_GELU_BWD, aux=gp, ldaux=Nn)
+    assert _rel(G, (X.float() @ W.float().t()) * gp.float()) < 4e-3
+    # N % 8 == 4: the last 8-column group holds 4 valid columns
+    Nr = 132
+    Cr = torch.empty(M, Nr, device=dev, dtype=torch.bfloat16)
+    gr = torch.empty(M, Nr, device=dev, dtype=torch.bfloat16)
+    Wr = (torch.randn(Nr, Kk, device=dev) * 0.1).bfloat16()
+    br = torch.randn(Nr, device=dev)
+    refr = X.float() @ Wr.float().t() + br
+    with pytest.raises(RuntimeError):   # ldc % 8 != 0 is rejected for the vectorised epilogue
+        K.gemm(X, Wr, Cr, M, Nr, Kk, epi=N.EPI_BF16, bias=br)
+    Cp = torch.empty(M, 136, device=dev, dtype=torch.bfloat16)
+    K.gemm(X, Wr, Cp, M, Nr, Kk, epi=N.EPI_BF16, bias=br, ldc=136)
+    assert _rel(Cp[:, :Nr], refr) < 4e-3
+    C32r = torch.empty(M, 136, device=dev)
+    K.gemm(X, Wr, C32r, M, Nr, Kk, epi=N.EPI_F32, bias=br, ldc=136)
+    assert _rel(C32r[:, :Nr], refr) < 1e-5
     # residual f32
     R = torch.randn(M, Nn, device=dev)
     C32 = torch.empty(M, Nn, device=dev)
