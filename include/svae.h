@@ -105,7 +105,7 @@ typedef struct svae_attn_desc {
   /* backward only */
   const void* dout; int64_t sdo, bdo;
   float* delta;             /* [B][H][Lq] f32 workspace */
-  float* dq;                /* f32 [B][Lq][H*hd] accumulator, batch stride bdq (must be zeroed) */
+  float* dq;                /* f32 [B][Lq][H*hd] output (written), batch stride bdq; used when dq_bf is NULL */
   int64_t bdq;
   void* dk; void* dv;       /* bf16 outputs, row stride sdk/sdv, batch stride bdk/bdv */
   int64_t sdk, sdv, bdk, bdv;
@@ -115,10 +115,19 @@ typedef struct svae_attn_desc {
      free of the bf16 rounding of O, which otherwise cancels badly when the keys are nearly alike */
   float* o32;
   int64_t so32, bo32;
+  /* dQ is summed over key blocks without atomics: the backward writes one f32 partial per 128-key block
+     into dq_part ([svae_attn_dq_part_elems] floats), then a second kernel sums them (times scale) into dq_bf
+     (bf16, row stride ldq_bf, inverse rotary with rot_tab at pos = query row when rot_tab is set) or, when
+     dq_bf is NULL, into dq (f32, no rotary). */
+  float* dq_part;
+  void* dq_bf;
+  int64_t ldq_bf;
 } svae_attn_desc;
 
 int svae_attn_fwd(const svae_attn_desc* d, svae_stream_t stream);
 int svae_attn_bwd(const svae_attn_desc* d, svae_stream_t stream);
+/* floats of the dq_part workspace: ceil(Lk / 128) * B * Lq * H * hd */
+int64_t svae_attn_dq_part_elems(int32_t B, int32_t H, int32_t Lq, int32_t Lk, int32_t hd);
 /* dq f32 [rows][H*hd] -> bf16 out (row stride ldo) with optional inverse rotary (pos = row % seq). */
 int svae_dq_finalize(const float* dq, void* out, int64_t ldo, int32_t rows, int32_t D, const float* rot_tab,
                      int32_t seq, svae_stream_t stream);

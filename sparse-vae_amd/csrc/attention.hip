@@ -33,6 +33,7 @@ struct AP {
   bf16* dk; bf16* dv; long long sdk, sdv, bdk, bdv;
   const float* rot; int rot_d;
   float* o32; long long so32, bo32;
+  float* dq_part; void* dq_bf; long long ldq_bf;
 };
 
 // [64 rows][HDP] bf16 tile in LDS, 16-B chunks XOR-swizzled by (row & (chunks-1)): conflict-free for the
@@ -72,49 +73,91 @@ __device__ __forceinline__ void store_rows(char* lds, const u32x4* r, int tid) {
   }
 }
 
+// LDS-DMA (buffer_load ... lds, 16 B per lane) of rows [row0, row0+64) into a Tile<HDP> image: each wave
+// instruction writes 1 KiB lane-linearly, so the chunk swizzle is applied to the SOURCE address. Rows >= nrows
+// and dims >= hd get an out-of-range offset and land as zeros. No staging registers.
+template <int HDP>
+__device__ __forceinline__ void dma_rows(const bf16* g, long long ld, int row0, int nrows, int hd, char* lds, int w,
+                                         int lane) {
+  using T = Tile<HDP>;
+  constexpr int NI = 64 * T::PITCH / 1024;   // wave instructions per tile: 8 (HDP 64) / 16 (HDP 128)
+  const __amdgpu_buffer_rsrc_t rsrc =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(g + (long long)row0 * ld), 0, 0x7FFFFFF0, 0x00020000);
+#pragma unroll
+  for (int i = 0; i < NI / 4; ++i) {
+    const int inst = w * (NI / 4) + i;
+    const int byte = inst * 1024 + lane * 16;
+    const int r = byte / T::PITCH, c = ((byte % T::PITCH) >> 4) ^ (r & (T::NCH - 1));
+    const bool ok = row0 + r < nrows && c * 8 < hd;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void*)(lds + inst * 1024), 16,
+                                             ok ? (r * (int)ld + c * 8) * 2 : 0x7FFFFFF0, 0, 0, 0);
+  }
+}
+
 __device__ __forceinline__ bf16x8 pack8(const f32x4& a, const f32x4& b) {
   return (bf16x8){f2bf(a[0]), f2bf(a[1]), f2bf(a[2]), f2bf(a[3]), f2bf(b[0]), f2bf(b[1]), f2bf(b[2]), f2bf(b[3])};
 }
 
+// cross-lane reductions over the 4 lane groups (lane ^ 16, lane ^ 32) with VALU permlane swaps (no LDS)
+__device__ __forceinline__ float max_x16_x32(float v) {
+  auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  auto c = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(c[0]), __uint_as_float(c[1]));
+}
+__device__ __forceinline__ float sum_x16_x32(float v) {
+  auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  auto c = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(c[0]) + __uint_as_float(c[1]);
+}
+
+constexpr float LOG2E = 1.4426950408889634f;
+
 // ===================================================================================== forward
+// One block = 128 queries of one (batch, head): 4 waves x 32 queries (two 16-query MFMA column tiles), so
+// every K fragment and V^T fragment read from LDS feeds two MFMAs. Softmax in the exp2 domain with the raw
+// (unscaled) running max: p = exp2(s c - m c), c = scale log2(e). Masks only on edge tiles (causal diagonal,
+// ragged end, padded keys present); causal tiles entirely above a wave's queries are skipped.
 template <int HDP>
 __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AP p) {
   using T = Tile<HDP>;
-  constexpr int NKK = HDP / 32, NT = HDP / 16, NV = T::NCH / 4;
+  constexpr int NKK = HDP / 32, NT = HDP / 16;
   __shared__ __attribute__((aligned(16))) char smem[4 * T::BYTES + 128];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, li = lane & 15;
-  const int q0 = blockIdx.x * 64, h = blockIdx.y, b = blockIdx.z;
+  const int q0 = blockIdx.x * 128, h = blockIdx.y, b = blockIdx.z;
   const bf16* Q = p.q + b * p.bq + (long long)h * p.hd;
   const bf16* K = p.k + b * p.bk + (long long)h * p.hd;
   const bf16* V = p.v + b * p.bv + (long long)h * p.hd;
   const unsigned char* pad = p.pad ? p.pad + (long long)b * p.Lk : nullptr;
   unsigned char* pm = (unsigned char*)(smem + 4 * T::BYTES);
 
-  const int qrow = q0 + 16 * w + li;
-  bf16x8 qf[NKK];
+  const int qw = q0 + 32 * w;
+  bf16x8 qf[2][NKK];
 #pragma unroll
-  for (int kk = 0; kk < NKK; ++kk) {
-    const int d = 32 * kk + 8 * g;
-    u32x4 v = {0u, 0u, 0u, 0u};
-    if (qrow < p.Lq && d < p.hd) v = *(const u32x4*)(Q + (long long)qrow * p.sq + d);
-    qf[kk] = __builtin_bit_cast(bf16x8, v);
-  }
-  f32x4 o[NT];
+  for (int j = 0; j < 2; ++j)
 #pragma unroll
-  for (int t = 0; t < NT; ++t) o[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  float m = -1e30f, lsum = 0.f;
-  const int kv_end = p.causal ? min(p.Lk, q0 + 64) : p.Lk;
+    for (int kk = 0; kk < NKK; ++kk) {
+      const int qrow = qw + 16 * j + li, d = 32 * kk + 8 * g;
+      u32x4 v = {0u, 0u, 0u, 0u};
+      if (qrow < p.Lq && d < p.hd) v = *(const u32x4*)(Q + (long long)qrow * p.sq + d);
+      qf[j][kk] = __builtin_bit_cast(bf16x8, v);
+    }
+  f32x4 o[2][NT];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int t = 0; t < NT; ++t) o[j][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float m[2] = {-1e30f, -1e30f}, ls[2] = {0.f, 0.f};
+  const int kv_end = p.causal ? min(p.Lk, q0 + 128) : p.Lk;
   const int ntiles = (kv_end + 63) / 64;
-  const float sl2 = p.scale;
+  const float c = p.scale * LOG2E;
 
-  u32x4 rk[NV], rv[NV];
   unsigned char rpm = 0;
-  load_rows<HDP>(K, p.sk, 0, p.Lk, p.hd, rk, tid);
-  load_rows<HDP>(V, p.sv, 0, p.Lk, p.hd, rv, tid);
-  if (tid < 64) rpm = (pad && tid < p.Lk) ? pad[tid] : 0;
-  store_rows<HDP>(smem, rk, tid);
-  store_rows<HDP>(smem + T::BYTES, rv, tid);
-  if (tid < 64) pm[tid] = rpm;
+  dma_rows<HDP>(K, p.sk, 0, p.Lk, p.hd, smem, w, lane);
+  dma_rows<HDP>(V, p.sv, 0, p.Lk, p.hd, smem + T::BYTES, w, lane);
+  if (tid < 64) pm[tid] = (pad && tid < p.Lk) ? pad[tid] : 0;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
   for (int kt = 0; kt < ntiles; ++kt) {
@@ -123,88 +166,100 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AP p) {
     const char* Vs = Ks + T::BYTES;
     const unsigned char* pms = pm + buf * 64;
     const bool more = kt + 1 < ntiles;
-    if (more) {
+    if (more) {   // next tile straight into the other buffer (its readers finished before the last barrier)
       const int kn = (kt + 1) * 64;
-      load_rows<HDP>(K, p.sk, kn, p.Lk, p.hd, rk, tid);
-      load_rows<HDP>(V, p.sv, kn, p.Lk, p.hd, rv, tid);
+      char* nb = smem + (buf ^ 1) * 2 * T::BYTES;
+      dma_rows<HDP>(K, p.sk, kn, p.Lk, p.hd, nb, w, lane);
+      dma_rows<HDP>(V, p.sv, kn, p.Lk, p.hd, nb + T::BYTES, w, lane);
       if (tid < 64) rpm = (pad && kn + tid < p.Lk) ? pad[kn + tid] : 0;
     }
-    // S^T = K . Q^T : s[st][r] = score(key = 16st + 4g + r, query = qrow)
-    f32x4 s[4];
-#pragma unroll
-    for (int st = 0; st < 4; ++st) {
-      s[st] = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int kk = 0; kk < NKK; ++kk) {
-        const bf16x8 kf = *(const bf16x8*)(Ks + T::off(16 * st + li, g + 4 * kk));
-        s[st] = mfma16(kf, qf[kk], s[st]);
-      }
-    }
     const int kbase = kt * 64;
-    float mx = -1e30f;
+    if (!p.causal || kbase <= qw + 31) {
+      // S^T = K . Q^T : s[j][st][r] = score(key = kbase + 16st + 4g + r, query = qw + 16j + li)
+      f32x4 s[2][4];
 #pragma unroll
-    for (int st = 0; st < 4; ++st)
+      for (int st = 0; st < 4; ++st) {
+        s[0][st] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        s[1][st] = s[0][st];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int kl = 16 * st + 4 * g + r, key = kbase + kl;
-        const bool masked = key >= p.Lk || pms[kl] || (p.causal && key > qrow);
-        const float x = masked ? -INFINITY : s[st][r] * sl2;
-        s[st][r] = x;
-        mx = fmaxf(mx, x);
+        for (int kk = 0; kk < NKK; ++kk) {
+          const bf16x8 kf = *(const bf16x8*)(Ks + T::off(16 * st + li, g + 4 * kk));
+          s[0][st] = mfma16(kf, qf[0][kk], s[0][st]);
+          s[1][st] = mfma16(kf, qf[1][kk], s[1][st]);
+        }
       }
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float mn = fmaxf(m, mx);
-    const float alpha = __expf(m - mn);
-    m = mn;
-    lsum *= alpha;
+      const bool pad_any = p.pad && __builtin_amdgcn_ballot_w64(pms[lane] != 0) != 0;
+      if (pad_any || kbase + 64 > p.Lk || (p.causal && kbase + 63 > qw)) {
 #pragma unroll
-    for (int t = 0; t < NT; ++t) o[t] *= alpha;
+        for (int j = 0; j < 2; ++j)
 #pragma unroll
-    for (int st = 0; st < 4; ++st)
+          for (int st = 0; st < 4; ++st)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float pv = __expf(s[st][r] - m);
-        s[st][r] = pv;
-        lsum += pv;
+            for (int r = 0; r < 4; ++r) {
+              const int kl = 16 * st + 4 * g + r, key = kbase + kl;
+              if (key >= p.Lk || pms[kl] || (p.causal && key > qw + 16 * j + li)) s[j][st][r] = -INFINITY;
+            }
       }
-    // O^T += V^T . P^T  (keys of k-step kk: 32kk + 16(j>>2) + 4g + (j&3))
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const bf16x8 pf = pack8(s[2 * kk], s[2 * kk + 1]);
-      const int r0 = 32 * kk + 4 * g + (li >> 2);
+      for (int j = 0; j < 2; ++j) {
+        float mx = -INFINITY;
 #pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        const int u = 4 * t + (li & 3);
-        const short4v lo = lds_read_tr(Vs + T::uoff(r0, u));
-        const short4v hi = lds_read_tr(Vs + T::uoff(r0 + 16, u));
-        o[t] = mfma16(cat44(lo, hi), pf, o[t]);
+        for (int st = 0; st < 4; ++st) mx = fmaxf(fmaxf(mx, fmaxf(s[j][st][0], s[j][st][1])), fmaxf(s[j][st][2], s[j][st][3]));
+        mx = max_x16_x32(mx);
+        const float mn = fmaxf(m[j], mx);
+        const float alpha = __builtin_amdgcn_exp2f((m[j] - mn) * c);
+        m[j] = mn;
+        ls[j] *= alpha;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) o[j][t] *= alpha;
+        const float mc = mn * c;
+#pragma unroll
+        for (int st = 0; st < 4; ++st)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float pv = __builtin_amdgcn_exp2f(fmaf(s[j][st][r], c, -mc));
+            s[j][st][r] = pv;
+            ls[j] += pv;
+          }
+      }
+      // O^T += V^T . P^T  (keys of k-step kk: 32kk + 16(jj>>2) + 4g + (jj&3))
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const bf16x8 pf0 = pack8(s[0][2 * kk], s[0][2 * kk + 1]);
+        const bf16x8 pf1 = pack8(s[1][2 * kk], s[1][2 * kk + 1]);
+        const int r0 = 32 * kk + 4 * g + (li >> 2);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          const int u = 4 * t + (li & 3);
+          const bf16x8 vf = cat44(lds_read_tr(Vs + T::uoff(r0, u)), lds_read_tr(Vs + T::uoff(r0 + 16, u)));
+          o[0][t] = mfma16(vf, pf0, o[0][t]);
+          o[1][t] = mfma16(vf, pf1, o[1][t]);
+        }
       }
     }
-    if (more) {
-      char* nb = smem + (buf ^ 1) * 2 * T::BYTES;
-      store_rows<HDP>(nb, rk, tid);
-      store_rows<HDP>(nb + T::BYTES, rv, tid);
-      if (tid < 64) pm[(buf ^ 1) * 64 + tid] = rpm;
-    }
+    if (more && tid < 64) pm[(buf ^ 1) * 64 + tid] = rpm;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
 
-  lsum += __shfl_xor(lsum, 16, 64);
-  lsum += __shfl_xor(lsum, 32, 64);
-  if (qrow < p.Lq) {
-    const float inv = 1.0f / lsum;
-    bf16* O = p.o + b * p.bo + (long long)h * p.hd + (long long)qrow * p.so;
 #pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      const int d = 16 * t + 4 * g;
-      if (d < p.hd) {
-        *(bf16x4*)(O + d) = (bf16x4){f2bf(o[t][0] * inv), f2bf(o[t][1] * inv), f2bf(o[t][2] * inv), f2bf(o[t][3] * inv)};
-        if (p.o32)
-          *(f32x4*)(p.o32 + b * p.bo32 + (long long)h * p.hd + (long long)qrow * p.so32 + d) = o[t] * inv;
+  for (int j = 0; j < 2; ++j) {
+    const float lsum = sum_x16_x32(ls[j]);
+    const int qrow = qw + 16 * j + li;
+    if (qrow < p.Lq) {
+      const float inv = lsum > 0.f ? 1.0f / lsum : 0.f;
+      bf16* O = p.o + b * p.bo + (long long)h * p.hd + (long long)qrow * p.so;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int d = 16 * t + 4 * g;
+        if (d < p.hd) {
+          const f32x4 v = o[j][t] * inv;
+          *(bf16x4*)(O + d) = (bf16x4){f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
+          if (p.o32) *(f32x4*)(p.o32 + b * p.bo32 + (long long)h * p.hd + (long long)qrow * p.so32 + d) = v;
+        }
       }
+      if (g == 0) p.lse[((long long)b * p.H + h) * p.Lq + qrow] = m[j] * p.scale + __logf(lsum);
     }
-    if (g == 0) p.lse[((long long)b * p.H + h) * p.Lq + qrow] = m + __logf(lsum);
   }
 }
 
@@ -239,123 +294,174 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(AP p) {
   if (li == 0) ((float*)p.delta)[((long long)b * p.H + h) * p.Lq + q] = s;
 }
 
+// Main backward: one block = 128 keys of one (batch, head) = 4 waves x 32 keys (two 16-key MFMA column
+// tiles), sweeping 64-query tiles (causal: from the tile holding the block's first key). Key on the lane:
+// S = Q K^T and dP = dO V^T accumulators are the B operands of dV^T += dO^T P and dK^T += Q^T dS; every
+// dO^T / Q^T fragment read feeds both key tiles. Row constants start the accumulators: S' = S - lse/scale,
+// dP' = dP - delta, so p = exp2(c S') and dS = p dP' with no per-element subtraction.
+// dQ: dS^T goes through LDS once, the block's 64 x hd partial dQ (over its 128 keys) is STORED to its own
+// slice of dq_part (no atomics); attn_dq_reduce_kernel sums the slices.
+constexpr int BWD_KEYS = 128;
+
 template <int HDP>
-__global__ __launch_bounds__(256, 2) void attn_bwd_kernel(AP p) {
-  using T = Tile<HDP>;
-  using TS = Tile<64>;   // dS^T tile [64 keys][64 queries]
-  constexpr int NKK = HDP / 32, NT = HDP / 16, NV = T::NCH / 4;
-  __shared__ __attribute__((aligned(16))) char smem[3 * T::BYTES + TS::BYTES + 2 * 64 * 4];
-  char* Qs = smem;
-  char* dOs = smem + T::BYTES;
-  char* Ks = smem + 2 * T::BYTES;
-  char* dSs = smem + 3 * T::BYTES;
-  float* lse_s = (float*)(smem + 3 * T::BYTES + TS::BYTES);
-  float* del_s = lse_s + 64;
+__global__ __launch_bounds__(256, HDP == 64 ? 2 : 1) void attn_bwd_kernel(AP p) {
+  using T = Tile<HDP>;          // [rows][HDP] bf16
+  using TS = Tile<64>;          // dS^T [128 keys][64 queries]
+  constexpr int NKK = HDP / 32, NT = HDP / 16;
+  __shared__ __attribute__((aligned(16))) char smem[6 * T::BYTES + 2 * TS::BYTES + 4 * 64 * 4];
+  char* QO = smem;                                  // [buf][Q, dO] tiles
+  char* Ks = smem + 4 * T::BYTES;                   // 128 key rows
+  char* dSs = smem + 6 * T::BYTES;                  // 128 key rows x 64 queries
+  float* cst = (float*)(smem + 6 * T::BYTES + 2 * TS::BYTES);   // [buf][-lse/scale, -delta][64]
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, li = lane & 15;
-  const int k0 = blockIdx.x * 64, h = blockIdx.y, b = blockIdx.z;
+  const int kb = blockIdx.x, k0 = kb * BWD_KEYS, h = blockIdx.y, b = blockIdx.z;
   const bf16* Q = p.q + b * p.bq + (long long)h * p.hd;
   const bf16* K = p.k + b * p.bk + (long long)h * p.hd;
   const bf16* V = p.v + b * p.bv + (long long)h * p.hd;
   const bf16* dO = p.dout + b * p.bdo + (long long)h * p.hd;
   const float* lse = p.lse + ((long long)b * p.H + h) * p.Lq;
   const float* delta = p.delta + ((long long)b * p.H + h) * p.Lq;
-  const int kw = k0 + 16 * w;
-  const int key = kw + li;                       // this lane's key (column of S / dP)
-  const bool key_ok = key < p.Lk && !(p.pad && p.pad[(long long)b * p.Lk + key]);
-
-  // K and V fragments of this wave's 16 keys (B operands of S = Q K^T and dP = dO V^T)
-  bf16x8 kf[NKK], vf[NKK];
+  const int kw = k0 + 32 * w;                       // this wave's first key
+  // V fragments of this wave's 32 keys stay in registers (B operands of dP = dO V^T); K fragments are read
+  // from the block's K tile in LDS each query tile (it is there anyway for dQ = dS K).
+  bool key_ok[2];
+  bf16x8 vf[2][NKK];
 #pragma unroll
-  for (int kk = 0; kk < NKK; ++kk) {
-    const int d = 32 * kk + 8 * g;
-    u32x4 a = {0u, 0u, 0u, 0u}, c = a;
-    if (key < p.Lk && d < p.hd) {
-      a = *(const u32x4*)(K + (long long)key * p.sk + d);
-      c = *(const u32x4*)(V + (long long)key * p.sv + d);
+  for (int j = 0; j < 2; ++j) {
+    const int key = kw + 16 * j + li;
+    key_ok[j] = key < p.Lk && !(p.pad && p.pad[(long long)b * p.Lk + key]);
+#pragma unroll
+    for (int kk = 0; kk < NKK; ++kk) {
+      const int d = 32 * kk + 8 * g;
+      u32x4 c = {0u, 0u, 0u, 0u};
+      if (key < p.Lk && d < p.hd) c = *(const u32x4*)(V + (long long)key * p.sv + d);
+      vf[j][kk] = __builtin_bit_cast(bf16x8, c);
     }
-    kf[kk] = __builtin_bit_cast(bf16x8, a);
-    vf[kk] = __builtin_bit_cast(bf16x8, c);
   }
-  {  // K tile for dQ = dS . K (transposed reads)
-    u32x4 rk[NV];
-    load_rows<HDP>(K, p.sk, k0, p.Lk, p.hd, rk, tid);
-    store_rows<HDP>(Ks, rk, tid);
+  const bool keys_all_ok = __builtin_amdgcn_ballot_w64(!(key_ok[0] && key_ok[1])) == 0;
+  {  // K tile (128 rows) for dQ = dS . K
+    dma_rows<HDP>(K, p.sk, k0, p.Lk, p.hd, Ks, w, lane);
+    dma_rows<HDP>(K, p.sk, k0 + 64, p.Lk, p.hd, Ks + T::BYTES, w, lane);
   }
-  f32x4 dk[NT], dv[NT];
+  f32x4 dk[2][NT], dv[2][NT];
 #pragma unroll
-  for (int t = 0; t < NT; ++t) { dk[t] = (f32x4){0.f, 0.f, 0.f, 0.f}; dv[t] = dk[t]; }
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int t = 0; t < NT; ++t) { dk[j][t] = (f32x4){0.f, 0.f, 0.f, 0.f}; dv[j][t] = dk[j][t]; }
 
+  const float inv_scale = 1.0f / p.scale, c = p.scale * LOG2E;
   const int qt0 = p.causal ? k0 / 64 : 0;
   const int nqt = (p.Lq + 63) / 64;
+  float* part = p.dq_part + ((long long)kb * p.B + b) * p.Lq * p.H * p.hd + (long long)h * p.hd;
+  const long long ldp = (long long)p.H * p.hd;
+
+  float rc = 0.f;
+  auto fetch = [&](int qb, int buf) {
+    dma_rows<HDP>(Q, p.sq, qb, p.Lq, p.hd, QO + buf * 2 * T::BYTES, w, lane);
+    dma_rows<HDP>(dO, p.sdo, qb, p.Lq, p.hd, QO + buf * 2 * T::BYTES + T::BYTES, w, lane);
+    if (tid < 128) {
+      const int q = qb + (tid & 63);
+      rc = q < p.Lq ? (tid < 64 ? -lse[q] * inv_scale : -delta[q]) : 0.f;
+    }
+  };
+  auto commit = [&](int buf) {
+    if (tid < 128) cst[buf * 128 + tid] = rc;
+  };
+  if (qt0 < nqt) {
+    fetch(qt0 * 64, 0);
+    commit(0);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
   for (int qt = qt0; qt < nqt; ++qt) {
+    const int buf = (qt - qt0) & 1;
     const int qb = qt * 64;
-    {
-      u32x4 rq[NV], ro[NV];
-      load_rows<HDP>(Q, p.sq, qb, p.Lq, p.hd, rq, tid);
-      load_rows<HDP>(dO, p.sdo, qb, p.Lq, p.hd, ro, tid);
-      __syncthreads();   // previous tile's readers are done
-      store_rows<HDP>(Qs, rq, tid);
-      store_rows<HDP>(dOs, ro, tid);
-      if (tid < 64) {
-        const int q = qb + tid;
-        lse_s[tid] = q < p.Lq ? lse[q] : 0.f;
-        del_s[tid] = q < p.Lq ? delta[q] : 0.f;
+    const char* Qs = QO + buf * 2 * T::BYTES;
+    const char* dOs = Qs + T::BYTES;
+    const float* nl = cst + buf * 128;
+    const bool more = qt + 1 < nqt;
+    if (more) fetch(qb + 64, buf ^ 1);
+    const bool live = !p.causal || kw <= qb + 63;   // some key of this wave is visible to some query
+    if (live) {
+      f32x4 s[2][4], dp[2][4];
+      bf16x8 kf[2][NKK];
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int kk = 0; kk < NKK; ++kk) kf[j][kk] = *(const bf16x8*)(Ks + T::off(32 * w + 16 * j + li, g + 4 * kk));
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const f32x4 sl = *(const f32x4*)(nl + 16 * t + 4 * g);
+        const f32x4 dl = *(const f32x4*)(nl + 64 + 16 * t + 4 * g);
+        s[0][t] = sl; s[1][t] = sl;
+        dp[0][t] = dl; dp[1][t] = dl;
+#pragma unroll
+        for (int kk = 0; kk < NKK; ++kk) {
+          const bf16x8 qa = *(const bf16x8*)(Qs + T::off(16 * t + li, g + 4 * kk));
+          const bf16x8 oa = *(const bf16x8*)(dOs + T::off(16 * t + li, g + 4 * kk));
+          s[0][t] = mfma16(qa, kf[0][kk], s[0][t]);
+          s[1][t] = mfma16(qa, kf[1][kk], s[1][t]);
+          dp[0][t] = mfma16(oa, vf[0][kk], dp[0][t]);
+          dp[1][t] = mfma16(oa, vf[1][kk], dp[1][t]);
+        }
       }
-      __syncthreads();
-    }
-    // S (q x key) and dP, key on the lane: s[t][r] -> q = qb + 16t + 4g + r
-    f32x4 s[4], dp[4];
+      const bool edge = !keys_all_ok || qb + 64 > p.Lq || (p.causal && kw + 31 > qb);
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      s[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
-      dp[t] = s[t];
+      for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int kk = 0; kk < NKK; ++kk) {
-        const bf16x8 qa = *(const bf16x8*)(Qs + T::off(16 * t + li, g + 4 * kk));
-        const bf16x8 oa = *(const bf16x8*)(dOs + T::off(16 * t + li, g + 4 * kk));
-        s[t] = mfma16(qa, kf[kk], s[t]);
-        dp[t] = mfma16(oa, vf[kk], dp[t]);
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float pr = __builtin_amdgcn_exp2f(s[j][t][r] * c);
+            if (edge) {
+              const int q = qb + 16 * t + 4 * g + r, key = kw + 16 * j + li;
+              if (!key_ok[j] || q >= p.Lq || (p.causal && key > q)) pr = 0.f;
+            }
+            s[j][t][r] = pr;
+            dp[j][t][r] = pr * dp[j][t][r];
+          }
+      // dV^T += dO^T P ; dK^T += Q^T dS   (query order of k-step kk: 32kk + 16(jj>>2) + 4g + (jj&3))
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const bf16x8 pf0 = pack8(s[0][2 * kk], s[0][2 * kk + 1]), pf1 = pack8(s[1][2 * kk], s[1][2 * kk + 1]);
+        const bf16x8 df0 = pack8(dp[0][2 * kk], dp[0][2 * kk + 1]), df1 = pack8(dp[1][2 * kk], dp[1][2 * kk + 1]);
+        const int r0 = 32 * kk + 4 * g + (li >> 2);
+#pragma unroll
+        for (int u = 0; u < NT; ++u) {
+          const int uu = 4 * u + (li & 3);
+          const bf16x8 ao = cat44(lds_read_tr(dOs + T::uoff(r0, uu)), lds_read_tr(dOs + T::uoff(r0 + 16, uu)));
+          dv[0][u] = mfma16(ao, pf0, dv[0][u]);
+          dv[1][u] = mfma16(ao, pf1, dv[1][u]);
+          const bf16x8 aq = cat44(lds_read_tr(Qs + T::uoff(r0, uu)), lds_read_tr(Qs + T::uoff(r0 + 16, uu)));
+          dk[0][u] = mfma16(aq, df0, dk[0][u]);
+          dk[1][u] = mfma16(aq, df1, dk[1][u]);
+        }
       }
-    }
+      // dS^T -> LDS [key][q]: lane holds q = 16t + 4g + (0..3) at key row 32w + 16j + li
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
+      for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int ql = 16 * t + 4 * g + r, q = qb + ql;
-        const bool ok = key_ok && q < p.Lq && !(p.causal && key > q);
-        const float pr = ok ? __expf(s[t][r] * p.scale - lse_s[ql]) : 0.f;
-        s[t][r] = pr;
-        dp[t][r] = pr * (dp[t][r] - del_s[ql]);
-      }
-    // dV^T += dO^T P ; dK^T += Q^T dS   (query order of k-step kk: 32kk + 16(j>>2) + 4g + (j&3))
+        for (int t = 0; t < 4; ++t)
+          *(bf16x4*)(dSs + TS::uoff(32 * w + 16 * j + li, 4 * t + g)) =
+              (bf16x4){f2bf(dp[j][t][0]), f2bf(dp[j][t][1]), f2bf(dp[j][t][2]), f2bf(dp[j][t][3])};
+    } else {
+      const bf16x4 z = {f2bf(0.f), f2bf(0.f), f2bf(0.f), f2bf(0.f)};
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const bf16x8 pf = pack8(s[2 * kk], s[2 * kk + 1]);
-      const bf16x8 df = pack8(dp[2 * kk], dp[2 * kk + 1]);
-      const int r0 = 32 * kk + 4 * g + (li >> 2);
+      for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int u = 0; u < NT; ++u) {
-        const int uu = 4 * u + (li & 3);
-        const bf16x8 ao = cat44(lds_read_tr(dOs + T::uoff(r0, uu)), lds_read_tr(dOs + T::uoff(r0 + 16, uu)));
-        dv[u] = mfma16(ao, pf, dv[u]);
-        const bf16x8 aq = cat44(lds_read_tr(Qs + T::uoff(r0, uu)), lds_read_tr(Qs + T::uoff(r0 + 16, uu)));
-        dk[u] = mfma16(aq, df, dk[u]);
-      }
-    }
-    // dS^T -> LDS [key][q]: this lane holds q = 16t + 4g + (0..3) at key row 16w + li
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const bf16x4 v4 = (bf16x4){f2bf(dp[t][0]), f2bf(dp[t][1]), f2bf(dp[t][2]), f2bf(dp[t][3])};
-      *(bf16x4*)(dSs + TS::uoff(16 * w + li, 4 * t + g)) = v4;
+        for (int t = 0; t < 4; ++t) *(bf16x4*)(dSs + TS::uoff(32 * w + 16 * j + li, 4 * t + g)) = z;
     }
     __syncthreads();
-    // dQ[q = qb + 16w + 4g + r][d = 16u + li] = scale * sum_key dS[q][key] K[key][d]
+    // partial dQ[q = qb + 16w + 4g + r][d = 16u + li] = sum over the block's 128 keys of dS[q][key] K[key][d]
     f32x4 dq[NT];
 #pragma unroll
     for (int u = 0; u < NT; ++u) dq[u] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    const int kvis = p.causal ? min(BWD_KEYS, qb + 64 - k0) : BWD_KEYS;   // keys past the tile's last query: dS = 0
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
+    for (int kk = 0; kk < 4; ++kk) {
+      if (32 * kk >= kvis) break;
       const int kr = 32 * kk + 8 * g + (li >> 2);
       const int uq = 4 * w + (li & 3);
       const bf16x8 a = cat44(lds_read_tr(dSs + TS::uoff(kr, uq)), lds_read_tr(dSs + TS::uoff(kr + 4, uq)));
@@ -366,23 +472,27 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kernel(AP p) {
         dq[u] = mfma16(a, bk, dq[u]);
       }
     }
-    float* DQ = p.dq + b * p.bdq + (long long)h * p.hd;
-    const long long ldq = (long long)p.H * p.hd;
 #pragma unroll
-    for (int u = 0; u < NT; ++u) {
-      const int d = 16 * u + li;
-      if (d < p.hd) {
+    for (int r = 0; r < 4; ++r) {
+      const int q = qb + 16 * w + 4 * g + r;
+      if (q < p.Lq) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int q = qb + 16 * w + 4 * g + r;
-          if (q < p.Lq) atomicAdd(DQ + (long long)q * ldq + d, dq[u][r] * p.scale);
+        for (int u = 0; u < NT; ++u) {
+          const int d = 16 * u + li;
+          if (d < p.hd) part[(long long)q * ldp + d] = dq[u][r];
         }
       }
     }
+    if (more) commit(buf ^ 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
   }
 
-  // epilogue: dK (scaled, inverse rotary) and dV for key = kw + li, dims 16u + 4g + (0..3)
-  if (key < p.Lk) {
+  // epilogue: dK (scaled, inverse rotary) and dV for key = kw + 16j + li, dims 16u + 4g + (0..3)
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int key = kw + 16 * j + li;
+    if (key >= p.Lk) continue;
     bf16* DK = p.dk + b * p.bdk + (long long)key * p.sdk + (long long)h * p.hd;
     bf16* DV = p.dv + b * p.bdv + (long long)key * p.sdv + (long long)h * p.hd;
 #pragma unroll
@@ -391,19 +501,51 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kernel(AP p) {
       if (d >= p.hd) continue;
       float x[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) x[r] = dk[u][r] * p.scale;
+      for (int r = 0; r < 4; ++r) x[r] = dk[j][u][r] * p.scale;
       if (p.rot) {
 #pragma unroll
         for (int e = 0; e < 2; ++e) {
           const int pair = (h * p.hd + d) / 2 + e;
           const float2 cs = ((const float2*)p.rot)[(long long)key * (p.rot_d / 2) + pair];
-          const float a = x[2 * e], c = x[2 * e + 1];
-          x[2 * e] = a * cs.x + c * cs.y;
-          x[2 * e + 1] = -a * cs.y + c * cs.x;
+          const float a = x[2 * e], cc = x[2 * e + 1];
+          x[2 * e] = a * cs.x + cc * cs.y;
+          x[2 * e + 1] = -a * cs.y + cc * cs.x;
         }
       }
       *(bf16x4*)(DK + d) = (bf16x4){f2bf(x[0]), f2bf(x[1]), f2bf(x[2]), f2bf(x[3])};
-      *(bf16x4*)(DV + d) = (bf16x4){f2bf(dv[u][0]), f2bf(dv[u][1]), f2bf(dv[u][2]), f2bf(dv[u][3])};
+      *(bf16x4*)(DV + d) = (bf16x4){f2bf(dv[j][u][0]), f2bf(dv[j][u][1]), f2bf(dv[j][u][2]), f2bf(dv[j][u][3])};
+    }
+  }
+}
+
+// dQ = scale * sum over the key blocks that can see the query (causal: kb <= q / 128) of the partials;
+// bf16 out with inverse rotary (pos = query) or f32 out. One thread per 4 columns of one (batch, query).
+__global__ __launch_bounds__(256) void attn_dq_reduce_kernel(AP p) {
+  const int D = p.H * p.hd, D4 = D / 4;
+  const long long total = (long long)p.B * p.Lq * D4;
+  const int nkb = (p.Lk + BWD_KEYS - 1) / BWD_KEYS;
+  const long long plane = (long long)p.B * p.Lq * D;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const int c4 = (int)(i % D4);
+    const long long row = i / D4;                 // b * Lq + q
+    const int q = (int)(row % p.Lq), b = (int)(row / p.Lq);
+    const int nk = p.causal ? min(nkb, q / BWD_KEYS + 1) : nkb;
+    const float* src = p.dq_part + row * D + 4 * c4;
+    f32x4 acc = *(const f32x4*)src;
+    for (int k = 1; k < nk; ++k) acc += *(const f32x4*)(src + k * plane);
+    acc *= p.scale;
+    if (p.dq_bf) {
+      if (p.rot) {   // inverse of (a c - b s, b c + a s) on the pairs (4c4, 4c4+1), (4c4+2, 4c4+3)
+        const f32x4 cs = *(const f32x4*)(p.rot + ((long long)q * (p.rot_d / 2) + 2 * c4) * 2);
+        const float a0 = acc[0], b0 = acc[1], a1 = acc[2], b1 = acc[3];
+        acc[0] = a0 * cs[0] + b0 * cs[1];
+        acc[1] = -a0 * cs[1] + b0 * cs[0];
+        acc[2] = a1 * cs[2] + b1 * cs[3];
+        acc[3] = -a1 * cs[3] + b1 * cs[2];
+      }
+      *(bf16x4*)((bf16*)p.dq_bf + row * p.ldq_bf + 4 * c4) = (bf16x4){f2bf(acc[0]), f2bf(acc[1]), f2bf(acc[2]), f2bf(acc[3])};
+    } else {
+      *(f32x4*)(p.dq + b * p.bdq + (long long)q * D + 4 * c4) = acc;
     }
   }
 }
@@ -423,6 +565,7 @@ bool fill(const svae_attn_desc* d, AP& p) {
   p.dk = (bf16*)d->dk; p.dv = (bf16*)d->dv; p.sdk = d->sdk; p.sdv = d->sdv; p.bdk = d->bdk; p.bdv = d->bdv;
   p.rot = d->rot_tab; p.rot_d = d->rot_d;
   p.o32 = d->o32; p.so32 = d->so32; p.bo32 = d->bo32;
+  p.dq_part = d->dq_part; p.dq_bf = d->dq_bf; p.ldq_bf = d->ldq_bf;
   if (p.o32 && ((p.so32 | p.bo32) % 4)) return false;
   return true;
 }
@@ -433,7 +576,7 @@ SVAE_EXPORT int svae_attn_fwd(const svae_attn_desc* d, svae_stream_t stream) {
   AP p;
   if (!fill(d, p)) return SVAE_EINVAL;
   if (d->causal && d->Lq != d->Lk) return SVAE_EINVAL;
-  dim3 grid((d->Lq + 63) / 64, d->H, d->B);
+  dim3 grid((d->Lq + 127) / 128, d->H, d->B);
   hipStream_t s = (hipStream_t)stream;
   if (d->hd <= 64) hipLaunchKernelGGL(attn_fwd_kernel<64>, grid, dim3(256), 0, s, p);
   else hipLaunchKernelGGL(attn_fwd_kernel<128>, grid, dim3(256), 0, s, p);
@@ -444,16 +587,25 @@ SVAE_EXPORT int svae_attn_fwd(const svae_attn_desc* d, svae_stream_t stream) {
 SVAE_EXPORT int svae_attn_bwd(const svae_attn_desc* d, svae_stream_t stream) {
   AP p;
   if (!fill(d, p)) return SVAE_EINVAL;
-  if (!d->dout || !d->delta || !d->dq || !d->dk || !d->dv) return SVAE_EINVAL;
+  if (!d->dout || !d->delta || !d->dq_part || !d->dk || !d->dv || (!d->dq && !d->dq_bf)) return SVAE_EINVAL;
   if ((d->sdo | d->bdo | d->sdk | d->sdv | d->bdk | d->bdv) % 4) return SVAE_EINVAL;
   if (d->causal && d->Lq != d->Lk) return SVAE_EINVAL;
   if (d->rot_tab && d->rot_d <= 0) return SVAE_EINVAL;
+  if (d->hd % 4 || (d->dq_bf && d->ldq_bf % 4) || (!d->dq_bf && d->bdq % 4)) return SVAE_EINVAL;
+  if (d->dq_bf && d->rot_tab && d->rot_d != d->H * d->hd) return SVAE_EINVAL;
   hipStream_t s = (hipStream_t)stream;
   const int rows = d->B * d->Lq * d->H;
   hipLaunchKernelGGL(attn_delta_kernel, dim3((rows + 15) / 16), dim3(256), 0, s, p);
-  dim3 grid((d->Lk + 63) / 64, d->H, d->B);
+  dim3 grid((d->Lk + BWD_KEYS - 1) / BWD_KEYS, d->H, d->B);
   if (d->hd <= 64) hipLaunchKernelGGL(attn_bwd_kernel<64>, grid, dim3(256), 0, s, p);
   else hipLaunchKernelGGL(attn_bwd_kernel<128>, grid, dim3(256), 0, s, p);
+  const long long work = (long long)d->B * d->Lq * (d->H * d->hd / 4);
+  hipLaunchKernelGGL(attn_dq_reduce_kernel, dim3((unsigned)min(8192LL, (work + 255) / 256)), dim3(256), 0, s, p);
   SVAE_LAUNCH_CHECK();
   return SVAE_OK;
+}
+
+SVAE_EXPORT int64_t svae_attn_dq_part_elems(int32_t B, int32_t H, int32_t Lq, int32_t Lk, int32_t hd) {
+  if (B <= 0 || H <= 0 || Lq <= 0 || Lk <= 0 || hd <= 0) return 0;
+  return (int64_t)((Lk + BWD_KEYS - 1) / BWD_KEYS) * B * Lq * H * hd;
 }

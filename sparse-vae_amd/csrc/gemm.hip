@@ -95,6 +95,24 @@ __device__ __forceinline__ bf16x8 read_frag(const char* lds, int base, int kk, i
 // f32 staging tile [128][128] for the epilogue: 16-B unit index XOR ((row >> 2) & 3) << 2
 __device__ __forceinline__ int cs_swz(int row, int col) { return (((col >> 2) ^ (((row >> 2) & 3) << 2)) << 2) | (col & 3); }
 
+// Block -> (tile, batch, split). The hardware deals consecutive block ids round-robin over the 8 XCDs; the
+// bijective remap gives each XCD one contiguous range of the (batch, split)-major / N-fastest logical order,
+// so blocks that share A rows, B columns or a K-chunk run together on one L2.
+__device__ __forceinline__ void tile_coords(const GP& p, int& bm, int& bn, int& batch, int& split) {
+  const int tiles = p.tiles_n * p.tiles_m;
+  const int nwg = gridDim.x;
+  int bid = blockIdx.x;
+  if (nwg >= 16) {
+    const int q = nwg / 8, r = nwg % 8, xcd = bid % 8, idx = bid / 8;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+  }
+  const int z = bid / tiles, t = bid - z * tiles;
+  bn = t % p.tiles_n;
+  bm = t / p.tiles_n;
+  batch = z / p.splits;
+  split = z - batch * p.splits;
+}
+
 __device__ __forceinline__ void store_bf16(bf16* dst, const f32x4& a, const f32x4& b, bool full) {
   if (full)
     *(bf16x8*)dst = (bf16x8){f2bf(a[0]), f2bf(a[1]), f2bf(a[2]), f2bf(a[3]), f2bf(b[0]), f2bf(b[1]), f2bf(b[2]), f2bf(b[3])};
@@ -278,15 +296,8 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GP p) {
   const int wm = wave >> 1, wn = wave & 1;
 
   // tile coordinates: XCD-aware remap (see gemm_glds_kernel), then N first inside an XCD's range
-  const int nwg = p.tiles_n * p.tiles_m;
-  int bid = blockIdx.x;
-  if (nwg >= 16) {
-    const int q = nwg / 8, r = nwg % 8, xcd = bid % 8, idx = bid / 8;
-    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
-  }
-  const int bn = bid % p.tiles_n, bm = bid / p.tiles_n;
-  const int z = blockIdx.z;
-  const int batch = z / p.splits, split = z % p.splits;
+  int bm, bn, batch, split;
+  tile_coords(p, bm, bn, batch, split);
   const int m0 = bm * BM, n0 = bn * BN;
   const int kbeg = split * p.kchunk;
   const int kend = min(p.K, kbeg + p.kchunk);
@@ -440,15 +451,8 @@ __global__ __launch_bounds__(256, 3) void gemm_glds_kernel(GP p) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
-  const int nwg = p.tiles_n * p.tiles_m;
-  int bid = blockIdx.x;
-  if (nwg >= 16) {
-    const int q = nwg / 8, r = nwg % 8, xcd = bid % 8, idx = bid / 8;
-    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
-  }
-  const int bn = bid % p.tiles_n, bm = bid / p.tiles_n;
-  const int z = blockIdx.z;
-  const int batch = z / p.splits, split = z % p.splits;
+  int bm, bn, batch, split;
+  tile_coords(p, bm, bn, batch, split);
   const int m0 = bm * BM, n0 = bn * BN;
   const int kbeg = split * p.kchunk;
   const int kend = min(p.K, kbeg + p.kchunk);
@@ -585,7 +589,9 @@ SVAE_EXPORT int svae_gemm(const svae_gemm_desc* d, svae_stream_t stream) {
   p.a_rowsum = d->a_rowsum;
   p.epi = d->epi;
 
-  dim3 grid(p.tiles_n * p.tiles_m, 1, d->batch * d->splits);
+  const long long nblocks = (long long)p.tiles_n * p.tiles_m * d->batch * d->splits;
+  if (nblocks > 0x7FFFFFFF) return SVAE_EINVAL;
+  dim3 grid((unsigned)nblocks);
   hipStream_t s = (hipStream_t)stream;
   const int lay = (d->a_t ? 2 : 0) | (d->b_t ? 1 : 0);
   // short-K GEMMs: the 3-stage LDS-DMA kernel (3 blocks/CU overlap prologues/epilogues); long-K GEMMs: the

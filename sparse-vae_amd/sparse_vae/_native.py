@@ -53,6 +53,7 @@ class AttnDesc(ctypes.Structure):
         ('sdk', c_int64), ('sdv', c_int64), ('bdk', c_int64), ('bdv', c_int64),
         ('rot_tab', c_void_p), ('rot_d', c_int32),
         ('o32', c_void_p), ('so32', c_int64), ('bo32', c_int64),
+        ('dq_part', c_void_p), ('dq_bf', c_void_p), ('ldq_bf', c_int64),
     ]
 
 
@@ -66,6 +67,7 @@ _SIGS = {
     'svae_colsum': [c_void_p, c_int32, c_int32, c_int32, c_int64, c_void_p, c_int32, c_void_p],
     'svae_attn_fwd': [ctypes.POINTER(AttnDesc), c_void_p],
     'svae_attn_bwd': [ctypes.POINTER(AttnDesc), c_void_p],
+    'svae_attn_dq_part_elems': [c_int32, c_int32, c_int32, c_int32, c_int32],
     'svae_dq_finalize': [c_void_p, c_void_p, c_int64, c_int32, c_int32, c_void_p, c_int32, c_void_p],
     'svae_embedding_fwd': [c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p],
     'svae_embedding_bwd': [c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p],
@@ -101,7 +103,7 @@ def _load():
     for name, argtypes in _SIGS.items():
         fn = getattr(lib, name)
         fn.argtypes = argtypes
-        fn.restype = ctypes.c_char_p if name == 'svae_version' else ctypes.c_int
+        fn.restype = {'svae_version': ctypes.c_char_p, 'svae_attn_dq_part_elems': c_int64}.get(name, ctypes.c_int)
     return lib
 
 

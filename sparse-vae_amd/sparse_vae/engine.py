@@ -289,6 +289,12 @@ class VAEEngine:
         st.update(h2=h2, gprime=gprime, f=f, xc=xc, rows_q=rows_q)
         return out, st
 
+    def _dq_part(self, B, H, Lq, Lk, hd):
+        """f32 workspace for the attention backward's per-key-block dQ partials (shared by all layers)."""
+        n = K.attn_dq_part_elems(B, H, Lq, Lk, hd)
+        t = self.ws.bufs.get('b.dqpart')
+        return t if t is not None and t.numel() >= n else self.ws.get('b.dqpart', (n,), f32)
+
     def layer_bwd(self, st, dout, dx_out, *, dx_accumulate=False, dctx=None):
         """Backward of layer_fwd. dout f32 [B*Lq, d] (consumed as scratch). Writes d x into dx_out
         (accumulating into it when dx_accumulate and the layer has no residual); cross-attention context
@@ -319,17 +325,15 @@ class VAEEngine:
             self._dw(gxc, st['Oc'], c + 'output_linear.weight', rows_q, d, d, bias=c + 'output_linear.bias')
             dOc = ws.get('b.dO', (rows_q, d))
             K.gemm(gxc, P.w(c + 'output_linear.weight'), dOc, rows_q, d, d, b_t=True, epi=EPI_BF16)
-            dq32 = ws.get('b.dq32', (rows_q, d), f32, zero=True)
+            dqc = ws.get('b.dqc', (rows_q, d))
             dkvc = ws.get('b.dkvc', (rows_c, 2 * d))
             delta = ws.get('b.delta', (B, heads, Lq), f32)
             K.attention(st['qc'], st['kvc'], st['kvc'][:, d:], st['Oc'], st['lsec'], B=B, H=heads, Lq=Lq, Lk=L,
                         hd=hd, sq=d, bq=Lq * d, sk=2 * d, sv=2 * d, bk=L * 2 * d, bv=L * 2 * d, so=d, bo=Lq * d,
                         key_pad=st['pad_ctx'], causal=False, backward=True,
-                        dout=dOc, sdo=d, bdo=Lq * d, delta=delta, dq=dq32, bdq=Lq * d, dk=dkvc, dv=dkvc[:, d:],
+                        dout=dOc, sdo=d, bdo=Lq * d, delta=delta, dq_bf=dqc, ldq_bf=d, dk=dkvc, dv=dkvc[:, d:],
                         sdk=2 * d, sdv=2 * d, bdk=L * 2 * d, bdv=L * 2 * d, rot=rot, rot_d=d, o32=st['Oc32'],
-                        so32=d, bo32=Lq * d)
-            dqc = ws.get('b.dqc', (rows_q, d))
-            K.dq_finalize(dq32, dqc, d, rows_q, d, rot, Lq)
+                        so32=d, bo32=Lq * d, dq_part=self._dq_part(B, heads, Lq, L, hd))
             self._dw(dqc, st['hq'], c + 'q_linear.weight', rows_q, d, d, bias=c + 'q_linear.bias')
             dhq = ws.get('b.dhq', (rows_q, d))
             K.gemm(dqc, P.w(c + 'q_linear.weight'), dhq, rows_q, d, d, b_t=True, epi=EPI_BF16)
@@ -347,27 +351,27 @@ class VAEEngine:
         delta = ws.get('b.delta', (B, heads, Lq), f32)
         if st['learned']:
             kv = st['kv']
-            dq32 = ws.get('b.dq32', (B * Lq, d), f32, zero=True)
+            dq32 = ws.get('b.dq32', (B * Lq, d), f32)
             dkv = ws.get('b.dkv', (rows_x, 2 * d))
             K.attention(P.w(a + 'learned_queries').view(Lq, d), kv, kv[:, d:], st['O'], st['lse'], B=B, H=heads,
                         Lq=Lq, Lk=Sx, hd=hd, sq=d, bq=0, sk=2 * d, sv=2 * d, bk=Sx * 2 * d, bv=Sx * 2 * d, so=d,
                         bo=Lq * d, key_pad=st['pad_k'], causal=False, backward=True, dout=dO, sdo=d, bdo=Lq * d,
                         delta=delta, dq=dq32, bdq=Lq * d, dk=dkv, dv=dkv[:, d:], sdk=2 * d, sdv=2 * d,
-                        bdk=Sx * 2 * d, bdv=Sx * 2 * d, rot=rot, rot_d=d, o32=st['O32'], so32=d, bo32=Lq * d)
+                        bdk=Sx * 2 * d, bdv=Sx * 2 * d, rot=rot, rot_d=d, o32=st['O32'], so32=d, bo32=Lq * d,
+                        dq_part=self._dq_part(B, heads, Lq, Sx, hd))
             K.colsum(dq32, B, Lq * d, Lq * d, P.g(a + 'learned_queries').view(-1))
             self._dw(dkv, st['h'], a + 'k_linear.weight', rows_x, 2 * d, d, bias=a + 'k_linear.bias')
             dh = ws.get('b.dh', (rows_x, d))
             K.gemm(dkv, P.w(a + 'k_linear.weight'), dh, rows_x, d, 2 * d, b_t=True, epi=EPI_BF16)
         else:
             qkv = st['qkv']
-            dq32 = ws.get('b.dq32', (rows_x, d), f32, zero=True)
             dqkv = ws.get('b.dqkv', (rows_x, 3 * d))
             K.attention(qkv, qkv[:, d:], qkv[:, 2 * d:], st['O'], st['lse'], B=B, H=heads, Lq=Lq, Lk=Sx, hd=hd,
                         sq=3 * d, bq=Sx * 3 * d, sk=3 * d, sv=3 * d, bk=Sx * 3 * d, bv=Sx * 3 * d, so=d, bo=Lq * d,
                         key_pad=st['pad_k'], causal=st['causal'], backward=True, dout=dO, sdo=d, bdo=Lq * d,
-                        delta=delta, dq=dq32, bdq=Sx * d, dk=dqkv[:, d:], dv=dqkv[:, 2 * d:], sdk=3 * d, sdv=3 * d,
-                        bdk=Sx * 3 * d, bdv=Sx * 3 * d, rot=rot, rot_d=d, o32=st['O32'], so32=d, bo32=Lq * d)
-            K.dq_finalize(dq32, dqkv, 3 * d, rows_x, d, rot, Sx)
+                        delta=delta, dq_bf=dqkv, ldq_bf=3 * d, dk=dqkv[:, d:], dv=dqkv[:, 2 * d:], sdk=3 * d,
+                        sdv=3 * d, bdk=Sx * 3 * d, bdv=Sx * 3 * d, rot=rot, rot_d=d, o32=st['O32'], so32=d,
+                        bo32=Lq * d, dq_part=self._dq_part(B, heads, Lq, Sx, hd))
             self._dw(dqkv, st['h'], a + 'q_linear.weight', rows_x, 3 * d, d, bias=a + 'q_linear.bias')
             dh = ws.get('b.dh', (rows_x, d))
             K.gemm(dqkv, P.w(a + 'q_linear.weight'), dh, rows_x, d, 3 * d, b_t=True, epi=EPI_BF16)

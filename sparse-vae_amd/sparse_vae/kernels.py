@@ -95,7 +95,10 @@ _attn_desc = N.AttnDesc()
 
 def attention(q, k, v, o, lse, *, B, H, Lq, Lk, hd, sq, sk, sv, so, bq, bk, bv, bo, key_pad=None, causal=False,
               scale=None, backward=False, dout=None, sdo=0, bdo=0, delta=None, dq=None, bdq=0, dk=None, dv=None,
-              sdk=0, sdv=0, bdk=0, bdv=0, rot=None, rot_d=0, o32=None, so32=0, bo32=0):
+              sdk=0, sdv=0, bdk=0, bdv=0, rot=None, rot_d=0, o32=None, so32=0, bo32=0, dq_part=None, dq_bf=None,
+              ldq_bf=0):
+    """Forward (o, lse[, o32]) or backward (dk, dv and dq: f32 `dq` or bf16 `dq_bf` with inverse rotary).
+    dq_part: f32 workspace of attn_dq_part_elems(...) floats (allocated here when not given)."""
     d = _attn_desc
     d.q, d.k, d.v, d.o = q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr()
     d.sq, d.sk, d.sv, d.so, d.bq, d.bk, d.bv, d.bo = sq, sk, sv, so, bq, bk, bv, bo
@@ -106,13 +109,22 @@ def attention(q, k, v, o, lse, *, B, H, Lq, Lk, hd, sq, sk, sv, so, bq, bk, bv, 
     d.o32, d.so32, d.bo32 = ptr(o32), so32, bo32
     if backward:
         d.dout, d.sdo, d.bdo = dout.data_ptr(), sdo, bdo
-        d.delta, d.dq, d.bdq = delta.data_ptr(), dq.data_ptr(), bdq
+        d.delta, d.bdq = delta.data_ptr(), bdq
         d.dk, d.dv, d.sdk, d.sdv, d.bdk, d.bdv = dk.data_ptr(), dv.data_ptr(), sdk, sdv, bdk, bdv
         d.rot_tab, d.rot_d = ptr(rot), rot_d
+        if dq_part is None:
+            dq_part = torch.empty(attn_dq_part_elems(B, H, Lq, Lk, hd), device=q.device, dtype=torch.float32)
+        assert dq_part.numel() >= attn_dq_part_elems(B, H, Lq, Lk, hd) and dq_part.dtype == torch.float32
+        d.dq_part, d.dq_bf, d.ldq_bf = dq_part.data_ptr(), ptr(dq_bf), ldq_bf
+        d.dq = ptr(dq)
         check(lib.svae_attn_bwd(ctypes.byref(d), stream()), 'svae_attn_bwd')
     else:
         d.dout = None
         check(lib.svae_attn_fwd(ctypes.byref(d), stream()), 'svae_attn_fwd')
+
+
+def attn_dq_part_elems(B, H, Lq, Lk, hd):
+    return lib.svae_attn_dq_part_elems(B, H, Lq, Lk, hd)
 
 
 def dq_finalize(dq, out, ldo, rows, D, rot=None, seq=0):

@@ -191,6 +191,8 @@ def _attn_ref(q, k, v, pad, causal, scale):
     (2, 2, 96, 96, 96, True, True, False),
     (1, 2, 130, 130, 32, True, False, False),
     (2, 8, 64, 64, 16, False, False, False),
+    (2, 2, 512, 512, 64, True, True, False),
+    (1, 2, 300, 520, 64, False, True, False),
 ])
 def test_attention_fwd_bwd(B, H, Lq, Lk, hd, causal, padded, learned):
     torch.manual_seed(Lq * 7 + hd)
@@ -220,7 +222,7 @@ def test_attention_fwd_bwd(B, H, Lq, Lk, hd, causal, padded, learned):
     assert _rel(o, ref_o) < 1e-2
     do = torch.randn(B, Lq, d, device=dev).bfloat16()
     ref_o.backward(do.float())
-    dq = torch.zeros(B, Lq, d, device=dev)
+    dq = torch.full((B, Lq, d), 7.0, device=dev)    # written, not accumulated
     dk = torch.empty(B, Lk, d, device=dev, dtype=torch.bfloat16)
     dv = torch.empty_like(dk)
     delta = torch.empty(B, H, Lq, device=dev)
@@ -233,6 +235,34 @@ def test_attention_fwd_bwd(B, H, Lq, Lk, hd, causal, padded, learned):
     assert _rel(dq, unheads(qr.grad)) < 2e-2
     assert _rel(dk, unheads(kr.grad)) < 2e-2
     assert _rel(dv, unheads(vr.grad)) < 2e-2
+
+
+def test_attention_bwd_fused_dq_rotary():
+    """bf16 dQ from the partial-sum reduce with inverse rotary == f32 dQ followed by dq_finalize."""
+    torch.manual_seed(9)
+    B, H, L, hd = 2, 4, 256, 64
+    d = H * hd
+    qkv = torch.randn(B * L, 3 * d, device=dev).bfloat16()
+    o = torch.empty(B * L, d, device=dev, dtype=torch.bfloat16)
+    lse = torch.empty(B, H, L, device=dev)
+    rot = rotary_table(L, d).to(dev)
+    common = dict(B=B, H=H, Lq=L, Lk=L, hd=hd, sq=3 * d, bq=L * 3 * d, sk=3 * d, sv=3 * d, bk=L * 3 * d,
+                  bv=L * 3 * d, so=d, bo=L * d, causal=True)
+    K.attention(qkv, qkv[:, d:], qkv[:, 2 * d:], o, lse, **common)
+    do = torch.randn(B * L, d, device=dev).bfloat16()
+    delta = torch.empty(B, H, L, device=dev)
+    g32 = torch.empty(B * L, 3 * d, device=dev, dtype=torch.bfloat16)
+    gbf = torch.empty_like(g32)
+    dq = torch.empty(B * L, d, device=dev)
+    bw = dict(backward=True, dout=do, sdo=d, bdo=L * d, delta=delta, sdk=3 * d, sdv=3 * d, bdk=L * 3 * d,
+              bdv=L * 3 * d, rot=rot, rot_d=d)
+    K.attention(qkv, qkv[:, d:], qkv[:, 2 * d:], o, lse, dq=dq, bdq=L * d, dk=g32[:, d:], dv=g32[:, 2 * d:],
+                **bw, **common)
+    K.dq_finalize(dq, g32, 3 * d, B * L, d, rot, L)
+    K.attention(qkv, qkv[:, d:], qkv[:, 2 * d:], o, lse, dq_bf=gbf, ldq_bf=3 * d, dk=gbf[:, d:], dv=gbf[:, 2 * d:],
+                **bw, **common)
+    torch.cuda.synchronize()
+    assert _rel(gbf, g32.float()) < 1e-3
 
 
 def test_attention_bwd_inverse_rotary_and_dq_finalize():
