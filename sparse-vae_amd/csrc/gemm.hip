@@ -33,6 +33,7 @@ struct GP {
   const int* labels; float* label_logit;
   float* a_rowsum;   // optional: += sum_k A[m][k] (bias gradient fused into the dW GEMM); a_t layout only
   int epi;
+  int tn2, tm2;      // 256-tile counts (gemm256)
 };
 
 // byte offset of (row, 16-B chunk c) in a K-contiguous [128][64] bf16 tile (128-B rows)
@@ -546,6 +547,184 @@ __global__ __launch_bounds__(256, 3) void gemm_glds_kernel(GP p) {
   }
 }
 
+// ===================================================================================================
+// gemm256: 256x256 output tile per 512-thread block (8 waves as 2 (M) x 4 (N), each wave 128 x 64 =
+// 8 x 4 accumulator tiles), BK = 64, A and B K-tiles double-buffered in LDS (2 x 64 KiB) and filled by
+// LDS-DMA one whole K-tile ahead: the next tile's 64 DMA pieces are issued right after the barrier that
+// frees its buffer, so they fly under the current tile's 128 MFMAs per wave. One counted wait + raw barrier
+// per K-tile. Inside a K-tile the wave walks its four 64 x 32 quadrants (A fragments reused across two,
+// B fragments across the turn), 16 MFMAs each. Layouts: A [M][K] (K-contiguous, 128-B rows, kc_off
+// swizzle); B [N][K] likewise, or B [K][N] (b_t) as two [64][128] MN-contiguous halves read with
+// ds_read_b64_tr_b16 (mn_off swizzle). All swizzles are applied on the DMA SOURCE address (the LDS image is
+// lane-linear per 1-KiB piece) and undone by the fragment reads. Epilogue: four 64-row passes staged as
+// f32 through the (then idle) LDS and handed to the shared vectorised epilogue, one 128-column half per
+// 256 threads.
+constexpr int G3_T = 256 * 64 * 2;   // 32 KiB per operand K-tile
+constexpr int G3_STAGE = 2 * G3_T;
+
+template <bool BT>
+__device__ __forceinline__ void g3_issue(const GP& p, const bf16* A, const bf16* B, int m0, int n0, int k0, int kend,
+                                         char* stage, int wave, int lane) {
+  // A: 32 pieces of 8 rows x 128 B; wave w issues pieces 4w..4w+3
+  {
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(A + (long long)m0 * p.lda + k0), 0, 0x7FFFFFF0, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int piece = wave * 4 + i;
+      const int r = piece * 8 + (lane >> 3), c = (lane & 7) ^ ((r >> 1) & 7);
+      const bool ok = (m0 + r < p.M) && (k0 + c * 8 < kend);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(stage + piece * 1024), 16,
+                                               ok ? (r * (int)p.lda + c * 8) * 2 : 0x7FFFFFF0, 0, 0, 0);
+    }
+  }
+  char* bst = stage + G3_T;
+  if constexpr (!BT) {
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(B + (long long)n0 * p.ldb + k0), 0, 0x7FFFFFF0, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int piece = wave * 4 + i;
+      const int r = piece * 8 + (lane >> 3), c = (lane & 7) ^ ((r >> 1) & 7);
+      const bool ok = (n0 + r < p.N) && (k0 + c * 8 < kend);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(bst + piece * 1024), 16,
+                                               ok ? (r * (int)p.ldb + c * 8) * 2 : 0x7FFFFFF0, 0, 0, 0);
+    }
+  } else {
+    // two [64 k][128 n] halves (16 KiB, 16 pieces of 4 k-rows x 256 B each); wave w issues pieces 4w..4w+3
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(B + (long long)k0 * p.ldb + n0), 0, 0x7FFFFFF0, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int piece = wave * 4 + i, half = piece >> 4;
+      const int kr = (piece & 15) * 4 + (lane >> 4);
+      const int sk = (kr & 3) | (((kr >> 3) & 1) << 2);
+      const int v = (lane & 15) ^ (sk << 1);
+      const int col = half * 128 + v * 8;
+      const bool ok = (k0 + kr < kend) && (n0 + col < p.N);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(bst + piece * 1024), 16,
+                                               ok ? (kr * (int)p.ldb + col) * 2 : 0x7FFFFFF0, 0, 0, 0);
+    }
+  }
+}
+
+// B fragment (16 n x 32 k) of n-tile at column cb (0..255) of the B tile, k-step ks
+template <bool BT>
+__device__ __forceinline__ bf16x8 g3_bfrag(const char* lb, int cb, int ks, int lane) {
+  if constexpr (!BT) return *(const bf16x8*)(lb + kc_off(cb + (lane & 15), (lane >> 4) + 4 * ks));
+  else return read_frag<true>(lb + (cb >> 7) * (G3_T / 2), cb & 127, ks, lane);
+}
+
+template <bool BT, int EPI>
+__global__ __launch_bounds__(512, 1) void gemm256_kernel(GP p) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * G3_STAGE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  // XCD-aware bijective remap, then N-fastest
+  const int nwg = gridDim.x;
+  int bid = blockIdx.x;
+  if (nwg >= 16) {
+    const int q = nwg / 8, r = nwg % 8, xcd = bid % 8, idx = bid / 8;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+  }
+  const int tiles = p.tn2 * p.tm2;
+  const int batch = bid / tiles, t = bid - batch * tiles;
+  const int bn = t % p.tn2, bm = t / p.tn2;
+  const int m0 = bm * 256, n0 = bn * 256;
+  const int kend = p.K;
+  const bf16* A = p.A + batch * p.sA;
+  const bf16* B = p.B + batch * p.sB;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (p.K + 63) / 64;
+  g3_issue<BT>(p, A, B, m0, n0, 0, kend, smem, wave, lane);
+  for (int kt = 0; kt < nk; ++kt) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's pieces of tile kt landed
+    __builtin_amdgcn_s_barrier();                      // everyone's pieces landed; tile kt-1 fully consumed
+    const char* la = smem + (kt & 1) * G3_STAGE;
+    const char* lb = la + G3_T;
+    if (kt + 1 < nk) g3_issue<BT>(p, A, B, m0, n0, (kt + 1) * 64, kend, smem + ((kt + 1) & 1) * G3_STAGE, wave, lane);
+    bf16x8 af[4][2], b0[2][2], b1[2][2];
+    // quadrant (mh 0, nh 0)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) af[i][ks] = *(const bf16x8*)(la + kc_off(wr * 128 + i * 16 + (lane & 15), (lane >> 4) + 4 * ks));
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) b0[j][ks] = g3_bfrag<BT>(lb, wc * 64 + j * 16, ks, lane);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = mfma16(af[i][ks], b0[j][ks], acc[i][j]);
+    // (mh 0, nh 1)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) b1[j][ks] = g3_bfrag<BT>(lb, wc * 64 + 32 + j * 16, ks, lane);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][2 + j] = mfma16(af[i][ks], b1[j][ks], acc[i][2 + j]);
+    // (mh 1, nh 1)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        af[i][ks] = *(const bf16x8*)(la + kc_off(wr * 128 + 64 + i * 16 + (lane & 15), (lane >> 4) + 4 * ks));
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[4 + i][2 + j] = mfma16(af[i][ks], b1[j][ks], acc[4 + i][2 + j]);
+    // (mh 1, nh 0)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[4 + i][j] = mfma16(af[i][ks], b0[j][ks], acc[4 + i][j]);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  // epilogue: 4 passes of 64 rows; staging = two [64][128] f32 halves (64 KiB)
+  float* cs = (float*)smem;
+  const long long cofs = (long long)batch * p.sC;
+  const int half = tid >> 8;
+#pragma unroll
+  for (int pass = 0; pass < 4; ++pass) {
+    if (wr == (pass >> 1)) {
+#pragma unroll
+      for (int ii = 0; ii < 4; ++ii) {
+        const int i = (pass & 1) * 4 + ii;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = ii * 16 + 4 * (lane >> 4) + r;
+            const int col = wc * 64 + j * 16 + (lane & 15);
+            cs[(col >> 7) * 8192 + row * 128 + cs_swz(row, col & 127)] = p.alpha * acc[i][j][r];
+          }
+      }
+    }
+    __syncthreads();
+    epilogue_half<EPI>(p, cs + half * 8192, m0, n0 + 128 * half, bn * 2 + half, pass * 64, cofs, tid & 255);
+    __syncthreads();
+  }
+}
+
 }  // namespace
 
 SVAE_EXPORT int svae_gemm(const svae_gemm_desc* d, svae_stream_t stream) {
@@ -598,7 +777,34 @@ SVAE_EXPORT int svae_gemm(const svae_gemm_desc* d, svae_stream_t stream) {
   // BK=64 register-staged kernel (half the barriers per MFMA). SVAE_GEMM_IMPL=1/2 forces one (A/B runs).
   static const int forced = [] { const char* e = getenv("SVAE_GEMM_IMPL"); return e ? atoi(e) : 0; }();
   const int kslice = (d->K + d->splits - 1) / d->splits;
-  const int impl = forced ? forced : ((kslice <= 2048 && !(d->a_t && d->b_t)) ? 2 : 1);
+  p.tn2 = (d->N + 255) / 256;
+  p.tm2 = (d->M + 255) / 256;
+  const long long blocks256 = (long long)p.tn2 * p.tm2 * d->batch;
+  const bool fit3 = !d->a_t && d->splits == 1 && !d->a_rowsum && blocks256 >= 192;
+  int impl = forced ? forced : (fit3 ? 3 : ((kslice <= 2048 && !(d->a_t && d->b_t)) ? 2 : 1));
+  if (impl == 3 && !(!d->a_t && d->splits == 1 && !d->a_rowsum)) impl = (kslice <= 2048 && !(d->a_t && d->b_t)) ? 2 : 1;
+  if (impl == 3) {
+    dim3 grid3((unsigned)blocks256);
+#define SVAE_GEMM3_CASE(E)                                                                                   \
+  case E:                                                                                                    \
+    if (d->b_t) hipLaunchKernelGGL((gemm256_kernel<true, E>), grid3, dim3(512), 0, s, p);                    \
+    else hipLaunchKernelGGL((gemm256_kernel<false, E>), grid3, dim3(512), 0, s, p);                          \
+    break;
+    switch (d->epi) {
+      SVAE_GEMM3_CASE(SVAE_EPI_BF16)
+      SVAE_GEMM3_CASE(SVAE_EPI_F32)
+      SVAE_GEMM3_CASE(SVAE_EPI_F32_ACC)
+      SVAE_GEMM3_CASE(SVAE_EPI_GELU)
+      SVAE_GEMM3_CASE(SVAE_EPI_GELU_BWD)
+      SVAE_GEMM3_CASE(SVAE_EPI_DROPOUT_RESID)
+      SVAE_GEMM3_CASE(SVAE_EPI_ROTARY_BF16)
+      SVAE_GEMM3_CASE(SVAE_EPI_CE_STATS)
+      default: return SVAE_EINVAL;
+    }
+#undef SVAE_GEMM3_CASE
+    SVAE_LAUNCH_CHECK();
+    return SVAE_OK;
+  }
   if (impl == 2) {
     int kchunk2 = (d->K + d->splits - 1) / d->splits;
     p.kchunk = (kchunk2 + BK2 - 1) / BK2 * BK2;

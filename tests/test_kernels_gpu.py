@@ -20,7 +20,8 @@ def _rel(a, b):
     return ((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-30)).item()
 
 
-@pytest.mark.parametrize('M,Nn,Kk', [(128, 128, 64), (200, 136, 72), (512, 384, 1024), (64, 1536, 512)])
+@pytest.mark.parametrize('M,Nn,Kk', [(128, 128, 64), (200, 136, 72), (512, 384, 1024), (64, 1536, 512),
+                                     (4000, 3064, 520)])   # last: >= 192 256x256 tiles -> gemm256 for a_t = 0
 @pytest.mark.parametrize('a_t,b_t', [(0, 0), (0, 1), (1, 1), (1, 0)])
 def test_gemm_layouts_exact(M, Nn, Kk, a_t, b_t):
     g = torch.Generator(device=dev).manual_seed(M + Nn + Kk)
@@ -47,9 +48,9 @@ def test_gemm_split_k_atomic_and_acc():
     assert torch.equal(C, 1 + 2 * (A.t() @ B))
 
 
-def test_gemm_epilogues():
+@pytest.mark.parametrize('M,Nn,Kk', [(300, 256, 192), (4000, 3072, 520)])   # small: 128-tile kernels; big: gemm256
+def test_gemm_epilogues(M, Nn, Kk):
     torch.manual_seed(0)
-    M, Nn, Kk = 300, 256, 192
     X = torch.randn(M, Kk, device=dev).bfloat16()
     W = (torch.randn(Nn, Kk, device=dev) * 0.1).bfloat16()
     b = torch.randn(Nn, device=dev)
@@ -100,9 +101,9 @@ def test_gemm_epilogues():
     assert agree.all()
 
 
-def test_gemm_rotary_matches_reference_rotation():
+@pytest.mark.parametrize('B,L,d', [(2, 96, 256), (16, 512, 512)])
+def test_gemm_rotary_matches_reference_rotation(B, L, d):
     torch.manual_seed(1)
-    B, L, d = 2, 96, 256
     X = torch.randn(B * L, d, device=dev).bfloat16()
     W = (torch.randn(3 * d, d, device=dev) * 0.05).bfloat16()
     b = torch.randn(3 * d, device=dev) * 0.1
@@ -114,9 +115,10 @@ def test_gemm_rotary_matches_reference_rotation():
     assert _rel(C.view(B, L, 3 * d).cpu(), ref) < 4e-3
 
 
-def test_ce_stats_epilogue_and_finalize():
+@pytest.mark.parametrize('T', [256, 512])
+def test_ce_stats_epilogue_and_finalize(T):
     torch.manual_seed(2)
-    T, d, V, L = 256, 128, 32768, 128
+    d, V, L = 128, 32768, 128
     X = torch.randn(T, d, device=dev).bfloat16()
     W = (torch.randn(V, d, device=dev) * 0.1).bfloat16()
     b = torch.randn(V, device=dev) * 0.1
