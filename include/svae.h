@@ -36,7 +36,9 @@ enum svae_epi {
   SVAE_EPI_BF16 = 0,          /* C bf16 = alpha*acc + bias                                            */
   SVAE_EPI_F32 = 1,           /* C f32  = alpha*acc + bias (+ resid)                                  */
   SVAE_EPI_F32_ACC = 2,       /* C f32 += alpha*acc                                                   */
-  SVAE_EPI_F32_ATOMIC = 3,    /* atomicAdd(C f32, alpha*acc)   (split-K / shared destinations)        */
+  SVAE_EPI_F32_ATOMIC = 3,    /* atomicAdd(C f32, alpha*acc)   (split-K / shared destinations); with
+                                 splits > 1 and aux != NULL: each split stores its partial tile into the
+                                 f32 workspace aux [splits][M][N] and a reduce pass adds them into C     */
   SVAE_EPI_GELU = 4,          /* C bf16 = gelu(acc + bias);  aux bf16 = gelu'(acc + bias)              */
   SVAE_EPI_GELU_BWD = 5,      /* C bf16 = acc * aux  (aux = the gelu' saved by SVAE_EPI_GELU)          */
   SVAE_EPI_DROPOUT_RESID = 6, /* C f32 = resid + keep(seed, m*N+n) * acc / (1 - p)                     */

@@ -34,6 +34,7 @@ struct GP {
   float* a_rowsum;   // optional: += sum_k A[m][k] (bias gradient fused into the dW GEMM); a_t layout only
   int epi;
   int tn2, tm2;      // 256-tile counts (gemm256)
+  long long slab;    // split-K slab mode: split s writes its partial tile at C + s * slab (0 = off)
 };
 
 // byte offset of (row, 16-B chunk c) in a K-contiguous [128][64] bf16 tile (128-B rows)
@@ -387,7 +388,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GP p) {
         cs[row * 128 + cs_swz(row, col)] = p.alpha * acc[i][j][r];
       }
   __syncthreads();
-  const long long cofs = (long long)batch * p.sC;
+  const long long cofs = (long long)batch * p.sC + split * p.slab;
   epilogue_half<EPI>(p, cs, m0, n0, bn, 0, cofs, tid);
   epilogue_half<EPI>(p, cs + 64 * 128, m0, n0, bn, 64, cofs, tid);
 }
@@ -526,7 +527,7 @@ __global__ __launch_bounds__(256, 3) void gemm_glds_kernel(GP p) {
   __syncthreads();
   // epilogue in two halves of 64 rows (the ring holds 48 KiB; a half tile of f32 is 32 KiB)
   float* cs = (float*)smem;
-  const long long cofs = (long long)batch * p.sC;
+  const long long cofs = (long long)batch * p.sC + split * p.slab;
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     if (wm == h) {
@@ -562,11 +563,32 @@ __global__ __launch_bounds__(256, 3) void gemm_glds_kernel(GP p) {
 constexpr int G3_T = 256 * 64 * 2;   // 32 KiB per operand K-tile
 constexpr int G3_STAGE = 2 * G3_T;
 
-template <bool BT>
+// [64 k][256 mn] MN-contiguous operand as two [64][128] halves (16 KiB, 16 pieces of 4 k-rows x 256 B each);
+// wave w issues pieces 4w..4w+3
+__device__ __forceinline__ void g3_issue_mn(const bf16* G, long long ld, int n0, int nlim, int k0, int kend, char* dst,
+                                            int wave, int lane) {
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(G + (long long)k0 * ld + n0), 0, 0x7FFFFFF0, 0x00020000);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int piece = wave * 4 + i, half = piece >> 4;
+    const int kr = (piece & 15) * 4 + (lane >> 4);
+    const int sk = (kr & 3) | (((kr >> 3) & 1) << 2);
+    const int v = (lane & 15) ^ (sk << 1);
+    const int col = half * 128 + v * 8;
+    const bool ok = (k0 + kr < kend) && (n0 + col < nlim);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(dst + piece * 1024), 16,
+                                             ok ? (kr * (int)ld + col) * 2 : 0x7FFFFFF0, 0, 0, 0);
+  }
+}
+
+template <bool AT, bool BT>
 __device__ __forceinline__ void g3_issue(const GP& p, const bf16* A, const bf16* B, int m0, int n0, int k0, int kend,
                                          char* stage, int wave, int lane) {
   // A: 32 pieces of 8 rows x 128 B; wave w issues pieces 4w..4w+3
-  {
+  if constexpr (AT) {
+    g3_issue_mn(A, p.lda, m0, p.M, k0, kend, stage, wave, lane);
+  } else {
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc((void*)(A + (long long)m0 * p.lda + k0), 0, 0x7FFFFFF0, 0x00020000);
 #pragma unroll
@@ -591,20 +613,7 @@ __device__ __forceinline__ void g3_issue(const GP& p, const bf16* A, const bf16*
                                                ok ? (r * (int)p.ldb + c * 8) * 2 : 0x7FFFFFF0, 0, 0, 0);
     }
   } else {
-    // two [64 k][128 n] halves (16 KiB, 16 pieces of 4 k-rows x 256 B each); wave w issues pieces 4w..4w+3
-    const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc((void*)(B + (long long)k0 * p.ldb + n0), 0, 0x7FFFFFF0, 0x00020000);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int piece = wave * 4 + i, half = piece >> 4;
-      const int kr = (piece & 15) * 4 + (lane >> 4);
-      const int sk = (kr & 3) | (((kr >> 3) & 1) << 2);
-      const int v = (lane & 15) ^ (sk << 1);
-      const int col = half * 128 + v * 8;
-      const bool ok = (k0 + kr < kend) && (n0 + col < p.N);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(bst + piece * 1024), 16,
-                                               ok ? (kr * (int)p.ldb + col) * 2 : 0x7FFFFFF0, 0, 0, 0);
-    }
+    g3_issue_mn(B, p.ldb, n0, p.N, k0, kend, bst, wave, lane);
   }
 }
 
@@ -615,7 +624,14 @@ __device__ __forceinline__ bf16x8 g3_bfrag(const char* lb, int cb, int ks, int l
   else return read_frag<true>(lb + (cb >> 7) * (G3_T / 2), cb & 127, ks, lane);
 }
 
-template <bool BT, int EPI>
+// A fragment (16 m x 32 k) of the m-tile at row rb (0..255), k-step ks
+template <bool AT>
+__device__ __forceinline__ bf16x8 g3_afrag(const char* la, int rb, int ks, int lane) {
+  if constexpr (!AT) return *(const bf16x8*)(la + kc_off(rb + (lane & 15), (lane >> 4) + 4 * ks));
+  else return read_frag<true>(la + (rb >> 7) * (G3_T / 2), rb & 127, ks, lane);
+}
+
+template <bool AT, bool BT, int EPI>
 __global__ __launch_bounds__(512, 1) void gemm256_kernel(GP p) {
   __shared__ __attribute__((aligned(16))) char smem[2 * G3_STAGE];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -629,12 +645,15 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GP p) {
     bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
   }
   const int tiles = p.tn2 * p.tm2;
-  const int batch = bid / tiles, t = bid - batch * tiles;
+  const int z = bid / tiles, t = bid - z * tiles;
+  const int batch = z / p.splits, split = z - batch * p.splits;
   const int bn = t % p.tn2, bm = t / p.tn2;
   const int m0 = bm * 256, n0 = bn * 256;
-  const int kend = p.K;
+  const int kbeg = split * p.kchunk;
+  const int kend = min(p.K, kbeg + p.kchunk);
   const bf16* A = p.A + batch * p.sA;
   const bf16* B = p.B + batch * p.sB;
+  float rsum[4] = {0.f, 0.f, 0.f, 0.f};
 
   f32x4 acc[8][4];
 #pragma unroll
@@ -642,20 +661,21 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GP p) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  const int nk = (p.K + 63) / 64;
-  g3_issue<BT>(p, A, B, m0, n0, 0, kend, smem, wave, lane);
+  const int nk = kend > kbeg ? (kend - kbeg + 63) / 64 : 0;
+  if (nk > 0) g3_issue<AT, BT>(p, A, B, m0, n0, kbeg, kend, smem, wave, lane);
   for (int kt = 0; kt < nk; ++kt) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's pieces of tile kt landed
     __builtin_amdgcn_s_barrier();                      // everyone's pieces landed; tile kt-1 fully consumed
     const char* la = smem + (kt & 1) * G3_STAGE;
     const char* lb = la + G3_T;
-    if (kt + 1 < nk) g3_issue<BT>(p, A, B, m0, n0, (kt + 1) * 64, kend, smem + ((kt + 1) & 1) * G3_STAGE, wave, lane);
+    if (kt + 1 < nk)
+      g3_issue<AT, BT>(p, A, B, m0, n0, kbeg + (kt + 1) * 64, kend, smem + ((kt + 1) & 1) * G3_STAGE, wave, lane);
     bf16x8 af[4][2], b0[2][2], b1[2][2];
     // quadrant (mh 0, nh 0)
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) af[i][ks] = *(const bf16x8*)(la + kc_off(wr * 128 + i * 16 + (lane & 15), (lane >> 4) + 4 * ks));
+      for (int ks = 0; ks < 2; ++ks) af[i][ks] = g3_afrag<AT>(la, wr * 128 + i * 16, ks, lane);
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -681,8 +701,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GP p) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-        af[i][ks] = *(const bf16x8*)(la + kc_off(wr * 128 + 64 + i * 16 + (lane & 15), (lane >> 4) + 4 * ks));
+      for (int ks = 0; ks < 2; ++ks) af[i][ks] = g3_afrag<AT>(la, wr * 128 + 64 + i * 16, ks, lane);
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
@@ -696,12 +715,32 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GP p) {
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[4 + i][j] = mfma16(af[i][ks], b0[j][ks], acc[4 + i][j]);
+    if constexpr (AT) {
+      if (p.a_rowsum && bn == 0) {   // sum_k A[k][m]: thread = 4 m (one 8-B unit) x 8 k-rows
+        const int u = tid & 63, kg = tid >> 6;
+        const char* lh = la + (u >> 5) * (G3_T / 2);
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          const bf16x4 v = __builtin_bit_cast(bf16x4, *(const short4v*)(lh + mn_off(kg * 8 + r, u & 31)));
+#pragma unroll
+          for (int e = 0; e < 4; ++e) rsum[e] += (float)v[e];
+        }
+      }
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  if constexpr (AT) {
+    if (p.a_rowsum && bn == 0) {
+      const int m = m0 + (tid & 63) * 4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (m + e < p.M) atomicAdd(p.a_rowsum + m + e, rsum[e]);
+    }
+  }
   // epilogue: 4 passes of 64 rows; staging = two [64][128] f32 halves (64 KiB)
   float* cs = (float*)smem;
-  const long long cofs = (long long)batch * p.sC;
+  const long long cofs = (long long)batch * p.sC + split * p.slab;
   const int half = tid >> 8;
 #pragma unroll
   for (int pass = 0; pass < 4; ++pass) {
@@ -725,7 +764,31 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GP p) {
   }
 }
 
+// C[m][n] += sum over splits of slab[s][m][n] (slab rows of N floats); 4 columns per thread
+__global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restrict__ slab, float* __restrict__ C,
+                                                          int M, int N, long long ldc, int splits) {
+  const int N4 = N / 4;
+  const long long total = (long long)M * N4, plane = (long long)M * N;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const long long m = i / N4;
+    const int n = (int)(i - m * N4) * 4;
+    const float* src = slab + m * N + n;
+    f32x4 acc = *(const f32x4*)src;
+    for (int s = 1; s < splits; ++s) acc += *(const f32x4*)(src + s * plane);
+    f32x4* dst = (f32x4*)(C + m * ldc + n);
+    *dst = *dst + acc;
+  }
+}
+
 }  // namespace
+
+static int launch_slab_reduce(const svae_gemm_desc* d, hipStream_t s) {
+  const long long work = (long long)d->M * (d->N / 4);
+  hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)min(4096LL, (work + 255) / 256)), dim3(256), 0, s,
+                     (const float*)d->aux, (float*)d->C, d->M, d->N, (long long)d->ldc, d->splits);
+  SVAE_LAUNCH_CHECK();
+  return SVAE_OK;
+}
 
 SVAE_EXPORT int svae_gemm(const svae_gemm_desc* d, svae_stream_t stream) {
   if (!d || !d->A || !d->B || !d->C) return SVAE_EINVAL;
@@ -767,6 +830,17 @@ SVAE_EXPORT int svae_gemm(const svae_gemm_desc* d, svae_stream_t stream) {
   p.labels = d->labels; p.label_logit = d->label_logit;
   p.a_rowsum = d->a_rowsum;
   p.epi = d->epi;
+  p.slab = 0;
+  // split-K slab mode (F32_ATOMIC with aux): every split stores its partial tile with plain stores into
+  // aux[split][M][N], then slab_reduce adds the splits into C (no float atomics on C).
+  const bool slab = d->epi == SVAE_EPI_F32_ATOMIC && d->splits > 1 && d->aux;
+  int epi_run = d->epi;
+  if (slab) {
+    if (d->batch != 1 || ((uintptr_t)d->aux & 15) || d->N % 4) return SVAE_EINVAL;
+    p.C = d->aux; p.ldc = d->N; p.sC = 0; p.slab = (long long)d->M * d->N;
+    p.bias = nullptr; p.resid = nullptr;
+    epi_run = SVAE_EPI_F32;
+  }
 
   const long long nblocks = (long long)p.tiles_n * p.tiles_m * d->batch * d->splits;
   if (nblocks > 0x7FFFFFFF) return SVAE_EINVAL;
@@ -779,18 +853,22 @@ SVAE_EXPORT int svae_gemm(const svae_gemm_desc* d, svae_stream_t stream) {
   const int kslice = (d->K + d->splits - 1) / d->splits;
   p.tn2 = (d->N + 255) / 256;
   p.tm2 = (d->M + 255) / 256;
-  const long long blocks256 = (long long)p.tn2 * p.tm2 * d->batch;
-  const bool fit3 = !d->a_t && d->splits == 1 && !d->a_rowsum && blocks256 >= 192;
-  int impl = forced ? forced : (fit3 ? 3 : ((kslice <= 2048 && !(d->a_t && d->b_t)) ? 2 : 1));
-  if (impl == 3 && !(!d->a_t && d->splits == 1 && !d->a_rowsum)) impl = (kslice <= 2048 && !(d->a_t && d->b_t)) ? 2 : 1;
+  const long long blocks256 = (long long)p.tn2 * p.tm2 * d->batch * d->splits;
+  const bool ok3 = !(d->a_t && !d->b_t);
+  int impl = forced ? forced : ((ok3 && blocks256 >= 192) ? 3 : ((kslice <= 2048 && !(d->a_t && d->b_t)) ? 2 : 1));
+  if (impl == 3 && !ok3) impl = 1;
   if (impl == 3) {
+    int kc3 = (d->K + d->splits - 1) / d->splits;
+    p.kchunk = (kc3 + 63) / 64 * 64;
     dim3 grid3((unsigned)blocks256);
 #define SVAE_GEMM3_CASE(E)                                                                                   \
   case E:                                                                                                    \
-    if (d->b_t) hipLaunchKernelGGL((gemm256_kernel<true, E>), grid3, dim3(512), 0, s, p);                    \
-    else hipLaunchKernelGGL((gemm256_kernel<false, E>), grid3, dim3(512), 0, s, p);                          \
+    if (d->a_t) hipLaunchKernelGGL((gemm256_kernel<true, true, E>), grid3, dim3(512), 0, s, p);              \
+    else if (d->b_t) hipLaunchKernelGGL((gemm256_kernel<false, true, E>), grid3, dim3(512), 0, s, p);        \
+    else hipLaunchKernelGGL((gemm256_kernel<false, false, E>), grid3, dim3(512), 0, s, p);                   \
     break;
-    switch (d->epi) {
+    switch (epi_run) {
+      SVAE_GEMM3_CASE(SVAE_EPI_F32_ATOMIC)
       SVAE_GEMM3_CASE(SVAE_EPI_BF16)
       SVAE_GEMM3_CASE(SVAE_EPI_F32)
       SVAE_GEMM3_CASE(SVAE_EPI_F32_ACC)
@@ -803,7 +881,7 @@ SVAE_EXPORT int svae_gemm(const svae_gemm_desc* d, svae_stream_t stream) {
     }
 #undef SVAE_GEMM3_CASE
     SVAE_LAUNCH_CHECK();
-    return SVAE_OK;
+    return slab ? launch_slab_reduce(d, s) : SVAE_OK;
   }
   if (impl == 2) {
     int kchunk2 = (d->K + d->splits - 1) / d->splits;
@@ -815,7 +893,7 @@ SVAE_EXPORT int svae_gemm(const svae_gemm_desc* d, svae_stream_t stream) {
     else if (lay == 2) hipLaunchKernelGGL((gemm_glds_kernel<true, false, E>), grid, dim3(256), 0, s, p); \
     else hipLaunchKernelGGL((gemm_glds_kernel<true, true, E>), grid, dim3(256), 0, s, p);                \
     break;
-    switch (d->epi) {
+    switch (epi_run) {
       SVAE_GEMM2_CASE(SVAE_EPI_BF16)
       SVAE_GEMM2_CASE(SVAE_EPI_F32)
       SVAE_GEMM2_CASE(SVAE_EPI_F32_ACC)
@@ -829,7 +907,7 @@ SVAE_EXPORT int svae_gemm(const svae_gemm_desc* d, svae_stream_t stream) {
     }
 #undef SVAE_GEMM2_CASE
     SVAE_LAUNCH_CHECK();
-    return SVAE_OK;
+    return slab ? launch_slab_reduce(d, s) : SVAE_OK;
   }
 #define SVAE_GEMM_CASE(E)                                                                             \
   case E:                                                                                             \
@@ -838,7 +916,7 @@ SVAE_EXPORT int svae_gemm(const svae_gemm_desc* d, svae_stream_t stream) {
     else if (lay == 2) hipLaunchKernelGGL((gemm_kernel<true, false, E>), grid, dim3(256), 0, s, p);    \
     else hipLaunchKernelGGL((gemm_kernel<true, true, E>), grid, dim3(256), 0, s, p);                   \
     break;
-  switch (d->epi) {
+  switch (epi_run) {
     SVAE_GEMM_CASE(SVAE_EPI_BF16)
     SVAE_GEMM_CASE(SVAE_EPI_F32)
     SVAE_GEMM_CASE(SVAE_EPI_F32_ACC)
@@ -852,5 +930,5 @@ SVAE_EXPORT int svae_gemm(const svae_gemm_desc* d, svae_stream_t stream) {
   }
 #undef SVAE_GEMM_CASE
   SVAE_LAUNCH_CHECK();
-  return SVAE_OK;
+  return slab ? launch_slab_reduce(d, s) : SVAE_OK;
 }

@@ -54,6 +54,14 @@ def gemm(A, B, C, M, N_, K, *, a_t=False, b_t=False, lda=None, ldb=None, ldc=Non
 
 
 def auto_splits(M, N_, K, target=512):
+    """Split-K count for a dW GEMM. First choice: >= 192 blocks of the 256x256 kernel (the library picks it
+    at that size) with K-slices of >= 2048; otherwise ~`target` blocks of the 128x128 kernels."""
+    t256 = -(-M // 256) * -(-N_ // 256)
+    if t256 >= 192:
+        return 1
+    s3 = -(-192 // t256)
+    if K // s3 >= 2048:
+        return s3
     tiles = -(-M // 128) * -(-N_ // 128)
     if tiles >= 256 or K < 1024:
         return 1
@@ -65,8 +73,21 @@ def linear_dw(dY, X, Wgrad, rows, n_out, n_in, ldy=None, ldx=None, bgrad=None):
     """Wgrad[n_out, n_in] += dY^T . X over `rows` rows (dY [rows, n_out] bf16, X [rows, n_in] bf16); with
     bgrad, also bgrad[n_out] += column sums of dY (the bias gradient, fused into the same pass over dY)."""
     s = auto_splits(n_out, n_in, rows)
+    slab = _slab_workspace(s * n_out * n_in, dY.device) if s > 1 else None
     gemm(dY, X, Wgrad, n_out, n_in, rows, a_t=True, b_t=True, lda=ldy or n_out, ldb=ldx or n_in, ldc=n_in,
-         epi=N.EPI_F32_ATOMIC if s > 1 else N.EPI_F32_ACC, splits=s, a_rowsum=bgrad)
+         epi=N.EPI_F32_ATOMIC if s > 1 else N.EPI_F32_ACC, splits=s, a_rowsum=bgrad, aux=slab)
+
+
+_slabs = {}
+
+
+def _slab_workspace(n, device):
+    """f32 split-K slab workspace (grown on demand, reused stream-ordered by every dW GEMM)."""
+    t = _slabs.get(device)
+    if t is None or t.numel() < n:
+        t = torch.empty(n, dtype=torch.float32, device=device)
+        _slabs[device] = t
+    return t
 
 
 def layernorm_fwd(x, w, b, y, mean, rstd, rows, D):

@@ -48,6 +48,26 @@ def test_gemm_split_k_atomic_and_acc():
     assert torch.equal(C, 1 + 2 * (A.t() @ B))
 
 
+def test_gemm256_split_k_rowsum_exact():
+    """dW layout on the 256x256 kernel: split-K f32 atomics + fused bias-gradient row sums, and the
+    unsplit f32 accumulate (the tied head's dW), all bit-exact on integer data."""
+    g = torch.Generator(device=dev).manual_seed(11)
+    Kk = 32768
+    for M, Nn, splits, use_slab in [(1536, 512, 16, False), (4096, 768, 1, False), (1536, 512, 16, True),
+                                    (1024, 512, 8, True)]:
+        A = torch.randint(-2, 3, (Kk, M), device=dev, generator=g).float()
+        B = torch.randint(-2, 3, (Kk, Nn), device=dev, generator=g).float()
+        C = torch.ones(M, Nn, device=dev)
+        rs = torch.full((M,), 3.0, device=dev)
+        epi = N.EPI_F32_ATOMIC if splits > 1 else N.EPI_F32_ACC
+        slab = torch.empty(splits, M, Nn, device=dev) if use_slab else None   # slab split-K (plain stores + reduce)
+        K.gemm(A.bfloat16(), B.bfloat16(), C, M, Nn, Kk, a_t=True, b_t=True, epi=epi, splits=splits, a_rowsum=rs,
+               aux=slab)
+        torch.cuda.synchronize()
+        assert torch.equal(C, 1 + A.t() @ B)
+        assert torch.equal(rs, 3 + A.sum(0))
+
+
 @pytest.mark.parametrize('M,Nn,Kk', [(300, 256, 192), (4000, 3072, 520)])   # small: 128-tile kernels; big: gemm256
 def test_gemm_epilogues(M, Nn, Kk):
     torch.manual_seed(0)
