@@ -173,6 +173,11 @@ int svae_dropout_bwd_cast(const float* g, void* out, float p, uint64_t seed, int
 int svae_gelu_bwd(const float* dx, const void* gp, void* out, int64_t n, svae_stream_t stream);
 /* cast f32 -> bf16 (n elements). */
 int svae_cast_bf16(const float* in, void* out, int64_t n, svae_stream_t stream);
+/* Transposed bf16 weight shadows (the K-contiguous B operand of the dX GEMMs): for each of nblocks
+ * blocks, table[4b..4b+3] = (element offset, rows, cols, first tile) on the device, rows and cols % 8 == 0,
+ * dst[offset + c * rows + r] = src[offset + r * cols + c]; one workgroup per 64 x 64 tile. */
+int svae_transpose_blocks(const void* src, void* dst, const int64_t* table, int32_t nblocks, int32_t total_tiles,
+                          svae_stream_t stream);
 /* rows of x (f32 [rows][D], stride ld) whose (row % mod == 0) are copied to out [rows/mod][D] and zeroed
  * (the position-0 gradient of the z-projection splice, transformer_vae.py:89-90). */
 int svae_extract_rows(float* x, int64_t ld, int32_t rows, int32_t mod, int32_t D, float* out,

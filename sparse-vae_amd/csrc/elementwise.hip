@@ -266,6 +266,47 @@ __global__ __launch_bounds__(256) void dq_finalize_kernel(const float* __restric
   }
 }
 
+
+// Transposed bf16 weight shadows: for each block b of table[b] = (offset, rows, cols, first_tile),
+// dst[offset + c * rows + r] = src[offset + r * cols + c]. One 64 x 64 tile per workgroup through a padded LDS
+// tile; 16-B loads and stores (rows, cols % 8 == 0).
+__global__ __launch_bounds__(256) void transpose_blocks_kernel(const bf16* __restrict__ src, bf16* __restrict__ dst,
+                                                               const long long* __restrict__ table, int nb) {
+  __shared__ unsigned short t[64][66];
+  const int tile = blockIdx.x;
+  int b = 0;
+  while (b + 1 < nb && table[(b + 1) * 4 + 3] <= tile) ++b;
+  const long long off = table[b * 4], rows = table[b * 4 + 1], cols = table[b * 4 + 2];
+  const int local = tile - (int)table[b * 4 + 3];
+  const int tcols = (int)((cols + 63) / 64);
+  const int r0 = (local / tcols) * 64, c0 = (local % tcols) * 64;
+  const int tid = threadIdx.x, c8 = (tid & 7) * 8;
+  const unsigned short* s = (const unsigned short*)src + off;
+  unsigned short* d = (unsigned short*)dst + off;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int r = (tid >> 3) + 32 * i;
+    if (r0 + r < rows && c0 + c8 < cols) {
+      const u32x4 v = *(const u32x4*)(s + (r0 + r) * cols + c0 + c8);
+      const unsigned short* e = (const unsigned short*)&v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) t[r][c8 + j] = e[j];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int c = (tid >> 3) + 32 * i;   // output row = input column
+    if (c0 + c < cols && r0 + c8 < rows) {
+      u32x4 v;
+      unsigned short* e = (unsigned short*)&v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) e[j] = t[c8 + j][c];
+      *(u32x4*)(d + (c0 + c) * rows + r0 + c8) = v;
+    }
+  }
+}
+
 // ------------------------------------------------------------------ optimiser
 __global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ g, long long n, float* __restrict__ part) {
   __shared__ float red[4];
@@ -414,6 +455,15 @@ SVAE_EXPORT int svae_gelu_bwd(const float* dx, const void* gp, void* out, int64_
 SVAE_EXPORT int svae_cast_bf16(const float* in, void* out, int64_t n, svae_stream_t stream) {
   if (!in || !out || n <= 0) return SVAE_EINVAL;
   hipLaunchKernelGGL(cast_kernel, dim3(grid_for(n, 1024)), dim3(256), 0, (hipStream_t)stream, in, (bf16*)out, n);
+  SVAE_LAUNCH_CHECK();
+  return SVAE_OK;
+}
+
+SVAE_EXPORT int svae_transpose_blocks(const void* src, void* dst, const int64_t* table, int32_t nblocks,
+                                      int32_t total_tiles, svae_stream_t stream) {
+  if (!src || !dst || !table || nblocks <= 0 || total_tiles <= 0) return SVAE_EINVAL;
+  hipLaunchKernelGGL(transpose_blocks_kernel, dim3(total_tiles), dim3(256), 0, (hipStream_t)stream, (const bf16*)src,
+                     (bf16*)dst, (const long long*)table, nblocks);
   SVAE_LAUNCH_CHECK();
   return SVAE_OK;
 }

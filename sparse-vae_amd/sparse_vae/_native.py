@@ -10,7 +10,7 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, 'libsvae.so')
+LIB_PATH = os.environ.get('SVAE_LIB') or os.path.join(_HERE, 'libsvae.so')   # SVAE_LIB: A/B builds
 
 c_void_p, c_int32, c_int64, c_float, c_uint64 = (ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64,
                                                   ctypes.c_float, ctypes.c_uint64)
@@ -68,6 +68,7 @@ _SIGS = {
     'svae_attn_fwd': [ctypes.POINTER(AttnDesc), c_void_p],
     'svae_attn_bwd': [ctypes.POINTER(AttnDesc), c_void_p],
     'svae_attn_dq_part_elems': [c_int32, c_int32, c_int32, c_int32, c_int32],
+    'svae_transpose_blocks': [c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p],
     'svae_dq_finalize': [c_void_p, c_void_p, c_int64, c_int32, c_int32, c_void_p, c_int32, c_void_p],
     'svae_embedding_fwd': [c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p],
     'svae_embedding_bwd': [c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p],

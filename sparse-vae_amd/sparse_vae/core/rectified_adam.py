@@ -70,6 +70,7 @@ class RAdam(Optimizer):
         part = self.model._norm_partials(fresh=False)
         K.radam(flat.master, flat.shadow, flat.grad, self.exp_avg, self.exp_avg_sq, n, part, self._scal_dev,
                 self.norm_out)
+        flat.refresh_transposed()                    # dX GEMMs read W^T copies of the shadow
         flat.shadow_version = flat.master._version   # the kernel kept the bf16 shadow in sync
         self.model._norm_valid = False
         group['step'] += 1

@@ -20,7 +20,7 @@ import torch
 
 from . import kernels as K
 from ._native import EPI_BF16, EPI_F32, EPI_F32_ACC, EPI_GELU, EPI_GELU_BWD, EPI_DROPOUT_RESID, \
-    EPI_ROTARY_BF16, EPI_CE_STATS
+    EPI_ROTARY_BF16, EPI_CE_STATS, EPI_F32_ATOMIC
 
 bf16, f32 = torch.bfloat16, torch.float32
 ALIGN = 64
@@ -99,6 +99,10 @@ class FlatParams:
         self.device = torch.device(device)
         self.master = torch.zeros(self.total, dtype=f32, device=self.device)
         self.shadow = torch.zeros(self.total, dtype=bf16, device=self.device) if self.device.type == 'cuda' else None
+        # transposed bf16 copies of the weight blocks the dX GEMMs read (K-contiguous B operand), same offsets
+        self.shadow_t = torch.zeros_like(self.shadow) if self.shadow is not None else None
+        self.t_blocks = OrderedDict()          # (name, rows, cols) -> (offset, rows, cols)
+        self._t_table = None
         self.grad = torch.zeros(self.total, dtype=f32, device=self.device)
         self.shadow_version = -1
 
@@ -120,11 +124,44 @@ class FlatParams:
     def g(self, name):
         return self.view(name, self.grad)
 
+    def wT(self, name, rows, cols):
+        """bf16 W^T [cols][rows] of the rows x cols weight block starting at `name` (e.g. a fused q|k|v
+        block), kept in sync with the shadow; the dX GEMM's K-contiguous B operand."""
+        key = (name, rows, cols)
+        off = self.offsets[name][0]
+        if key not in self.t_blocks:
+            assert rows % 8 == 0 and cols % 8 == 0, key
+            for o, r, c in self.t_blocks.values():
+                assert off + rows * cols <= o or o + r * c <= off, f'overlapping transposed blocks at {name}'
+            self.t_blocks[key] = (off, rows, cols)
+            self._t_table = None
+            self.refresh_transposed([key])
+        return self.shadow_t[off:off + rows * cols].view(cols, rows)
+
+    def refresh_transposed(self, keys=None):
+        """Re-derive the transposed shadows from the shadow (after every shadow write)."""
+        if not self.t_blocks:
+            return
+        if keys is None and self._t_table is not None:
+            table, nb, tiles = self._t_table
+        else:
+            rows_tab, tiles = [], 0
+            for k in (keys if keys is not None else self.t_blocks):
+                o, r, c = self.t_blocks[k]
+                rows_tab.append([o, r, c, tiles])
+                tiles += -(-r // 64) * -(-c // 64)
+            table = torch.tensor(rows_tab, dtype=torch.int64).to(self.device)
+            nb = len(rows_tab)
+            if keys is None:
+                self._t_table = (table, nb, tiles)
+        K.transpose_blocks(self.shadow, self.shadow_t, table, nb, tiles)
+
     def sync_shadow(self, force=False):
         """Refresh the bf16 shadow if the master changed outside the fused optimiser (load_state_dict,
         initialize_weights, manual edits) — detected through the arena's shared version counter."""
         if force or self.master._version != self.shadow_version:
             K.cast_bf16(self.master, self.shadow)
+            self.refresh_transposed()
             self.shadow_version = self.master._version
 
 
@@ -310,11 +347,11 @@ class VAEEngine:
         K.dropout_bwd_cast(dout, g2, st['drop_p'], st['seed'], rows_q, d)
         self._dw(g2, st['f'], pre + 'ffn.2.weight', rows_q, d, 4 * d)
         dpre = ws.get('b.dpre', (rows_q, 4 * d))
-        K.gemm(g2, P.w(pre + 'ffn.2.weight'), dpre, rows_q, 4 * d, d, b_t=True, epi=EPI_GELU_BWD, aux=st['gprime'],
+        K.gemm(g2, P.wT(pre + 'ffn.2.weight', d, 4 * d), dpre, rows_q, 4 * d, d, epi=EPI_GELU_BWD, aux=st['gprime'],
                ldaux=4 * d)
         self._dw(dpre, st['h2'], pre + 'ffn.0.weight', rows_q, 4 * d, d, bias=pre + 'ffn.0.bias')
         dh2 = ws.get('b.dh2', (rows_q, d))
-        K.gemm(dpre, P.w(pre + 'ffn.0.weight'), dh2, rows_q, d, 4 * d, b_t=True, epi=EPI_BF16)
+        K.gemm(dpre, P.wT(pre + 'ffn.0.weight', 4 * d, d), dh2, rows_q, d, 4 * d, epi=EPI_BF16)
         dxc = ws.get('b.dxc', (rows_q, d), f32)
         gxc = ws.get('b.gxc', (rows_q, d))
         self._ln_bwd(pre + 'ffn_layer_norm', dh2, st['ln_f'], rows_q, dout, dxc, gxc)
@@ -324,7 +361,7 @@ class VAEEngine:
             rows_c = B * L
             self._dw(gxc, st['Oc'], c + 'output_linear.weight', rows_q, d, d, bias=c + 'output_linear.bias')
             dOc = ws.get('b.dO', (rows_q, d))
-            K.gemm(gxc, P.w(c + 'output_linear.weight'), dOc, rows_q, d, d, b_t=True, epi=EPI_BF16)
+            K.gemm(gxc, P.wT(c + 'output_linear.weight', d, d), dOc, rows_q, d, d, epi=EPI_BF16)
             dqc = ws.get('b.dqc', (rows_q, d))
             dkvc = ws.get('b.dkvc', (rows_c, 2 * d))
             delta = ws.get('b.delta', (B, heads, Lq), f32)
@@ -336,10 +373,10 @@ class VAEEngine:
                         so32=d, bo32=Lq * d, dq_part=self._dq_part(B, heads, Lq, L, hd))
             self._dw(dqc, st['hq'], c + 'q_linear.weight', rows_q, d, d, bias=c + 'q_linear.bias')
             dhq = ws.get('b.dhq', (rows_q, d))
-            K.gemm(dqc, P.w(c + 'q_linear.weight'), dhq, rows_q, d, d, b_t=True, epi=EPI_BF16)
+            K.gemm(dqc, P.wT(c + 'q_linear.weight', d, d), dhq, rows_q, d, d, epi=EPI_BF16)
             self._dw(dkvc, st['cx'], c + 'k_linear.weight', rows_c, 2 * d, d, bias=c + 'k_linear.bias')
             dcx = ws.get('b.dcx', (rows_c, d))
-            K.gemm(dkvc, P.w(c + 'k_linear.weight'), dcx, rows_c, d, 2 * d, b_t=True, epi=EPI_BF16)
+            K.gemm(dkvc, P.wT(c + 'k_linear.weight', 2 * d, d), dcx, rows_c, d, 2 * d, epi=EPI_BF16)
             dx1 = ws.get('b.dx1', (rows_q, d), f32)
             gx1 = ws.get('b.gx1', (rows_q, d))
             self._ln_bwd(pre + 'cross_attn_layer_norm', dhq, st['ln_cross'], rows_q, dxc, dx1, gx1)
@@ -347,7 +384,7 @@ class VAEEngine:
         # ---- self / learned-query attention (attention.py:51-105)
         self._dw(gx1, st['O'], a + 'output_linear.weight', rows_q, d, d, bias=a + 'output_linear.bias')
         dO = ws.get('b.dO', (rows_q, d))
-        K.gemm(gx1, P.w(a + 'output_linear.weight'), dO, rows_q, d, d, b_t=True, epi=EPI_BF16)
+        K.gemm(gx1, P.wT(a + 'output_linear.weight', d, d), dO, rows_q, d, d, epi=EPI_BF16)
         delta = ws.get('b.delta', (B, heads, Lq), f32)
         if st['learned']:
             kv = st['kv']
@@ -362,7 +399,7 @@ class VAEEngine:
             K.colsum(dq32, B, Lq * d, Lq * d, P.g(a + 'learned_queries').view(-1))
             self._dw(dkv, st['h'], a + 'k_linear.weight', rows_x, 2 * d, d, bias=a + 'k_linear.bias')
             dh = ws.get('b.dh', (rows_x, d))
-            K.gemm(dkv, P.w(a + 'k_linear.weight'), dh, rows_x, d, 2 * d, b_t=True, epi=EPI_BF16)
+            K.gemm(dkv, P.wT(a + 'k_linear.weight', 2 * d, d), dh, rows_x, d, 2 * d, epi=EPI_BF16)
         else:
             qkv = st['qkv']
             dqkv = ws.get('b.dqkv', (rows_x, 3 * d))
@@ -374,7 +411,7 @@ class VAEEngine:
                         bo32=Lq * d, dq_part=self._dq_part(B, heads, Lq, Sx, hd))
             self._dw(dqkv, st['h'], a + 'q_linear.weight', rows_x, 3 * d, d, bias=a + 'q_linear.bias')
             dh = ws.get('b.dh', (rows_x, d))
-            K.gemm(dqkv, P.w(a + 'q_linear.weight'), dh, rows_x, d, 3 * d, b_t=True, epi=EPI_BF16)
+            K.gemm(dqkv, P.wT(a + 'q_linear.weight', 3 * d, d), dh, rows_x, d, 3 * d, epi=EPI_BF16)
         if st['resid']:
             self._ln_bwd(pre + 'attn_layer_norm', dh, st['ln_a'], rows_x, dx1, dx_out)
             if dx_accumulate:
@@ -577,14 +614,14 @@ class VAEEngine:
         K.ce_grad(logits, V, sv['lse'], sv['chunk_w'], sv['labels'], gs[0:1], T, V, L, sv['nchunks'], sv['chunk_len'])
         self._dw(logits, sv['hh'], 'input_layer.0.weight', T, V, d, bias='output_layer.3.bias')
         dhh = ws.get('b.dhh', (T, d))
-        K.gemm(logits, P.w('input_layer.0.weight'), dhh, T, d, V, b_t=True, epi=EPI_BF16)
+        K.gemm(logits, P.wT('input_layer.0.weight', V, d), dhh, T, d, V, epi=EPI_BF16)
         dh0 = ws.get('b.dh0', (T, d), f32)
         self._ln_bwd('output_layer.2', dhh, sv['ln_h'], T, None, dh0)
         dpre0 = ws.get('b.dpre0', (T, d))
         K.gelu_bwd(dh0, sv['gp0'], dpre0, T * d)
         self._dw(dpre0, sv['xf'], 'output_layer.0.weight', T, d, d, bias='output_layer.0.bias')
         dx = ws.get('b.dx_dec', (T, d), f32)
-        K.gemm(dpre0, P.w('output_layer.0.weight'), dx, T, d, d, b_t=True, epi=EPI_F32)
+        K.gemm(dpre0, P.wT('output_layer.0.weight', d, d), dx, T, d, d, epi=EPI_F32)
         ready(P.end('output_layer.3.bias'))
 
         # ---- decoder layers, last to first
@@ -600,7 +637,9 @@ class VAEEngine:
             K.cast_bf16(dzh, dzh_bf)
             self._dw(dzh_bf, sv['z_bf'], f'z_projections.{i}.weight', B, d, Z)
             self._db(dzh, f'z_projections.{i}.bias', B, d)
-            K.gemm(dzh_bf, P.w(f'z_projections.{i}.weight'), dz, B, Z, d, b_t=True, epi=EPI_F32_ACC)
+            # dz += dzh . W_i: a 64 x 64 output over K = d -> split K over blocks (f32 atomics into dz)
+            K.gemm(dzh_bf, P.w(f'z_projections.{i}.weight'), dz, B, Z, d, b_t=True, epi=EPI_F32_ATOMIC,
+                   splits=max(1, min(8, d // 64)))
             ready(P.end(f'z_projections.{i}.bias'))
             dx, dx_prev = dx_prev, dx
         dx_emb = dx                                   # decoder part of d x_emb (rows 0 already zero)

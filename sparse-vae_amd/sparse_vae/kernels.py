@@ -195,6 +195,11 @@ def cast_bf16(x, out, n=None):
           'svae_cast_bf16')
 
 
+def transpose_blocks(src, dst, table, nblocks, total_tiles):
+    check(lib.svae_transpose_blocks(src.data_ptr(), dst.data_ptr(), table.data_ptr(), nblocks, total_tiles, stream()),
+          'svae_transpose_blocks')
+
+
 def gelu_bwd(dx, gp, out, n):
     check(lib.svae_gelu_bwd(dx.data_ptr(), gp.data_ptr(), out.data_ptr(), n, stream()), 'svae_gelu_bwd')
 

@@ -371,3 +371,18 @@ def test_radam_kernel_matches_oracle():
         assert abs(norm.item() - total.item()) / total.item() < 1e-5
         assert _rel(p, ref['p'].to(dev)) < 1e-6
     assert torch.equal(pbf, p.bfloat16())
+
+
+def test_transpose_blocks_exact():
+    g = torch.Generator(device=dev).manual_seed(3)
+    src = torch.randn(200000, device=dev, generator=g).bfloat16()
+    dst = torch.zeros_like(src)
+    blocks = [(0, 192, 64), (20000, 1536, 72), (150000, 40, 1000)]   # (offset, rows, cols)
+    tab, tiles = [], 0
+    for o, r, c in blocks:
+        tab.append([o, r, c, tiles])
+        tiles += -(-r // 64) * -(-c // 64)
+    K.transpose_blocks(src, dst, torch.tensor(tab, dtype=torch.int64, device=dev), len(blocks), tiles)
+    torch.cuda.synchronize()
+    for o, r, c in blocks:
+        assert torch.equal(dst[o:o + r * c].view(c, r), src[o:o + r * c].view(r, c).t())
