@@ -173,24 +173,37 @@ __global__ __launch_bounds__(256) void ce_grad_kernel(bf16* __restrict__ logits,
   const float g = gscale[0];
   float db[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if (c0 < V) {
-    for (int row = r0; row < r1; ++row) {
-      bf16x8* ptr = (bf16x8*)(logits + (long long)row * ld + c0);
-      const int lab = labels[row];
-      if (lab == 0) { *ptr = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0}; continue; }
-      const int ch = min((row % seq) / chunk_len, nchunks - 1);
-      const float w = g * chunk_w[ch];
-      const float l = lse[row];
-      const bf16x8 v = *ptr;
-      bf16x8 o;
+    // 4 rows per iteration with all loads issued before any store (the stores would otherwise order the next
+    // row's load behind them: one HBM round trip per row)
+    for (int row = r0; row < r1; row += 4) {
+      bf16x8 v[4];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        float pr = __expf((float)v[e] - l);
-        if (c0 + e == lab) pr -= 1.0f;
-        const float d = w * pr;
-        db[e] += d;
-        o[e] = f2bf(d);
+      for (int u = 0; u < 4; ++u)
+        if (row + u < r1) v[u] = *(const bf16x8*)(logits + (long long)(row + u) * ld + c0);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int rr = row + u;
+        if (rr >= r1) break;
+        bf16x8* ptr = (bf16x8*)(logits + (long long)rr * ld + c0);
+        const int lab = labels[rr];
+        bf16x8 o;
+        if (lab == 0) {
+          o = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
+        } else {
+          const int ch = min((rr % seq) / chunk_len, nchunks - 1);
+          const float w = g * chunk_w[ch];
+          const float l = lse[rr];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            float pr = __expf((float)v[u][e] - l);
+            if (c0 + e == lab) pr -= 1.0f;
+            const float d = w * pr;
+            db[e] += d;
+            o[e] = f2bf(d);
+          }
+        }
+        *ptr = o;
       }
-      *ptr = o;
     }
     if (dbias) {
 #pragma unroll
@@ -348,17 +361,21 @@ __global__ __launch_bounds__(256) void radam_kernel(float* __restrict__ p, bf16*
   const float lr = scal[0], bcm = scal[1], bcv = scal[2], rho_ok = scal[3], b1 = scal[4], b2 = scal[5], eps = scal[6],
               wd = scal[7];
   const float step = lr / bcm, decay = 1.0f - lr * wd;
-  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
-    const float gi = g[i] * coef;
-    const float mi = m[i] * b1 + (1.0f - b1) * gi;
-    const float vi = v[i] * b2 + (1.0f - b2) * gi * gi;
-    m[i] = mi;
-    v[i] = vi;
-    float pi = p[i] * decay;
-    if (rho_ok != 0.f) pi -= step * (mi / (sqrtf(vi) / bcv + eps));
-    else pi -= step * mi;
-    p[i] = pi;
-    if (pbf) pbf[i] = f2bf(pi);
+  const long long n4 = n / 4;   // n % 4 == 0 (checked on the host): 16-B vectors
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
+    const f32x4 gi = ((const f32x4*)g)[i] * coef;
+    const f32x4 mi = ((const f32x4*)m)[i] * b1 + (1.0f - b1) * gi;
+    const f32x4 vi = ((const f32x4*)v)[i] * b2 + (1.0f - b2) * gi * gi;
+    ((f32x4*)m)[i] = mi;
+    ((f32x4*)v)[i] = vi;
+    f32x4 pi = ((const f32x4*)p)[i] * decay;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      if (rho_ok != 0.f) pi[e] -= step * (mi[e] / (sqrtf(vi[e]) / bcv + eps));
+      else pi[e] -= step * mi[e];
+    }
+    ((f32x4*)p)[i] = pi;
+    if (pbf) ((bf16x4*)pbf)[i] = (bf16x4){f2bf(pi[0]), f2bf(pi[1]), f2bf(pi[2]), f2bf(pi[3])};
   }
 }
 
@@ -497,8 +514,9 @@ SVAE_EXPORT int svae_sumsq(const float* g, int64_t n, float* part, int32_t nblk,
 
 SVAE_EXPORT int svae_radam(float* p, void* pbf, const float* g, float* m, float* v, int64_t n, const float* part,
                            int32_t nblk, const float* scal, float* norm_out, svae_stream_t stream) {
-  if (!p || !g || !m || !v || !part || !scal || n <= 0 || nblk <= 0) return SVAE_EINVAL;
-  hipLaunchKernelGGL(radam_kernel, dim3(grid_for(n, 256, 2048)), dim3(256), 0, (hipStream_t)stream, p, (bf16*)pbf, g, m,
+  if (!p || !g || !m || !v || !part || !scal || n <= 0 || n % 4 || nblk <= 0) return SVAE_EINVAL;
+  if (((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15 || ((uintptr_t)pbf & 7)) return SVAE_EINVAL;
+  hipLaunchKernelGGL(radam_kernel, dim3(grid_for(n / 4, 256, 2048)), dim3(256), 0, (hipStream_t)stream, p, (bf16*)pbf, g, m,
                      v, n, part, nblk, scal, norm_out);
   SVAE_LAUNCH_CHECK();
   return SVAE_OK;

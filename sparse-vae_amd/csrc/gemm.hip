@@ -35,7 +35,6 @@ struct GP {
   int epi;
   int tn2, tm2;      // 256-tile counts (gemm256)
   long long slab;    // split-K slab mode: split s writes its partial tile at C + s * slab (0 = off)
-  int dbg;           // timing experiments only (SVAE_GEMM_DBG): 1 = no DMA after the first K-tile
 };
 
 // byte offset of (row, 16-B chunk c) in a K-contiguous [128][64] bf16 tile (128-B rows)
@@ -170,29 +169,30 @@ __device__ __forceinline__ void epilogue_half(const GP& p, const float* cs, int 
     if (full) b1 = *(const f32x4*)(p.bias + n + 4);
   }
   if constexpr (EPI == SVAE_EPI_CE_STATS) {
-    // (a) bf16 logits
-#pragma unroll
-    for (int it = 0; it < 4; ++it) {
-      const int row = (tid >> 4) + 16 * it, m = m0 + rbase + row;
-      if (m >= p.M || !ncol) continue;
-      const f32x4 x0 = *(const f32x4*)(cs + row * 128 + cs_swz(row, cc)) + b0;
-      const f32x4 x1 = *(const f32x4*)(cs + row * 128 + cs_swz(row, cc + 4)) + b1;
-      store_bf16((bf16*)p.C + cofs + (long long)m * p.ldc + n, x0, x1, full);
-    }
-    // (b) per row: 4 threads x 32 columns -> (max, sumexp), label logit
+    // one pass: thread = (row, quarter qd); its 32 columns are 32u + 8qd + (0..7), u < 4, so each of the 4
+    // bf16 stores of a row covers 64 contiguous bytes across the row's 4 lanes. Per row: (max, sumexp) over
+    // the tile's 128 columns and the label logit.
     const int row = tid >> 2, qd = tid & 3, m = m0 + rbase + row;
     float v[32];
     float mx = -INFINITY;
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int c = qd * 32 + 4 * u;
-      f32x4 x = *(const f32x4*)(cs + row * 128 + cs_swz(row, c));
-      if (p.bias) x += (n0 + c < p.N) ? *(const f32x4*)(p.bias + n0 + c) : zero;
+    for (int u = 0; u < 4; ++u) {
+      const int c = 32 * u + 8 * qd;
+      f32x4 x0 = *(const f32x4*)(cs + row * 128 + cs_swz(row, c));
+      f32x4 x1 = *(const f32x4*)(cs + row * 128 + cs_swz(row, c + 4));
+      if (p.bias) {
+        x0 += (n0 + c < p.N) ? *(const f32x4*)(p.bias + n0 + c) : zero;
+        x1 += (n0 + c + 4 < p.N) ? *(const f32x4*)(p.bias + n0 + c + 4) : zero;
+      }
+      if (m < p.M && n0 + c < p.N)
+        store_bf16((bf16*)p.C + cofs + (long long)m * p.ldc + n0 + c, x0, x1, n0 + c + 8 <= p.N);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const float y = (n0 + c + e < p.N) ? x[e] : -INFINITY;
-        v[4 * u + e] = y;
-        mx = fmaxf(mx, y);
+        const float y0 = (n0 + c + e < p.N) ? x0[e] : -INFINITY;
+        const float y1 = (n0 + c + 4 + e < p.N) ? x1[e] : -INFINITY;
+        v[8 * u + e] = y0;
+        v[8 * u + 4 + e] = y1;
+        mx = fmaxf(mx, fmaxf(y0, y1));
       }
     }
     mx = fmaxf(mx, __shfl_xor(mx, 1, 64));
@@ -203,11 +203,12 @@ __device__ __forceinline__ void epilogue_half(const GP& p, const float* cs, int 
     se += __shfl_xor(se, 1, 64);
     se += __shfl_xor(se, 2, 64);
     if (m < p.M) {
-      const int lc = p.labels[m] - n0 - qd * 32;
-      if (lc >= 0 && lc < 32) {
+      const int lc = p.labels[m] - n0;   // label column within the tile
+      if (lc >= 0 && lc < 128 && ((lc >> 3) & 3) == qd) {
+        const int idx = 8 * (lc >> 5) + (lc & 7);
 #pragma unroll
         for (int e = 0; e < 32; ++e)
-          if (e == lc) p.label_logit[m] = v[e];
+          if (e == idx) p.label_logit[m] = v[e];
       }
       if (qd == 0) {
         float* part = (float*)p.aux + ((long long)m * p.tiles_n + bn) * 2;
@@ -673,176 +674,6 @@ __device__ __forceinline__ void g3_epilogue(const GP& p, char* smem, const f32x4
   }
 }
 
-// ---------------------------------------------------------------------------------------------------
-// gemm256r: the same 256x256 / 8-wave block with a deeper pipeline: BK = 32 K-steps in an NST-slot LDS-DMA
-// ring (32 KiB per slot), NST-1 steps in flight, a counted vmcnt + raw barrier per step. Tile images:
-// K-contiguous [256][32] (64-B rows, kc2_off swizzle); MN-contiguous two [32][128] halves (mn_off).
-constexpr int R_T = 256 * 32 * 2;       // 16 KiB per operand step
-constexpr int R_STAGE = 2 * R_T;
-
-struct RSrc {
-  int off[2];
-  int kq[2];
-};
-__device__ __forceinline__ RSrc r_src_k(long long ld, int row0, int nrows, int wave, int lane) {
-  RSrc s;
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {      // 16 pieces of 16 rows x 64 B; wave w: pieces 2w, 2w+1
-    const int piece = wave * 2 + i;
-    const int r = piece * 16 + (lane >> 2), c = (lane & 3) ^ ((r >> 1) & 3);
-    s.off[i] = (row0 + r < nrows) ? (r * (int)ld + c * 8) * 2 : 0x7FFFFFF0;
-    s.kq[i] = c * 8;
-  }
-  return s;
-}
-__device__ __forceinline__ RSrc r_src_mn(long long ld, int col0, int ncols, int wave, int lane) {
-  RSrc s;
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {      // two [32][128] halves of 8 pieces (4 k-rows x 256 B)
-    const int piece = wave * 2 + i, half = piece >> 3;
-    const int kr = (piece & 7) * 4 + (lane >> 4);
-    const int sk = (kr & 3) | (((kr >> 3) & 1) << 2);
-    const int col = half * 128 + (((lane & 15) ^ (sk << 1)) * 8);
-    s.off[i] = (col0 + col < ncols) ? (kr * (int)ld + col) * 2 : 0x7FFFFFF0;
-    s.kq[i] = kr;
-  }
-  return s;
-}
-__device__ __forceinline__ void r_issue_one(const bf16* tile_base, const RSrc& src, int krem, char* dst, int wave) {
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)tile_base, 0, 0x7FFFFFF0, 0x00020000);
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int off = (krem >= 32 || src.kq[i] < krem) ? src.off[i] : 0x7FFFFFF0;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(dst + (wave * 2 + i) * 1024),
-                                             16, off, 0, 0, 0);
-  }
-}
-template <bool AT, bool BT>
-__device__ __forceinline__ void r_issue(const GP& p, const bf16* A, const bf16* B, const RSrc& sa, const RSrc& sb,
-                                        int m0, int n0, int k0, int kend, char* stage, int wave) {
-  const int krem = kend - k0;
-  if constexpr (AT) r_issue_one(A + (long long)k0 * p.lda + m0, sa, krem, stage, wave);
-  else r_issue_one(A + (long long)m0 * p.lda + k0, sa, krem, stage, wave);
-  if constexpr (BT) r_issue_one(B + (long long)k0 * p.ldb + n0, sb, krem, stage + R_T, wave);
-  else r_issue_one(B + (long long)n0 * p.ldb + k0, sb, krem, stage + R_T, wave);
-}
-template <bool TR>
-__device__ __forceinline__ bf16x8 r_frag(const char* l, int rb, int lane) {
-  if constexpr (!TR) return *(const bf16x8*)(l + kc2_off(rb + (lane & 15), lane >> 4));
-  else return read_frag2<true>(l + (rb >> 7) * (R_T / 2), rb & 127, lane);
-}
-// wait until at most n of this wave's DMA pieces are outstanding (n = 4 per step still in flight)
-__device__ __forceinline__ void r_wait(int n) {
-  switch (n) {
-    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-  }
-}
-
-template <bool AT, bool BT, int EPI, int NST>
-__global__ __launch_bounds__(512, 1) void gemm256r_kernel(GP p) {
-  __shared__ __attribute__((aligned(16))) char smem[NST * R_STAGE];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wave >> 2, wc = wave & 3;
-  const int nwg = gridDim.x;
-  int bid = blockIdx.x;
-  if (nwg >= 16) {
-    const int q = nwg / 8, r = nwg % 8, xcd = bid % 8, idx = bid / 8;
-    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
-  }
-  const int tiles = p.tn2 * p.tm2;
-  const int z = bid / tiles, t = bid - z * tiles;
-  const int batch = z / p.splits, split = z - batch * p.splits;
-  const int bn = t % p.tn2, bm = t / p.tn2;
-  const int m0 = bm * 256, n0 = bn * 256;
-  const int kbeg = split * p.kchunk;
-  const int kend = min(p.K, kbeg + p.kchunk);
-  const bf16* A = p.A + batch * p.sA;
-  const bf16* B = p.B + batch * p.sB;
-  float rsum[4] = {0.f, 0.f, 0.f, 0.f};
-
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
-  const int nk = kend > kbeg ? (kend - kbeg + 31) / 32 : 0;
-  RSrc sa, sb;
-  if constexpr (AT) sa = r_src_mn(p.lda, m0, p.M, wave, lane);
-  else sa = r_src_k(p.lda, m0, p.M, wave, lane);
-  if constexpr (BT) sb = r_src_mn(p.ldb, n0, p.N, wave, lane);
-  else sb = r_src_k(p.ldb, n0, p.N, wave, lane);
-#pragma unroll
-  for (int s = 0; s < NST - 1; ++s)
-    if (s < nk) r_issue<AT, BT>(p, A, B, sa, sb, m0, n0, kbeg + s * 32, kend, smem + s * R_STAGE, wave);
-  int slot = 0;
-  for (int kt = 0; kt < nk; ++kt) {
-    r_wait(4 * min(NST - 2, nk - 1 - kt));   // step kt landed (this wave's pieces)
-    __builtin_amdgcn_s_barrier();            // everyone's; the slot of step kt-1 is free
-    if (kt + NST - 1 < nk) {
-      int sl = slot + NST - 1;
-      if (sl >= NST) sl -= NST;
-      r_issue<AT, BT>(p, A, B, sa, sb, m0, n0, kbeg + (kt + NST - 1) * 32, kend, smem + sl * R_STAGE, wave);
-    }
-    const char* la = smem + slot * R_STAGE;
-    const char* lb = la + R_T;
-    bf16x8 a0[4], a1[4], b0[2], b1[2];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) a0[i] = r_frag<AT>(la, wr * 128 + i * 16, lane);
-#pragma unroll
-    for (int j = 0; j < 2; ++j) b0[j] = r_frag<BT>(lb, wc * 64 + j * 16, lane);
-#pragma unroll
-    for (int j = 0; j < 2; ++j) b1[j] = r_frag<BT>(lb, wc * 64 + 32 + j * 16, lane);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) a1[i] = r_frag<AT>(la, wr * 128 + 64 + i * 16, lane);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) acc[i][j] = mfma16(a0[i], b0[j], acc[i][j]);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) acc[i][2 + j] = mfma16(a0[i], b1[j], acc[i][2 + j]);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) acc[4 + i][2 + j] = mfma16(a1[i], b1[j], acc[4 + i][2 + j]);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) acc[4 + i][j] = mfma16(a1[i], b0[j], acc[4 + i][j]);
-    if constexpr (AT) {
-      if (p.a_rowsum && bn == 0) {   // sum_k A[k][m]: thread = 4 m (one 8-B unit) x 4 k-rows
-        const int u = tid & 63, kg = tid >> 6;
-        const char* lh = la + (u >> 5) * (R_T / 2);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const bf16x4 v = __builtin_bit_cast(bf16x4, *(const short4v*)(lh + mn_off(kg * 4 + r, u & 31)));
-#pragma unroll
-          for (int e = 0; e < 4; ++e) rsum[e] += (float)v[e];
-        }
-      }
-    }
-    slot = slot + 1 == NST ? 0 : slot + 1;
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if constexpr (AT) {
-    if (p.a_rowsum && bn == 0) {
-      const int m = m0 + (tid & 63) * 4;
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        if (m + e < p.M) atomicAdd(p.a_rowsum + m + e, rsum[e]);
-    }
-  }
-  g3_epilogue<EPI>(p, smem, acc, m0, n0, bn, batch, split, wr, wc, tid, lane);
-}
-
 template <bool AT, bool BT, int EPI>
 __global__ __launch_bounds__(512, 1) void gemm256_kernel(GP p) {
   __shared__ __attribute__((aligned(16))) char smem[2 * G3_STAGE];
@@ -885,7 +716,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GP p) {
     __builtin_amdgcn_s_barrier();                      // everyone's pieces landed; tile kt-1 fully consumed
     const char* la = smem + (kt & 1) * G3_STAGE;
     const char* lb = la + G3_T;
-    if (kt + 1 < nk && !(p.dbg & 1))
+    if (kt + 1 < nk)
       g3_issue<AT, BT>(p, A, B, sa, sb, m0, n0, kbeg + (kt + 1) * 64, kend, smem + ((kt + 1) & 1) * G3_STAGE, wave);
     // Quadrant walk (mh, nh) = (0,0) (0,1) (1,1) (1,0): A fragments of a half reused by two quadrants, B
     // fragments of a half by the turn. The next quadrant's fragment reads are issued ahead of the current
@@ -1038,8 +869,6 @@ SVAE_EXPORT int svae_gemm(const svae_gemm_desc* d, svae_stream_t stream) {
   p.a_rowsum = d->a_rowsum;
   p.epi = d->epi;
   p.slab = 0;
-  static const int dbg = [] { const char* e = getenv("SVAE_GEMM_DBG"); return e ? atoi(e) : 0; }();
-  p.dbg = dbg;
   // split-K slab mode (F32_ATOMIC with aux): every split stores its partial tile with plain stores into
   // aux[split][M][N], then slab_reduce adds the splits into C (no float atomics on C).
   const bool slab = d->epi == SVAE_EPI_F32_ATOMIC && d->splits > 1 && d->aux;
@@ -1065,34 +894,7 @@ SVAE_EXPORT int svae_gemm(const svae_gemm_desc* d, svae_stream_t stream) {
   const long long blocks256 = (long long)p.tn2 * p.tm2 * d->batch * d->splits;
   const bool ok3 = !(d->a_t && !d->b_t);
   int impl = forced ? forced : ((ok3 && blocks256 >= 192) ? 3 : ((kslice <= 2048 && !(d->a_t && d->b_t)) ? 2 : 1));
-  if ((impl == 3 || impl == 4) && !ok3) impl = 1;
-  if (impl == 3 && (dbg & 2)) impl = 4;
-  if (impl == 4) {
-    int kc4 = (d->K + d->splits - 1) / d->splits;
-    p.kchunk = (kc4 + 31) / 32 * 32;
-    dim3 grid4((unsigned)blocks256);
-#define SVAE_GEMM4_CASE(E)                                                                                   \
-  case E:                                                                                                    \
-    if (d->a_t) hipLaunchKernelGGL((gemm256r_kernel<true, true, E, 4>), grid4, dim3(512), 0, s, p);          \
-    else if (d->b_t) hipLaunchKernelGGL((gemm256r_kernel<false, true, E, 4>), grid4, dim3(512), 0, s, p);    \
-    else hipLaunchKernelGGL((gemm256r_kernel<false, false, E, 4>), grid4, dim3(512), 0, s, p);               \
-    break;
-    switch (epi_run) {
-      SVAE_GEMM4_CASE(SVAE_EPI_F32_ATOMIC)
-      SVAE_GEMM4_CASE(SVAE_EPI_BF16)
-      SVAE_GEMM4_CASE(SVAE_EPI_F32)
-      SVAE_GEMM4_CASE(SVAE_EPI_F32_ACC)
-      SVAE_GEMM4_CASE(SVAE_EPI_GELU)
-      SVAE_GEMM4_CASE(SVAE_EPI_GELU_BWD)
-      SVAE_GEMM4_CASE(SVAE_EPI_DROPOUT_RESID)
-      SVAE_GEMM4_CASE(SVAE_EPI_ROTARY_BF16)
-      SVAE_GEMM4_CASE(SVAE_EPI_CE_STATS)
-      default: return SVAE_EINVAL;
-    }
-#undef SVAE_GEMM4_CASE
-    SVAE_LAUNCH_CHECK();
-    return slab ? launch_slab_reduce(d, s) : SVAE_OK;
-  }
+  if (impl == 3 && !ok3) impl = 1;
   if (impl == 3) {
     int kc3 = (d->K + d->splits - 1) / d->splits;
     p.kchunk = (kc3 + 63) / 64 * 64;

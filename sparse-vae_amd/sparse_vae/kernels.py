@@ -54,14 +54,15 @@ def gemm(A, B, C, M, N_, K, *, a_t=False, b_t=False, lda=None, ldb=None, ldc=Non
 
 
 def auto_splits(M, N_, K, target=512):
-    """Split-K count for a dW GEMM. First choice: >= 192 blocks of the 256x256 kernel (the library picks it
-    at that size) with K-slices of >= 2048; otherwise ~`target` blocks of the 128x128 kernels."""
+    """Split-K count for a dW GEMM. First choice: one round of 192..256 blocks of the 256x256 kernel (the
+    library picks it at >= 192 blocks); otherwise ~`target` blocks of the 128x128 kernels."""
     t256 = -(-M // 256) * -(-N_ // 256)
     if t256 >= 192:
         return 1
-    s3 = -(-192 // t256)
-    if K // s3 >= 2048:
-        return s3
+    if t256 >= 8:   # fill the 256 CUs with one round of 256x256 blocks (1 per CU), K-slices >= 1024
+        s3 = min(256 // t256, max(1, K // 1024))
+        if t256 * s3 >= 192:
+            return s3
     tiles = -(-M // 128) * -(-N_ // 128)
     if tiles >= 256 or K < 1024:
         return 1
