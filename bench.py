@@ -35,6 +35,8 @@ CONFIGS = {
     'c2': dict(layers=6, d=512, heads=8, L=512, B=64),
     'c4': dict(layers=12, d=768, heads=8, L=1024, B=64),
     'c5': dict(layers=12, d=768, heads=8, L=2048, B=32),
+    # the C2 model with the reference's default decoder attention (sparse_self_attention, attn_window_size 4)
+    'c2s': dict(layers=6, d=512, heads=8, L=512, B=64, window=4),
 }
 V, NLAT = 32768, 64
 PEAK_BF16_TFLOPS = 2500.0      # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, chip-level parameters)
@@ -52,7 +54,8 @@ def flops_per_token(nl, d, L, V=V, N=NLAT):
 def build(cfg, device):
     from sparse_vae import TransformerVAE, TransformerVAEHparams, TextDataModule
     hp = TransformerVAEHparams(d_model=cfg['d'], num_layers=cfg['layers'], num_heads=cfg['heads'], latent_depth=64,
-                               sparse_self_attention=False, grad_clip_threshold=150.0, init_scale=0.02,
+                               sparse_self_attention=bool(cfg.get('window')), attn_window_size=cfg.get('window', 4),
+                               grad_clip_threshold=150.0, init_scale=0.02,
                                kl_weight_start=0.3, kl_weight_end=1.0, kl_annealing_steps=8000, lr=3e-4)
     model = TransformerVAE(hp, device=device)
     model.initialize_weights()
@@ -208,7 +211,10 @@ def main():
             'warmup': args.warmup, 'ms_per_step': round(ms, 3), 'higher_is_better': True, 'scaling': 'weak',
             'vs_baseline': None, 'dtype': 'bf16', 'data': 'synthetic (uniform ids in [3, 32768), [CLS] first, no padding; random-init weights)',
             'config': {'workload': f'{cfg_name}: TransformerVAE {cfg["layers"]}L d{cfg["d"]} heads {cfg["heads"]} seq {cfg["L"]}, '
-                                   f'batch {cfg["B"]}/GPU, dense attention, dropout 0.1, fwd+bwd+allreduce+clip+RAdam',
+                                   f'batch {cfg["B"]}/GPU, '
+                                   + (f'sliding-window decoder attention (window {cfg["window"]} x 32)' if cfg.get('window')
+                                      else 'dense attention')
+                                   + ', dropout 0.1, fwd+bwd+allreduce+clip+RAdam',
                        'model': f'TransformerVAE-{cfg["layers"]}L-d{cfg["d"]}', 'global_batch': cfg['B'] * world,
                        'seq_len': cfg['L'], 'parallelism': f'dp{world}'},
             'model_tflops_per_gpu': round(value / world * fpt / 1e12, 1),

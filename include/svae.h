@@ -124,6 +124,10 @@ typedef struct svae_attn_desc {
   float* dq_part;
   void* dq_bf;
   int64_t ldq_bf;
+  /* > 0 (causal only): block-sparse sliding window of SparseAttention (sparse_attention.py:39-60 with
+     block_size 32, include_cls): query q sees key k <= q iff k < 32 or k / 32 >= q / 32 - (window - 1).
+     0 = dense. */
+  int32_t window;
 } svae_attn_desc;
 
 int svae_attn_fwd(const svae_attn_desc* d, svae_stream_t stream);
@@ -194,14 +198,14 @@ int svae_radam(float* p, void* pbf, const float* g, float* m, float* v, int64_t 
 /* ---- fp32 kernel mode (argmax-reconstruction parity; TransformerVAE.reconstruct in exact f32) ---------
  * svae_gemm_f32: C[M,N] = epi(A[M,K] . W[N,K]^T) on f32-input MFMA; epi in {SVAE_EPI_F32 (+bias, +resid),
  * SVAE_EPI_ROTARY_BF16 (rotary on cols < rot_cols, f32 out), SVAE_EPI_GELU (f32 out)}.
- * svae_attn_fwd_f32: dense attention forward in f32 (same strides / masks as svae_attn_desc).
+ * svae_attn_fwd_f32: attention forward in f32 (same strides / masks / window as svae_attn_desc).
  * svae_layernorm_fwd_f32: LayerNorm with f32 output. */
 int svae_gemm_f32(const float* A, const float* W, float* C, int32_t M, int32_t N, int32_t K, int64_t lda, int64_t ldw,
                   int64_t ldc, const float* bias, const float* resid, int64_t ldr, int32_t epi, const float* rot_tab,
                   int32_t rot_cols, int32_t rot_d, int32_t rot_seq, svae_stream_t stream);
 int svae_attn_fwd_f32(const float* q, const float* k, const float* v, float* o, int64_t sq, int64_t sk, int64_t sv,
                       int64_t so, int64_t bq, int64_t bk, int64_t bv, int64_t bo, const uint8_t* key_pad, int32_t B,
-                      int32_t H, int32_t Lq, int32_t Lk, int32_t hd, int32_t causal, float scale,
+                      int32_t H, int32_t Lq, int32_t Lk, int32_t hd, int32_t causal, int32_t window, float scale,
                       svae_stream_t stream);
 int svae_layernorm_fwd_f32(const float* x, const float* w, const float* b, float* y, int32_t rows, int32_t D,
                            svae_stream_t stream);

@@ -30,6 +30,7 @@ class HParams:
     kl_weight: float = 1.0
     num_latents: int = 64          # transformer_vae.py:35 (hard-coded 64)
     vocab_size: int = VOCAB_SIZE
+    attn_window: int = 0           # decoder: 0 = dense, else sparse_self_attention with attn_window_size
 
     @property
     def enc_layers(self) -> int:   # transformer_vae.py:35 -> Perceiver(num_layers // 2)

@@ -15,7 +15,7 @@ import torch
 import torch.nn.functional as F
 
 __all__ = [
-    'rotary', 'attention', 'transformer_layer', 'perceiver', 'conditional_gaussian',
+    'rotary', 'sparse_layout', 'sparse_mask', 'attention', 'transformer_layer', 'perceiver', 'conditional_gaussian',
     'sample_z', 'reconstruct', 'output_layer', 'robust_cross_entropy', 'marginal_kl',
     'training_step', 'radam_step', 'clip_grad_norm', 'cosine_decay', 'kl_anneal',
     'RAdamState',
@@ -41,16 +41,37 @@ def _linear(p, name, x, bias=True):
     return F.linear(x, p[name + '.weight'], p[name + '.bias'] if bias else None)
 
 
+def sparse_layout(num_blocks: int, window: int) -> torch.Tensor:
+    """SparseAttention.get_master_layout, sparse_attention.py:39-60, causal with include_cls: block row r
+    attends block columns r - (window - 1) .. r (left_context = window, right_context = 0) and column 0."""
+    r = torch.arange(num_blocks)
+    off = r[:, None] - r[None, :]
+    layout = (off >= 0) & (off < window)
+    layout[:, 0] = True
+    return layout
+
+
+def sparse_mask(L: int, window: int) -> torch.Tensor:
+    """[L, L] True where a key is NOT visible to a query under SparseAttention.__call__ (sparse_attention.py:
+    75-92): outside the block layout, or above the diagonal (blocksparse softmax is_causal). Absent blocks
+    never enter the softmax; the -1e7 shift below gives them exactly zero weight, so the two agree."""
+    blk = sparse_layout(L // 32, window).repeat_interleave(32, 0).repeat_interleave(32, 1)
+    return ~blk | torch.ones(L, L, dtype=torch.bool).triu(1)
+
+
 def attention(p: Dict[str, torch.Tensor], pre: str, q_in, k_in, v_in, pad: Optional[torch.Tensor],
-              num_heads: int, causal: bool = False) -> torch.Tensor:
-    """Dense Attention.forward, attention.py:51-105 (sparse branch :78-81 out of scope)."""
+              num_heads: int, causal: bool = False, window: int = 0) -> torch.Tensor:
+    """Attention.forward, attention.py:51-105: the dense branch, and with window > 0 the SparseAttention
+    branch (:78-81; sparse_attention.py:75-92) restated densely with its block mask and rotary base
+    max_pos = 2 * window * block_size (:52)."""
     B = k_in.shape[0]
+    max_pos = 2 * window * 32 if window else 10000       # :52
     lq = p.get(pre + 'learned_queries')
     if lq is not None:                                   # :55-56
         q = lq.expand(B, *lq.shape[1:])
     else:                                                # :60-61
-        q = rotary(_linear(p, pre + 'q_linear', q_in))
-    k = rotary(_linear(p, pre + 'k_linear', k_in))       # :67, :70
+        q = rotary(_linear(p, pre + 'q_linear', q_in), max_pos=max_pos)
+    k = rotary(_linear(p, pre + 'k_linear', k_in), max_pos=max_pos)       # :67, :70
     v = _linear(p, pre + 'v_linear', v_in)
     mask = pad if (pad is not None and pad.shape[-1] == k.shape[-2]) else None   # :75 + getter
     d = q.shape[-1]
@@ -62,7 +83,10 @@ def attention(p: Dict[str, torch.Tensor], pre: str, q_in, k_in, v_in, pad: Optio
     q, k, v = split(q), split(k), split(v)
     scores = q @ k.transpose(-1, -2) * k.shape[-1] ** -0.5          # :83
     causal_mask = None
-    if causal:                                           # :85-87
+    if window:                                           # sparse: band + [CLS] block + causal (is_causal)
+        assert causal and q.shape[-2] % 32 == 0
+        causal_mask = sparse_mask(q.shape[-2], window)
+    elif causal:                                         # :85-87
         ql = q.shape[-2]
         causal_mask = torch.ones(ql, ql, dtype=torch.bool).triu(1)
     if mask is not None:                                 # :93
@@ -81,11 +105,11 @@ def _ln(p, name, x):
 
 
 def transformer_layer(p, pre, x, pad, num_heads, causal=False, context=None,
-                      dropout_mask: Optional[torch.Tensor] = None, dropout_p: float = 0.1):
+                      dropout_mask: Optional[torch.Tensor] = None, dropout_p: float = 0.1, window: int = 0):
     """TransformerLayer.forward, transformer_layer.py:44-61 (pre-LN). `dropout_mask`, if given,
     is the keep-mask of nn.Dropout(0.1) at :58 (None = dropout disabled)."""
     y = _ln(p, pre + 'attn_layer_norm', x)
-    y = attention(p, pre + 'attention.', y, y, y, pad, num_heads, causal)
+    y = attention(p, pre + 'attention.', y, y, y, pad, num_heads, causal, window)
     x = x + y if x.shape == y.shape else y               # :49
     if (pre + 'cross_attention.k_linear.weight') in p and context is not None:   # :51-54
         ctx = _ln(p, pre + 'context_layer_norm', context)
@@ -144,7 +168,7 @@ def reconstruct(p, x, z, pad, hp, dropout_masks=None):
         zh = _linear(p, f'z_projections.{i}', z)
         x = torch.cat([zh, x[..., 1:, :]], dim=-2)
         x = transformer_layer(p, f'decoder_layers.{i}.', x, pad, hp.num_heads, causal=True,
-                              dropout_mask=dm.get(f'decoder_layers.{i}'))
+                              dropout_mask=dm.get(f'decoder_layers.{i}'), window=getattr(hp, 'attn_window', 0))
     return output_layer(p, x)
 
 

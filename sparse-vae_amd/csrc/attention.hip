@@ -34,7 +34,18 @@ struct AP {
   const float* rot; int rot_d;
   float* o32; long long so32, bo32;
   float* dq_part; void* dq_bf; long long ldq_bf;
+  int window;        // > 0: causal sliding window of `window` 32-key blocks plus key block 0 (SparseAttention)
 };
+
+// Block-sparse sliding window of SparseAttention (sparse_attention.py:39-60, causal, block 32): query q sees
+// key k <= q iff k < 32 (the [CLS] block, layout[:, 0] = 1) or k / 32 >= q / 32 - (window - 1).
+constexpr int SBLK = 32;
+__device__ __forceinline__ int band_lo(int q, int window) {   // first in-band key of query q's 32-block
+  return window > 0 ? max(0, (q / SBLK - (window - 1)) * SBLK) : 0;
+}
+__device__ __forceinline__ bool band_hidden(int key, int q, int window) {
+  return window > 0 && key >= SBLK && key < band_lo(q, window);
+}
 
 // [64 rows][HDP] bf16 tile in LDS, 16-B chunks XOR-swizzled by (row & (chunks-1)): conflict-free for the
 // row-wise ds_read_b128 fragment reads, <= 2-way for the ds_read_b64_tr_b16 reads.
@@ -152,6 +163,10 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AP p) {
   const int kv_end = p.causal ? min(p.Lk, q0 + 128) : p.Lk;
   const int ntiles = (kv_end + 63) / 64;
   const float c = p.scale * LOG2E;
+  // key tiles visited: tile 0, then the band from the tile holding the block's first in-band key (dense: all)
+  const int kt1 = max(1, band_lo(q0, p.window) / 64);
+  const int nvisit = 1 + max(0, ntiles - kt1);
+  const int lo_w = band_lo(qw, p.window);          // this wave's 32 queries share one 32-block
 
   unsigned char rpm = 0;
   dma_rows<HDP>(K, p.sk, 0, p.Lk, p.hd, smem, w, lane);
@@ -160,21 +175,22 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AP p) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
-  for (int kt = 0; kt < ntiles; ++kt) {
-    const int buf = kt & 1;
+  for (int it = 0; it < nvisit; ++it) {
+    const int kt = it == 0 ? 0 : kt1 + it - 1;
+    const int buf = it & 1;
     const char* Ks = smem + buf * 2 * T::BYTES;
     const char* Vs = Ks + T::BYTES;
     const unsigned char* pms = pm + buf * 64;
-    const bool more = kt + 1 < ntiles;
+    const bool more = it + 1 < nvisit;
     if (more) {   // next tile straight into the other buffer (its readers finished before the last barrier)
-      const int kn = (kt + 1) * 64;
+      const int kn = (it == 0 ? kt1 : kt + 1) * 64;
       char* nb = smem + (buf ^ 1) * 2 * T::BYTES;
       dma_rows<HDP>(K, p.sk, kn, p.Lk, p.hd, nb, w, lane);
       dma_rows<HDP>(V, p.sv, kn, p.Lk, p.hd, nb + T::BYTES, w, lane);
       if (tid < 64) rpm = (pad && kn + tid < p.Lk) ? pad[kn + tid] : 0;
     }
     const int kbase = kt * 64;
-    if (!p.causal || kbase <= qw + 31) {
+    if ((!p.causal || kbase <= qw + 31) && (kbase < SBLK || kbase + 63 >= lo_w)) {
       // S^T = K . Q^T : s[j][st][r] = score(key = kbase + 16st + 4g + r, query = qw + 16j + li)
       f32x4 s[2][4];
 #pragma unroll
@@ -189,7 +205,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AP p) {
         }
       }
       const bool pad_any = p.pad && __builtin_amdgcn_ballot_w64(pms[lane] != 0) != 0;
-      if (pad_any || kbase + 64 > p.Lk || (p.causal && kbase + 63 > qw)) {
+      if (pad_any || kbase + 64 > p.Lk || (p.causal && kbase + 63 > qw) || (kbase + 63 >= SBLK && kbase < lo_w)) {
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -197,7 +213,8 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AP p) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               const int kl = 16 * st + 4 * g + r, key = kbase + kl;
-              if (key >= p.Lk || pms[kl] || (p.causal && key > qw + 16 * j + li)) s[j][st][r] = -INFINITY;
+              if (key >= p.Lk || pms[kl] || (p.causal && key > qw + 16 * j + li) || (key >= SBLK && key < lo_w))
+                s[j][st][r] = -INFINITY;
             }
       }
 #pragma unroll
@@ -352,7 +369,11 @@ __global__ __launch_bounds__(256, HDP == 64 ? 2 : 1) void attn_bwd_kernel(AP p) 
 
   const float inv_scale = 1.0f / p.scale, c = p.scale * LOG2E;
   const int qt0 = p.causal ? k0 / 64 : 0;
-  const int nqt = (p.Lq + 63) / 64;
+  // sliding window: queries past the last in-band query of the block's last key block see none of its keys
+  // (block 0 holds the [CLS] keys, which every later query sees)
+  const int q_end = (p.window > 0 && k0 > 0) ? min(p.Lq, k0 + BWD_KEYS - SBLK + SBLK * p.window) : p.Lq;
+  const int nqt = (q_end + 63) / 64;
+  const int band_end = p.window > 0 && kw >= SBLK ? kw + SBLK * p.window : 0x7FFFFFFF;   // first query past kw's band
   float* part = p.dq_part + ((long long)kb * p.B + b) * p.Lq * p.H * p.hd + (long long)h * p.hd;
   const long long ldp = (long long)p.H * p.hd;
 
@@ -383,7 +404,7 @@ __global__ __launch_bounds__(256, HDP == 64 ? 2 : 1) void attn_bwd_kernel(AP p) 
     const float* nl = cst + buf * 128;
     const bool more = qt + 1 < nqt;
     if (more) fetch(qb + 64, buf ^ 1);
-    const bool live = !p.causal || kw <= qb + 63;   // some key of this wave is visible to some query
+    const bool live = (!p.causal || kw <= qb + 63) && qb < band_end;   // some key of this wave visible to some query
     if (live) {
       f32x4 s[2][4], dp[2][4];
       bf16x8 kf[2][NKK];
@@ -407,7 +428,7 @@ __global__ __launch_bounds__(256, HDP == 64 ? 2 : 1) void attn_bwd_kernel(AP p) 
           dp[1][t] = mfma16(oa, vf[1][kk], dp[1][t]);
         }
       }
-      const bool edge = !keys_all_ok || qb + 64 > p.Lq || (p.causal && kw + 31 > qb);
+      const bool edge = !keys_all_ok || qb + 64 > p.Lq || (p.causal && kw + 31 > qb) || qb + 63 >= band_end;
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -417,7 +438,7 @@ __global__ __launch_bounds__(256, HDP == 64 ? 2 : 1) void attn_bwd_kernel(AP p) 
             float pr = __builtin_amdgcn_exp2f(s[j][t][r] * c);
             if (edge) {
               const int q = qb + 16 * t + 4 * g + r, key = kw + 16 * j + li;
-              if (!key_ok[j] || q >= p.Lq || (p.causal && key > q)) pr = 0.f;
+              if (!key_ok[j] || q >= p.Lq || (p.causal && key > q) || q >= band_end) pr = 0.f;
             }
             s[j][t][r] = pr;
             dp[j][t][r] = pr * dp[j][t][r];
@@ -530,9 +551,13 @@ __global__ __launch_bounds__(256) void attn_dq_reduce_kernel(AP p) {
     const long long row = i / D4;                 // b * Lq + q
     const int q = (int)(row % p.Lq), b = (int)(row / p.Lq);
     const int nk = p.causal ? min(nkb, q / BWD_KEYS + 1) : nkb;
+    // sliding window: key block k >= 1 wrote partials only for the query tiles it swept (see attn_bwd_kernel)
+    int k1 = 1;
+    if (p.window > 0)
+      while (k1 < nk && q >= (min(p.Lq, k1 * BWD_KEYS + BWD_KEYS - SBLK + SBLK * p.window) + 63) / 64 * 64) ++k1;
     const float* src = p.dq_part + row * D + 4 * c4;
     f32x4 acc = *(const f32x4*)src;
-    for (int k = 1; k < nk; ++k) acc += *(const f32x4*)(src + k * plane);
+    for (int k = k1; k < nk; ++k) acc += *(const f32x4*)(src + k * plane);
     acc *= p.scale;
     if (p.dq_bf) {
       if (p.rot) {   // inverse of (a c - b s, b c + a s) on the pairs (4c4, 4c4+1), (4c4+2, 4c4+3)
@@ -566,6 +591,8 @@ bool fill(const svae_attn_desc* d, AP& p) {
   p.rot = d->rot_tab; p.rot_d = d->rot_d;
   p.o32 = d->o32; p.so32 = d->so32; p.bo32 = d->bo32;
   p.dq_part = d->dq_part; p.dq_bf = d->dq_bf; p.ldq_bf = d->ldq_bf;
+  p.window = d->window;
+  if (p.window < 0 || (p.window > 0 && !p.causal)) return false;
   if (p.o32 && ((p.so32 | p.bo32) % 4)) return false;
   return true;
 }

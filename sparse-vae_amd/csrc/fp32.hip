@@ -89,7 +89,8 @@ __global__ __launch_bounds__(256) void attn_fwd_f32_kernel(const float* __restri
                                                            long long sq, long long sk, long long sv, long long so,
                                                            long long bq, long long bk, long long bv, long long bo,
                                                            const unsigned char* __restrict__ pad, int B, int H,
-                                                           int Lq, int Lk, int hd, int causal, float scale) {
+                                                           int Lq, int Lk, int hd, int causal, int window,
+                                                           float scale) {
   extern __shared__ float sc[];   // [4 waves][Lk]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const long long gid_raw = (long long)blockIdx.x * 4 + wave;
@@ -104,7 +105,10 @@ __global__ __launch_bounds__(256) void attn_fwd_f32_kernel(const float* __restri
     float dot = 0.f;
     for (int dd = 0; dd < hd; ++dd) dot = fmaf(qp[dd], kp[dd], dot);
     float x = dot * scale;
-    const bool m = (pad && pad[(long long)b * Lk + j]) || (causal && j > qi);
+    // window > 0: keys outside SparseAttention's causal band + [CLS] block (sparse_attention.py:39-60) are
+    // absent from the reference's block-sparse softmax; the -1e7 shift gives them exactly zero weight too
+    const bool out_of_band = window > 0 && j >= 32 && j / 32 < qi / 32 - (window - 1);
+    const bool m = (pad && pad[(long long)b * Lk + j]) || (causal && j > qi) || out_of_band;
     if (m) x = x - 1e7f;          // attention.py:98 (score - mask * 1e7)
     s[j] = x;
     mx = fmaxf(mx, x);
@@ -161,12 +165,13 @@ SVAE_EXPORT int svae_gemm_f32(const float* A, const float* W, float* C, int32_t 
 SVAE_EXPORT int svae_attn_fwd_f32(const float* q, const float* k, const float* v, float* o, int64_t sq, int64_t sk,
                                   int64_t sv, int64_t so, int64_t bq, int64_t bk, int64_t bv, int64_t bo,
                                   const uint8_t* key_pad, int32_t B, int32_t H, int32_t Lq, int32_t Lk, int32_t hd,
-                                  int32_t causal, float scale, svae_stream_t stream) {
+                                  int32_t causal, int32_t window, float scale, svae_stream_t stream) {
   if (!q || !k || !v || !o || B <= 0 || H <= 0 || Lq <= 0 || Lk <= 0 || hd <= 0 || Lk > 8192) return SVAE_EINVAL;
+  if (window < 0 || (window > 0 && !causal)) return SVAE_EINVAL;
   const long long n = (long long)B * H * Lq;
   hipLaunchKernelGGL(attn_fwd_f32_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 4 * Lk * sizeof(float),
                      (hipStream_t)stream, q, k, v, o, sq, sk, sv, so, bq, bk, bv, bo, key_pad, B, H, Lq, Lk, hd, causal,
-                     scale);
+                     window, scale);
   SVAE_LAUNCH_CHECK();
   return SVAE_OK;
 }

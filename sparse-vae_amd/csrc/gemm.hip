@@ -34,6 +34,7 @@ struct GP {
   float* a_rowsum;   // optional: += sum_k A[m][k] (bias gradient fused into the dW GEMM); a_t layout only
   int epi;
   int tn2, tm2;      // 256-tile counts (gemm256)
+  int group;         // L2 grouping: consecutive tiles walk `group` tile rows (M) before the next tile column
   long long slab;    // split-K slab mode: split s writes its partial tile at C + s * slab (0 = off)
 };
 
@@ -97,6 +98,21 @@ __device__ __forceinline__ bf16x8 read_frag(const char* lds, int base, int kk, i
 // f32 staging tile [128][128] for the epilogue: 16-B unit index XOR ((row >> 2) & 3) << 2
 __device__ __forceinline__ int cs_swz(int row, int col) { return (((col >> 2) ^ (((row >> 2) & 3) << 2)) << 2) | (col & 3); }
 
+// Tile index -> (bm, bn). group <= 1: N-fastest rows of tiles. group = G: tiles run in bands of G tile rows,
+// M-fastest inside a band, so the ~32 tiles an XCD holds at once cover a G x (32/G) patch whose A and B panels
+// fit its 4 MiB L2 (instead of 32 different B panels that miss it on every tile).
+__device__ __forceinline__ void group_tile(int t, int tiles_m, int tiles_n, int group, int& bm, int& bn) {
+  if (group <= 1) {
+    bn = t % tiles_n;
+    bm = t / tiles_n;
+    return;
+  }
+  const int per = group * tiles_n, grp = t / per, first = grp * group;
+  const int gs = min(group, tiles_m - first), r = t - grp * per;
+  bm = first + r % gs;
+  bn = r / gs;
+}
+
 // Block -> (tile, batch, split). The hardware deals consecutive block ids round-robin over the 8 XCDs; the
 // bijective remap gives each XCD one contiguous range of the (batch, split)-major / N-fastest logical order,
 // so blocks that share A rows, B columns or a K-chunk run together on one L2.
@@ -109,8 +125,7 @@ __device__ __forceinline__ void tile_coords(const GP& p, int& bm, int& bn, int& 
     bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
   }
   const int z = bid / tiles, t = bid - z * tiles;
-  bn = t % p.tiles_n;
-  bm = t / p.tiles_n;
+  group_tile(t, p.tiles_m, p.tiles_n, p.group, bm, bn);
   batch = z / p.splits;
   split = z - batch * p.splits;
 }
@@ -690,7 +705,8 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GP p) {
   const int tiles = p.tn2 * p.tm2;
   const int z = bid / tiles, t = bid - z * tiles;
   const int batch = z / p.splits, split = z - batch * p.splits;
-  const int bn = t % p.tn2, bm = t / p.tn2;
+  int bm, bn;
+  group_tile(t, p.tm2, p.tn2, p.group, bm, bn);
   const int m0 = bm * 256, n0 = bn * 256;
   const int kbeg = split * p.kchunk;
   const int kend = min(p.K, kbeg + p.kchunk);
@@ -891,6 +907,8 @@ SVAE_EXPORT int svae_gemm(const svae_gemm_desc* d, svae_stream_t stream) {
   const int kslice = (d->K + d->splits - 1) / d->splits;
   p.tn2 = (d->N + 255) / 256;
   p.tm2 = (d->M + 255) / 256;
+  static const int group_env = [] { const char* e = getenv("SVAE_GEMM_GROUP"); return e ? atoi(e) : -1; }();
+  p.group = group_env >= 0 ? group_env : 0;   // measured: no gain on the C2 shapes (L2 misses were not the limit)
   const long long blocks256 = (long long)p.tn2 * p.tm2 * d->batch * d->splits;
   const bool ok3 = !(d->a_t && !d->b_t);
   int impl = forced ? forced : ((ok3 && blocks256 >= 192) ? 3 : ((kslice <= 2048 && !(d->a_t && d->b_t)) ? 2 : 1));

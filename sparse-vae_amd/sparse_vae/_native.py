@@ -54,6 +54,7 @@ class AttnDesc(ctypes.Structure):
         ('rot_tab', c_void_p), ('rot_d', c_int32),
         ('o32', c_void_p), ('so32', c_int64), ('bo32', c_int64),
         ('dq_part', c_void_p), ('dq_bf', c_void_p), ('ldq_bf', c_int64),
+        ('window', c_int32),
     ]
 
 
@@ -89,8 +90,8 @@ _SIGS = {
     'svae_gemm_f32': [c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_int32, c_int64, c_int64, c_int64, c_void_p,
                       c_void_p, c_int64, c_int32, c_void_p, c_int32, c_int32, c_int32, c_void_p],
     'svae_attn_fwd_f32': [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_int64, c_int64, c_int64,
-                          c_int64, c_int64, c_void_p, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, c_float,
-                          c_void_p],
+                          c_int64, c_int64, c_void_p, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32,
+                          c_float, c_void_p],
     'svae_layernorm_fwd_f32': [c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p],
     'svae_version': [],
 }

@@ -27,9 +27,12 @@ class Attention(nn.Module):
         self.v_linear = nn.Linear(d_model, d_model)
         self.output_linear = nn.Linear(d_model, d_model)
         self.pos_linear = nn.Linear(d_model, d_model)   # never used by the reference either (no gradient)
-        if sparse:
-            raise NotImplementedError('sparse (Triton block-sparse) self-attention is not implemented on MI355X '
-                                      'yet; use sparse_self_attention=False (the dense path)')
+        # SparseAttention(window_size=sparse if isinstance(sparse, int) else 4) (attention.py:45-48; note that
+        # True is an int there too). Causal sliding window of `window` 32-token blocks plus the [CLS] block,
+        # rotary base 2 * window * 32 (attention.py:52); run by the attention kernel's window mode.
+        self.sparse_window = (int(sparse) if isinstance(sparse, int) else 4) if sparse else 0
+        if self.sparse_window and not causal:
+            raise NotImplementedError('non-causal sparse attention (two-sided window) is not used by the reference')
 
     forward = _no_forward('Attention')
 

@@ -181,13 +181,14 @@ class Workspace:
         return t
 
 
-def rotary_table(positions, d):
+def rotary_table(positions, d, max_pos=10000):
     """cos/sin table exactly as encode_position_rotary builds it (attention.py:194-200), in fp32 on the
-    host so the factors are bitwise those of the fp32 reference; layout [pos][d/2][2]."""
+    host so the factors are bitwise those of the fp32 reference; layout [pos][d/2][2]. max_pos is 10000 for
+    dense attention and 2 * window * 32 for SparseAttention (attention.py:52)."""
     half = d // 2
     freqs = torch.arange(half, dtype=f32)
     pos = torch.arange(0, positions, dtype=f32)
-    theta = 10000 ** (-freqs / half)
+    theta = max_pos ** (-freqs / half)
     ang = pos[:, None] * theta
     return torch.stack([ang.cos(), ang.sin()], dim=-1).contiguous()
 
@@ -209,16 +210,21 @@ class VAEEngine:
         self.He = hp.d_model // 64
         assert self.d % self.H == 0 and self.d % 64 == 0
         self.hd = self.d // self.H
-        self._rot = None
+        self._rot = {}
+        self.window = getattr(hp, 'attn_window', 0)     # decoder self-attention: 0 dense, > 0 sliding window
         self.saved = None
         self.probe = None      # list -> HIP events around each vocab-head GEMM launch (bench roofline)
 
     # ------------------------------------------------------------------ helpers
-    def rot(self, L):
+    def rot(self, L, window=0):
+        """Rotary cos/sin table for positions < L; window > 0 selects SparseAttention's base 2 * window * 32."""
         need = max(L, self.hp.num_latents)
-        if self._rot is None or self._rot.shape[0] < need:
-            self._rot = rotary_table(max(need, 512), self.d).to(self.P.device)
-        return self._rot
+        base = 2 * window * 32 if window else 10000
+        t = self._rot.get(base)
+        if t is None or t.shape[0] < need:
+            t = rotary_table(max(need, 512), self.d, base).to(self.P.device)
+            self._rot[base] = t
+        return t
 
     def _ln_fwd(self, name, x, rows, tag):
         D = self.d
@@ -248,14 +254,14 @@ class VAEEngine:
 
     # ------------------------------------------------------------------ one transformer layer
     def layer_fwd(self, pre, x, B, Sx, L, pad, *, learned=0, cross=False, causal=False, ctx=None, heads, hd,
-                  drop_p=0.0, seed=0, tag, out=None):
+                  drop_p=0.0, seed=0, tag, out=None, window=0):
         """TransformerLayer.forward (transformer_layer.py:44-61) on x f32 [B*Sx, d]. Returns the f32 output
-        [B*Lq, d] and the saved state for layer_bwd."""
+        [B*Lq, d] and the saved state for layer_bwd. window > 0: sliding-window self-attention."""
         d, ws, P = self.d, self.ws, self.P
         rows_x = B * Sx
-        rot = self.rot(max(Sx, L))
+        rot = self.rot(max(Sx, L), window)
         st = {'pre': pre, 'B': B, 'Sx': Sx, 'L': L, 'learned': learned, 'cross': cross, 'causal': causal,
-              'heads': heads, 'hd': hd, 'drop_p': drop_p, 'seed': seed, 'x': x, 'tag': tag}
+              'heads': heads, 'hd': hd, 'drop_p': drop_p, 'seed': seed, 'x': x, 'tag': tag, 'window': window}
         a = pre + 'attention.'
         h, st['ln_a'] = self._ln_fwd(pre + 'attn_layer_norm', x, rows_x, tag + '.ln_a')
         st['h'] = h
@@ -283,7 +289,8 @@ class VAEEngine:
         O32 = ws.get(tag + '.O32', (rows_q, d), f32)
         lse = ws.get(tag + '.lse', (B, heads, Lq), f32)
         K.attention(q, kt, vt, O, lse, B=B, H=heads, Lq=Lq, Lk=Sx, hd=hd, so=d, bo=Lq * d, sk=sk, sv=sk,
-                    bk=Sx * sk, bv=Sx * sk, key_pad=pad_k, causal=causal, o32=O32, so32=d, bo32=Lq * d, **qargs)
+                    bk=Sx * sk, bv=Sx * sk, key_pad=pad_k, causal=causal, window=window, o32=O32, so32=d, bo32=Lq * d,
+                    **qargs)
         st.update(O=O, O32=O32, lse=lse, Lq=Lq, pad_k=pad_k)
         resid = Lq == Sx                           # transformer_layer.py:49
         x1 = ws.get(tag + '.x1', (rows_q, d), f32)
@@ -340,7 +347,7 @@ class VAEEngine:
         pre, B, Sx, L, Lq = st['pre'], st['B'], st['Sx'], st['L'], st['Lq']
         heads, hd = st['heads'], st['hd']
         rows_x, rows_q = B * Sx, st['rows_q']
-        rot = self.rot(max(Sx, L))
+        rot = self.rot(max(Sx, L), st['window'])
         a = pre + 'attention.'
         # ---- FFN (transformer_layer.py:56-61)
         g2 = ws.get('b.g2', (rows_q, d))
@@ -405,7 +412,8 @@ class VAEEngine:
             dqkv = ws.get('b.dqkv', (rows_x, 3 * d))
             K.attention(qkv, qkv[:, d:], qkv[:, 2 * d:], st['O'], st['lse'], B=B, H=heads, Lq=Lq, Lk=Sx, hd=hd,
                         sq=3 * d, bq=Sx * 3 * d, sk=3 * d, sv=3 * d, bk=Sx * 3 * d, bv=Sx * 3 * d, so=d, bo=Lq * d,
-                        key_pad=st['pad_k'], causal=st['causal'], backward=True, dout=dO, sdo=d, bdo=Lq * d,
+                        key_pad=st['pad_k'], causal=st['causal'], window=st['window'], backward=True, dout=dO,
+                        sdo=d, bdo=Lq * d,
                         delta=delta, dq_bf=dqkv, ldq_bf=3 * d, dk=dqkv[:, d:], dv=dqkv[:, 2 * d:], sdk=3 * d,
                         sdv=3 * d, bdk=Sx * 3 * d, bdv=Sx * 3 * d, rot=rot, rot_d=d, o32=st['O32'], so32=d,
                         bo32=Lq * d, dq_part=self._dq_part(B, heads, Lq, Sx, hd))
@@ -520,6 +528,9 @@ class VAEEngine:
     def _decode(self, x_emb, zb, padm, B, L, dropout, seed):
         hp, d, ws, P = self.hp, self.d, self.ws, self.P
         T, Z = B * L, hp.latent_depth
+        if self.window and L % 32:
+            raise ValueError(f'sparse decoder attention needs seq_len % 32 == 0 (SparseAttention block_size 32, '
+                             f'sparse_attention.py:81), got {L}')
         xs = ws.get('x_dec0', (T, d), f32)
         xs.copy_(x_emb)
         dec = []
@@ -528,7 +539,7 @@ class VAEEngine:
                    bias=P.f(f'z_projections.{i}.bias'))
             xs, st = self.layer_fwd(f'decoder_layers.{i}.', xs, B, L, L, padm, causal=True, heads=self.H,
                                     hd=self.hd, drop_p=dropout, seed=_mix_seed(seed, i), tag=f'd{i}',
-                                    out=ws.get(f'x_dec{i + 1}', (T, d), f32))
+                                    out=ws.get(f'x_dec{i + 1}', (T, d), f32), window=self.window)
             dec.append(st)
         return xs, dec
 
@@ -539,7 +550,7 @@ class VAEEngine:
         dev = P.device
         B, L = x_emb.shape[0], x_emb.shape[1]
         T, V, Z, H, hd = B * L, hp.vocab_size, hp.latent_depth, self.H, self.hd
-        rot = self.rot(L)
+        rot = self.rot(L, self.window)
         padm = None
         if pad is not None:
             padm = torch.empty(B, L, dtype=torch.uint8, device=dev)
@@ -559,7 +570,8 @@ class VAEEngine:
             K.gemm_f32(h, P.f(a + 'q_linear.weight'), qkv, T, 3 * d, d, epi=EPI_ROTARY_BF16, bias=P.f(a + 'q_linear.bias'),
                        rot=rot, rot_cols=2 * d, rot_d=d, rot_seq=L)
             K.attention_f32(qkv, qkv[:, d:], qkv[:, 2 * d:], o, B=B, H=H, Lq=L, Lk=L, hd=hd, sq=3 * d, sk=3 * d,
-                            sv=3 * d, so=d, bq=L * 3 * d, bk=L * 3 * d, bv=L * 3 * d, bo=L * d, key_pad=padm, causal=True)
+                            sv=3 * d, so=d, bq=L * 3 * d, bk=L * 3 * d, bv=L * 3 * d, bo=L * d, key_pad=padm, causal=True,
+                            window=self.window)
             K.gemm_f32(o, P.f(a + 'output_linear.weight'), x1, T, d, d, bias=P.f(a + 'output_linear.bias'), resid=x, ldr=d)
             K.layernorm_fwd_f32(x1, P.f(pre + 'ffn_layer_norm.weight'), P.f(pre + 'ffn_layer_norm.bias'), h, T, d)
             K.gemm_f32(h, P.f(pre + 'ffn.0.weight'), f, T, 4 * d, d, epi=EPI_GELU, bias=P.f(pre + 'ffn.0.bias'))

@@ -116,17 +116,19 @@ _attn_desc = N.AttnDesc()
 
 
 def attention(q, k, v, o, lse, *, B, H, Lq, Lk, hd, sq, sk, sv, so, bq, bk, bv, bo, key_pad=None, causal=False,
-              scale=None, backward=False, dout=None, sdo=0, bdo=0, delta=None, dq=None, bdq=0, dk=None, dv=None,
+              window=0, scale=None, backward=False, dout=None, sdo=0, bdo=0, delta=None, dq=None, bdq=0, dk=None, dv=None,
               sdk=0, sdv=0, bdk=0, bdv=0, rot=None, rot_d=0, o32=None, so32=0, bo32=0, dq_part=None, dq_bf=None,
               ldq_bf=0):
     """Forward (o, lse[, o32]) or backward (dk, dv and dq: f32 `dq` or bf16 `dq_bf` with inverse rotary).
-    dq_part: f32 workspace of attn_dq_part_elems(...) floats (allocated here when not given)."""
+    dq_part: f32 workspace of attn_dq_part_elems(...) floats (allocated here when not given).
+    window > 0 (causal): SparseAttention's sliding window of `window` 32-key blocks + the [CLS] block."""
     d = _attn_desc
     d.q, d.k, d.v, d.o = q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr()
     d.sq, d.sk, d.sv, d.so, d.bq, d.bk, d.bv, d.bo = sq, sk, sv, so, bq, bk, bv, bo
     d.key_pad = ptr(key_pad)
     d.lse = lse.data_ptr()
     d.B, d.H, d.Lq, d.Lk, d.hd, d.causal = B, H, Lq, Lk, hd, int(causal)
+    d.window = int(window)
     d.scale = hd ** -0.5 if scale is None else scale
     d.o32, d.so32, d.bo32 = ptr(o32), so32, bo32
     if backward:
@@ -227,9 +229,11 @@ def gemm_f32(A, W, C, M, N_, K_, *, lda=None, ldw=None, ldc=None, epi=N.EPI_F32,
           'svae_gemm_f32')
 
 
-def attention_f32(q, k, v, o, *, B, H, Lq, Lk, hd, sq, sk, sv, so, bq, bk, bv, bo, key_pad=None, causal=False):
+def attention_f32(q, k, v, o, *, B, H, Lq, Lk, hd, sq, sk, sv, so, bq, bk, bv, bo, key_pad=None, causal=False,
+                  window=0):
     check(lib.svae_attn_fwd_f32(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), sq, sk, sv, so, bq, bk, bv, bo,
-                                ptr(key_pad), B, H, Lq, Lk, hd, int(causal), hd ** -0.5, stream()), 'svae_attn_fwd_f32')
+                                ptr(key_pad), B, H, Lq, Lk, hd, int(causal), int(window), hd ** -0.5, stream()),
+          'svae_attn_fwd_f32')
 
 
 def layernorm_fwd_f32(x, w, b, y, rows, D):

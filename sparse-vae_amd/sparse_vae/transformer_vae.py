@@ -41,6 +41,9 @@ class _EngineHP:
         self.d_model, self.num_heads, self.num_layers = hp.d_model, hp.num_heads, hp.num_layers
         self.latent_depth, self.num_latents, self.vocab_size = hp.latent_depth, 64, VOCAB_SIZE
         self.enc_layers = hp.num_layers // 2
+        # decoder self-attention: 0 = dense, else SparseAttention's window in 32-token blocks
+        # (transformer_language_model.py:67-69 passes attn_window_size when sparse_self_attention)
+        self.attn_window = int(hp.get('attn_window_size', 4)) if hp.get('sparse_self_attention', True) else 0
 
 
 class _StepFn(torch.autograd.Function):

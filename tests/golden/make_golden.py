@@ -160,11 +160,33 @@ def op_vectors(sv):
     print('ops: written')
 
 
+def sparse_vectors(sv):
+    """The block layout of the reference's SparseAttention (sparse_attention.py:39-60) for several windows,
+    and the attention module's sparse rotary base (attention.py:52). The Triton blocksparse kernels that
+    consume the layout (GPU-only, triton 1.1) cannot run here: their softmax masking is parity-unpinned."""
+    SA = sys.modules['sparse_vae.core.sparse_attention'].SparseAttention
+    Att = sys.modules['sparse_vae.core.attention'].Attention
+    rec = {}
+    for w in (1, 2, 3, 4, 6):
+        lay = SA(window_size=w, max_seq_len=640, num_heads=2).get_master_layout()
+        rec[f'layout_w{w}'] = lay.numpy().astype(np.int8)
+    for w in (4, 2):
+        a = Att(64, 4, causal=True, sparse=w)
+        rec[f'window_of_sparse_{w}'] = np.asarray([a.sparse_attention.window_size,
+                                                   a.sparse_attention.block_size, a.sparse_attention.causal,
+                                                   a.sparse_attention.include_cls])
+    np.savez_compressed(os.path.join(HERE, 'sparse.npz'), **rec)
+    print('sparse: written')
+
+
 def main():
     torch.set_num_threads(min(8, os.cpu_count()))
     sv = ref_stubs.import_reference()
     keys = {}
     only = sys.argv[1:]
+    if only == ['sparse']:
+        sparse_vectors(sv)
+        return
     for name, cfg in CONFIGS.items():
         if only and name not in only:
             continue

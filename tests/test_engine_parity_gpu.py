@@ -63,3 +63,42 @@ def test_step_matches_oracle(name):
     print(f'[{name}] loss {loss:.6f} ref {ref["loss"].item():.6f} kl {kl:.6f} ref {ref["kl"].item():.6f}\n' + msg)
     assert worst[0][0] > 0.98, msg
     assert all(0.95 < r < 1.05 for _, r, _ in worst), msg
+
+
+@pytest.mark.parametrize('name,window', [('tiny_pad', 1), ('small6_pad', 2), ('c2shape', 4)])
+def test_sparse_step_matches_oracle(name, window):
+    """Decoder self-attention in SparseAttention's sliding-window mode (sparse_self_attention=True,
+    attn_window_size=window): full step vs the oracle's dense restatement of the block-sparse mask. The oracle's
+    layout is pinned to the reference (tests/golden/sparse.npz); the Triton kernels themselves cannot run here,
+    so the softmax semantics inside the layout are parity-unpinned."""
+    torch.set_num_threads(min(16, os.cpu_count()))
+    g, hp, params, ids = setup(name)
+    hp.attn_window = window
+    ntok = torch.from_numpy(g['lens'])
+    eps = torch.from_numpy(g['eps'])
+    kw = float(g['kl_weight'])
+    p = {k: v.clone().requires_grad_(True) for k, v in params.items()}
+    ref = oracle.training_step(p, hp, ids, ntok, eps, kl_weight=kw)
+    ref['loss'].backward()
+    dense = oracle.training_step(params, oracle.HParams(**{**hp.__dict__, 'attn_window': 0}), ids, ntok, eps,
+                                 kl_weight=kw)
+    assert abs(dense['loss'].item() - ref['loss'].item()) > 1e-6    # the window actually changes the model
+
+    flat, eng = _build(hp, params)
+    assert eng.window == window
+    out = eng.forward(ids.cuda(), ntok.cuda(), eps=eps.cuda(), dropout=0.0, kl_weight=kw)
+    flat.grad.zero_()
+    eng.backward(torch.ones((), device='cuda'), kw)
+    torch.cuda.synchronize()
+    loss = out['loss'].item()
+    assert abs(loss - ref['loss'].item()) / abs(ref['loss'].item()) < 1e-3
+    worst = []
+    for n in flat.live_names:
+        gg = flat.g(n).cpu().double().flatten()
+        gr = p[n].grad.double().flatten()
+        worst.append(((gg @ gr / (gg.norm() * gr.norm() + 1e-30)).item(), (gg.norm() / (gr.norm() + 1e-30)).item(), n))
+    worst.sort()
+    msg = '\n'.join(f'{c:.5f} {r:.4f} {n}' for c, r, n in worst[:8])
+    print(f'[{name} w{window}] loss {loss:.6f} ref {ref["loss"].item():.6f}\n' + msg)
+    assert worst[0][0] > 0.98, msg
+    assert all(0.95 < r < 1.05 for _, r, _ in worst), msg

@@ -259,6 +259,60 @@ def test_attention_fwd_bwd(B, H, Lq, Lk, hd, causal, padded, learned):
     assert _rel(dv, unheads(vr.grad)) < 2e-2
 
 
+@pytest.mark.parametrize('B,H,L,hd,window,padded', [
+    (2, 4, 512, 64, 4, True),       # the reference default (attn_window_size 4), C2 head dim
+    (1, 2, 1024, 64, 4, False),     # band far from the [CLS] block
+    (2, 2, 320, 96, 2, True),       # hd 96 (the 128-padded kernels)
+    (1, 2, 640, 64, 1, False),      # window 1: diagonal block + [CLS] block only
+    (2, 2, 256, 64, 8, False),      # window wider than the sequence: plain causal
+    (1, 3, 1184, 32, 3, True),      # ragged tail (1184 = 37 blocks of 32), small head dim
+])
+def test_attention_sliding_window_fwd_bwd(B, H, L, hd, window, padded):
+    """window mode (SparseAttention's causal band + [CLS] block) vs a dense fp32 reference with the oracle's
+    sparse mask; also the f32 kernel mode's forward."""
+    torch.manual_seed(L + window)
+    d = H * hd
+    q, k, v = (torch.randn(B, L, d, device=dev).bfloat16() for _ in range(3))
+    pad = None
+    if padded:
+        pad = torch.zeros(B, L, device=dev, dtype=torch.uint8)
+        for b in range(B):
+            pad[b, L - 1 - 37 * b - 9:] = 1
+    o = torch.empty(B, L, d, device=dev, dtype=torch.bfloat16)
+    lse = torch.empty(B, H, L, device=dev)
+    common = dict(B=B, H=H, Lq=L, Lk=L, hd=hd, sq=d, bq=L * d, sk=d, sv=d, bk=L * d, bv=L * d, so=d, bo=L * d,
+                  key_pad=pad, causal=True, window=window)
+    K.attention(q, k, v, o, lse, **common)
+
+    def heads(t):
+        return t.float().view(B, L, H, hd).transpose(1, 2)
+
+    def unheads(t):
+        return t.transpose(1, 2).reshape(B, L, d)
+
+    qr, kr, vr = (heads(t).requires_grad_() for t in (q, k, v))
+    s = qr @ kr.transpose(-1, -2) * hd ** -0.5
+    mask = oracle.sparse_mask(L, window).to(dev)[None, None]
+    if pad is not None:
+        mask = mask | pad[:, None, None, :].bool()
+    ref_o = unheads((s - mask * 1e7).softmax(-1) @ vr)
+    assert _rel(o, ref_o) < 1e-2
+    o32 = torch.empty(B, L, d, device=dev)
+    K.attention_f32(q.float(), k.float(), v.float(), o32, **{kk: vv for kk, vv in common.items()})
+    assert _rel(o32, ref_o) < 1e-5
+    do = torch.randn(B, L, d, device=dev).bfloat16()
+    ref_o.backward(do.float())
+    dq = torch.full((B, L, d), 7.0, device=dev)    # every row written by the reduce
+    dk = torch.empty(B, L, d, device=dev, dtype=torch.bfloat16)
+    dv = torch.empty_like(dk)
+    delta = torch.empty(B, H, L, device=dev)
+    K.attention(q, k, v, o, lse, backward=True, dout=do, sdo=d, bdo=L * d, delta=delta, dq=dq, bdq=L * d,
+                dk=dk, dv=dv, sdk=d, sdv=d, bdk=L * d, bdv=L * d, **common)
+    assert _rel(dq, unheads(qr.grad)) < 2e-2
+    assert _rel(dk, unheads(kr.grad)) < 2e-2
+    assert _rel(dv, unheads(vr.grad)) < 2e-2
+
+
 def test_attention_bwd_fused_dq_rotary():
     """bf16 dQ from the partial-sum reduce with inverse rotary == f32 dQ followed by dq_finalize."""
     torch.manual_seed(9)

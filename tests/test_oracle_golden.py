@@ -87,3 +87,38 @@ def test_cosine_decay_matches_reference():
     np.testing.assert_allclose(got, g['cosine'], rtol=0, atol=0)
     with pytest.raises(KeyboardInterrupt):
         oracle.cosine_decay(1000, 1000)
+
+
+def test_sparse_layout_matches_reference():
+    """oracle.sparse_layout == SparseAttention.get_master_layout (sparse_attention.py:39-60) of the reference,
+    and Attention(sparse=w) builds SparseAttention(window_size=w, block_size=32, causal, include_cls)."""
+    g = load('sparse')
+    for w in (1, 2, 3, 4, 6):
+        ref = g[f'layout_w{w}']
+        nb = ref.shape[-1]
+        ours = oracle.sparse_layout(nb, w).to(torch.int8).numpy()
+        for h in range(ref.shape[0]):
+            np.testing.assert_array_equal(ours, ref[h])
+    for w in (4, 2):
+        np.testing.assert_array_equal(g[f'window_of_sparse_{w}'], [w, 32, 1, 1])
+    # the mask the kernels implement: key k <= q visible iff k < 32 or k // 32 >= q // 32 - (w - 1)
+    L, w = 320, 3
+    m = oracle.sparse_mask(L, w)
+    q, k = torch.meshgrid(torch.arange(L), torch.arange(L), indexing='ij')
+    vis = (k <= q) & ((k < 32) | (k // 32 >= q // 32 - (w - 1)))
+    assert torch.equal(~m, vis)
+
+
+def test_sparse_rotary_table_matches_reference():
+    """The engine's host-built rotary table at SparseAttention's base 2 * 4 * 32 = 256 reproduces the reference's
+    encode_position_rotary(max_pos=256) (golden rot2: positions 0..299, d 32)."""
+    from sparse_vae.engine import rotary_table
+    g = load('ops')
+    start, max_pos = [int(v) for v in g['rot2_meta']]
+    assert (start, max_pos) == (0, 256)
+    x = torch.from_numpy(g['rot2_in'])[0]
+    tab = rotary_table(x.shape[0], x.shape[1], max_pos)
+    c, s = tab[..., 0], tab[..., 1]
+    a, b = x[:, 0::2], x[:, 1::2]
+    out = torch.stack([a * c + (-b) * s, b * c + a * s], -1).flatten(-2)
+    np.testing.assert_allclose(out.numpy(), g['rot2_out'][0], rtol=0, atol=2e-6)
