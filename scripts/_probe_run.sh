@@ -1,4 +1,7 @@
-export TMPDIR=/tmp; mkdir -p gpurun_out/gp2
-for g in 0 4 8 16; do SVAE_GEMM_GROUP=$g timeout -k 10 120 python3 scripts/gemm_probe.py all >> gpurun_out/gp2/probe.log 2>&1 || exit 1; done
-SVAE_GEMM_GROUP=8 timeout -s KILL 90 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex gemm256 -f csv -d gpurun_out/gp2/fetch -o run -- python3 scripts/gemm_probe.py > gpurun_out/gp2/f.log 2>&1
-grep -v amdgpu.ids gpurun_out/gp2/probe.log
+export TMPDIR=/tmp; mkdir -p gpurun_out/gp4
+timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -x -q --timeout 120 --timeout-method thread -k gemm > gpurun_out/gp4/pytest.log 2>&1; rc=$?; tail -3 gpurun_out/gp4/pytest.log; [ $rc = 0 ] || exit $rc
+for cfg in "SVAE_GEMM_PERSIST=0" "SVAE_GEMM_DESYNC=0 SVAE_GEMM_RELAX=0" "SVAE_GEMM_RELAX=0" "SVAE_GEMM_DESYNC=0" "SVAE_GEMM_X=1" "SVAE_GEMM_DESYNC=1" "SVAE_GEMM_DESYNC=4"; do
+  echo "== $cfg" >> gpurun_out/gp4/probe.log
+  env $cfg timeout -k 10 120 python3 scripts/gemm_probe.py all 2>&1 | grep -v amdgpu.ids >> gpurun_out/gp4/probe.log || exit 1
+done
+cat gpurun_out/gp4/probe.log

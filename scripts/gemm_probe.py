@@ -69,7 +69,7 @@ def shape_cases():
 
 
 if __name__ == '__main__':
-    print('SVAE_GEMM_GROUP =', os.environ.get('SVAE_GEMM_GROUP'))
+    print('SVAE_GEMM_GROUP =', os.environ.get('SVAE_GEMM_GROUP'), 'SVAE_GEMM_EXPT =', os.environ.get('SVAE_GEMM_EXPT'))
     head_cases()
     if len(sys.argv) > 1 and sys.argv[1] == 'all':
         shape_cases()

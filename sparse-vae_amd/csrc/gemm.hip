@@ -11,6 +11,7 @@
 #include "common.h"
 #include "../../include/svae.h"
 #include <stdlib.h>
+#include <algorithm>
 
 using namespace svae;
 
@@ -35,6 +36,9 @@ struct GP {
   int epi;
   int tn2, tm2;      // 256-tile counts (gemm256)
   int group;         // L2 grouping: consecutive tiles walk `group` tile rows (M) before the next tile column
+  int total3;        // gemm256: tiles x batch x splits (blocks loop over tiles with stride gridDim.x)
+  int desync;        // gemm256 persistent: odd blocks start this many s_sleep(127) late (staggered epilogues)
+  int relaxed;       // gemm256 persistent: allow the vmcnt(G3_EPI_STORES) first wait after interior epilogues
   long long slab;    // split-K slab mode: split s writes its partial tile at C + s * slab (0 = off)
 };
 
@@ -161,9 +165,9 @@ __device__ __forceinline__ void dropout4(const GP& p, f32x4& x, int m, int n) {
 // Epilogue over 64 rows x 128 columns of the f32 staging tile cs (local rows; global row m0 + rbase + row).
 // Thread = 8 consecutive columns x 4 rows (16 threads per row): 16-B bf16 / 2 x 16-B f32 global vectors.
 // N % 4 == 0, so a thread's group is either fully inside N or holds exactly 4 valid columns ("full").
-template <int EPI>
+template <int EPI, bool BIAS_DONE = false>
 __device__ __forceinline__ void epilogue_half(const GP& p, const float* cs, int m0, int n0, int bn, int rbase,
-                                              long long cofs, int tid) {
+                                              long long cofs, int tid, int label_pre = -1) {
   if constexpr (EPI == SVAE_EPI_F32_ATOMIC) {
     // one column per lane: each wave-wide atomic covers 256 contiguous bytes (the full-rate shape)
     const int col = tid & 127, n = n0 + col;
@@ -179,7 +183,7 @@ __device__ __forceinline__ void epilogue_half(const GP& p, const float* cs, int 
   const bool ncol = n < p.N, full = n + 8 <= p.N;
   const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
   f32x4 b0 = zero, b1 = zero;
-  if (p.bias && ncol) {
+  if (!BIAS_DONE && p.bias && ncol) {
     b0 = *(const f32x4*)(p.bias + n);
     if (full) b1 = *(const f32x4*)(p.bias + n + 4);
   }
@@ -195,7 +199,7 @@ __device__ __forceinline__ void epilogue_half(const GP& p, const float* cs, int 
       const int c = 32 * u + 8 * qd;
       f32x4 x0 = *(const f32x4*)(cs + row * 128 + cs_swz(row, c));
       f32x4 x1 = *(const f32x4*)(cs + row * 128 + cs_swz(row, c + 4));
-      if (p.bias) {
+      if (!BIAS_DONE && p.bias) {
         x0 += (n0 + c < p.N) ? *(const f32x4*)(p.bias + n0 + c) : zero;
         x1 += (n0 + c + 4 < p.N) ? *(const f32x4*)(p.bias + n0 + c + 4) : zero;
       }
@@ -218,7 +222,7 @@ __device__ __forceinline__ void epilogue_half(const GP& p, const float* cs, int 
     se += __shfl_xor(se, 1, 64);
     se += __shfl_xor(se, 2, 64);
     if (m < p.M) {
-      const int lc = p.labels[m] - n0;   // label column within the tile
+      const int lc = (BIAS_DONE ? label_pre : p.labels[m]) - n0;   // label column within the tile (gemm256: preloaded)
       if (lc >= 0 && lc < 128 && ((lc >> 3) & 3) == qd) {
         const int idx = 8 * (lc >> 5) + (lc & 7);
 #pragma unroll
@@ -660,16 +664,23 @@ __device__ __forceinline__ bf16x8 g3_afrag(const char* la, int rb, int ks, int l
   else return read_frag<true>(la + (rb >> 7) * (G3_T / 2), rb & 127, ks, lane);
 }
 
-// gemm256 epilogue: 4 passes of 64 rows; staging = two [64][128] f32 halves (64 KiB of the idle ring)
+// gemm256 epilogue: 4 passes of 64 rows; staging = two [64][128] f32 halves (one 64 KiB stage of the ring, the one
+// the last K-tile was read from). The bias (bcol: this lane's 4 columns, preloaded) goes in with the staging write
+// and the CE labels are preloaded (lab: this thread's row of each pass), so no global load follows a store: the
+// passes' stores stay in flight (raw barriers, no vmcnt drain) and overlap the next tile's first K-step.
 template <int EPI>
-__device__ __forceinline__ void g3_epilogue(const GP& p, char* smem, const f32x4 (&acc)[8][4], int m0, int n0, int bn,
-                                            int batch, int split, int wr, int wc, int tid, int lane) {
+__device__ __forceinline__ void g3_epilogue(const GP& p, char* smem, const f32x4 (&acc)[8][4], const float* sbias,
+                                            const int* slab_, int m0, int n0, int bn, int batch, int split, int wr,
+                                            int wc, int tid, int lane) {
   float* cs = (float*)smem;
   const long long cofs = (long long)batch * p.sC + split * p.slab;
   const int half = tid >> 8;
 #pragma unroll
   for (int pass = 0; pass < 4; ++pass) {
     if (wr == (pass >> 1)) {
+      float bcol[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bcol[j] = sbias[wc * 64 + j * 16 + (lane & 15)];
 #pragma unroll
       for (int ii = 0; ii < 4; ++ii) {
         const int i = (pass & 1) * 4 + ii;
@@ -679,143 +690,212 @@ __device__ __forceinline__ void g3_epilogue(const GP& p, char* smem, const f32x4
           for (int r = 0; r < 4; ++r) {
             const int row = ii * 16 + 4 * (lane >> 4) + r;
             const int col = wc * 64 + j * 16 + (lane & 15);
-            cs[(col >> 7) * 8192 + row * 128 + cs_swz(row, col & 127)] = p.alpha * acc[i][j][r];
+            cs[(col >> 7) * 8192 + row * 128 + cs_swz(row, col & 127)] = fmaf(p.alpha, acc[i][j][r], bcol[j]);
           }
       }
     }
-    __syncthreads();
-    epilogue_half<EPI>(p, cs + half * 8192, m0, n0 + 128 * half, bn * 2 + half, pass * 64, cofs, tid & 255);
-    __syncthreads();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    epilogue_half<EPI, true>(p, cs + half * 8192, m0, n0 + 128 * half, bn * 2 + half, pass * 64, cofs, tid & 255,
+                             EPI == SVAE_EPI_CE_STATS ? slab_[pass * 64 + ((tid & 255) >> 2)] : -1);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
   }
 }
 
+struct G3Tile {
+  int m0, n0, bn, batch, split, kbeg, kend, nk;
+  const bf16* A; const bf16* B;
+};
+
+__device__ __forceinline__ G3Tile g3_tile(const GP& p, int t3) {
+  G3Tile T;
+  const int tiles = p.tn2 * p.tm2;
+  const int z = t3 / tiles, t = t3 - z * tiles;
+  T.batch = z / p.splits;
+  T.split = z - T.batch * p.splits;
+  int bm, bn;
+  group_tile(t, p.tm2, p.tn2, p.group, bm, bn);
+  T.bn = bn;
+  T.m0 = bm * 256;
+  T.n0 = bn * 256;
+  T.kbeg = T.split * p.kchunk;
+  T.kend = min(p.K, T.kbeg + p.kchunk);
+  T.nk = T.kend > T.kbeg ? (T.kend - T.kbeg + 63) / 64 : 0;
+  T.A = p.A + T.batch * p.sA;
+  T.B = p.B + T.batch * p.sB;
+  return T;
+}
+
+// stores issued by every wave of an interior tile's epilogue (lower bound over the epilogues): the next tile's first
+// K-step waits vmcnt(G3_EPI_STORES) instead of 0, so those stores drain under its MFMAs
+constexpr int G3_EPI_STORES = 16;
+static_assert(G3_EPI_STORES == 16, "the first K-step's s_waitcnt literal below");
+
 template <bool AT, bool BT, int EPI>
 __global__ __launch_bounds__(512, 1) void gemm256_kernel(GP p) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * G3_STAGE];
+  // 2 ring stages + a side area for the epilogue's per-tile bias (256 f32) and CE labels (256 i32); one array
+  __shared__ __attribute__((aligned(16))) char smem[2 * G3_STAGE + 2048];
+  float* sbias = (float*)(smem + 2 * G3_STAGE);
+  int* slabel = (int*)(smem + 2 * G3_STAGE + 1024);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3;
-  // XCD-aware bijective remap, then N-fastest
+  // XCD-aware bijective remap of the block id; block b then walks tiles b, b + G, b + 2G, ... (G = gridDim.x):
+  // with G = 256 every XCD runs one contiguous N-fastest range of tiles at a time.
   const int nwg = gridDim.x;
   int bid = blockIdx.x;
   if (nwg >= 16) {
     const int q = nwg / 8, r = nwg % 8, xcd = bid % 8, idx = bid / 8;
     bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
   }
-  const int tiles = p.tn2 * p.tm2;
-  const int z = bid / tiles, t = bid - z * tiles;
-  const int batch = z / p.splits, split = z - batch * p.splits;
-  int bm, bn;
-  group_tile(t, p.tm2, p.tn2, p.group, bm, bn);
-  const int m0 = bm * 256, n0 = bn * 256;
-  const int kbeg = split * p.kchunk;
-  const int kend = min(p.K, kbeg + p.kchunk);
-  const bf16* A = p.A + batch * p.sA;
-  const bf16* B = p.B + batch * p.sB;
-  float rsum[4] = {0.f, 0.f, 0.f, 0.f};
-
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
-  const int nk = kend > kbeg ? (kend - kbeg + 63) / 64 : 0;
+  int t3 = bid;
+  if (t3 >= p.total3) return;
+  G3Tile T = g3_tile(p, t3);
   G3Src sa, sb;
-  if constexpr (AT) sa = g3_src_mn(p.lda, m0, p.M, wave, lane);
-  else sa = g3_src_k(p.lda, m0, p.M, wave, lane);
-  if constexpr (BT) sb = g3_src_mn(p.ldb, n0, p.N, wave, lane);
-  else sb = g3_src_k(p.ldb, n0, p.N, wave, lane);
-  if (nk > 0) g3_issue<AT, BT>(p, A, B, sa, sb, m0, n0, kbeg, kend, smem, wave);
-  for (int kt = 0; kt < nk; ++kt) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's pieces of tile kt landed
-    __builtin_amdgcn_s_barrier();                      // everyone's pieces landed; tile kt-1 fully consumed
-    const char* la = smem + (kt & 1) * G3_STAGE;
-    const char* lb = la + G3_T;
-    if (kt + 1 < nk)
-      g3_issue<AT, BT>(p, A, B, sa, sb, m0, n0, kbeg + (kt + 1) * 64, kend, smem + ((kt + 1) & 1) * G3_STAGE, wave);
-    // Quadrant walk (mh, nh) = (0,0) (0,1) (1,1) (1,0): A fragments of a half reused by two quadrants, B
-    // fragments of a half by the turn. The next quadrant's fragment reads are issued ahead of the current
-    // quadrant's MFMAs, and the MFMA clusters run at raised wave priority.
-    bf16x8 a0[4][2], a1[4][2], b0[2][2], b1[2][2];
+  auto srcs = [&](const G3Tile& X, G3Src& xa, G3Src& xb) {
+    if constexpr (AT) xa = g3_src_mn(p.lda, X.m0, p.M, wave, lane);
+    else xa = g3_src_k(p.lda, X.m0, p.M, wave, lane);
+    if constexpr (BT) xb = g3_src_mn(p.ldb, X.n0, p.N, wave, lane);
+    else xb = g3_src_k(p.ldb, X.n0, p.N, wave, lane);
+  };
+  srcs(T, sa, sb);
+  int g = 0;   // K-tiles consumed so far by this block: the stage of K-tile g is g & 1
+  if (T.nk > 0) g3_issue<AT, BT>(p, T.A, T.B, sa, sb, T.m0, T.n0, T.kbeg, T.kend, smem, wave);
+  if (p.desync > 0 && (bid & 1)) {   // stagger the epilogues of neighbouring blocks (HBM write bursts)
+    for (int i = 0; i < p.desync; ++i) __builtin_amdgcn_s_sleep(127);
+  }
+
+  bool relaxed = false;   // the previous tile was interior: its epilogue issued >= G3_EPI_STORES stores per wave
+  while (true) {
+    const int t3n = t3 + nwg;
+    const bool has_next = t3n < p.total3;
+    float rsum[4] = {0.f, 0.f, 0.f, 0.f};
+    f32x4 acc[8][4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 8; ++i)
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) a0[i][ks] = g3_afrag<AT>(la, wr * 128 + i * 16, ks, lane);
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) b0[j][ks] = g3_bfrag<BT>(lb, wc * 64 + j * 16, ks, lane);
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) b1[j][ks] = g3_bfrag<BT>(lb, wc * 64 + 32 + j * 16, ks, lane);
-    G3_PRIO_HI();
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = mfma16(a0[i][ks], b0[j][ks], acc[i][j]);
-    G3_PRIO_LO();
-    if constexpr (!AT) {   // (AT: transposed A reads need the registers; load after the a0 quadrants)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) a1[i][ks] = g3_afrag<AT>(la, wr * 128 + 64 + i * 16, ks, lane);
-    }
-    G3_PRIO_HI();
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][2 + j] = mfma16(a0[i][ks], b1[j][ks], acc[i][2 + j]);
-    if constexpr (AT) {
-      G3_PRIO_LO();
+      for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+    for (int kt = 0; kt < T.nk; ++kt, ++g) {
+      // this wave's pieces of K-tile g landed (after an interior epilogue, up to G3_EPI_STORES younger stores may
+      // still be in flight: vmcnt retires in issue order)
+      if (kt == 0 && relaxed) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();                      // everyone's landed; K-tile g-1 (other stage) consumed
+      const char* la = smem + (g & 1) * G3_STAGE;
+      const char* lb = la + G3_T;
+      char* nxt = smem + ((g + 1) & 1) * G3_STAGE;
+      if (kt + 1 < T.nk)
+        g3_issue<AT, BT>(p, T.A, T.B, sa, sb, T.m0, T.n0, T.kbeg + (kt + 1) * 64, T.kend, nxt, wave);
+      else if (has_next) {   // the next tile's first K-tile, in flight during this tile's epilogue
+        const G3Tile TN = g3_tile(p, t3n);
+        if (TN.nk > 0) {
+          G3Src xa, xb;
+          srcs(TN, xa, xb);
+          g3_issue<AT, BT>(p, TN.A, TN.B, xa, xb, TN.m0, TN.n0, TN.kbeg, TN.kend, nxt, wave);
+        }
+      }
+      // Quadrant walk (mh, nh) = (0,0) (0,1) (1,1) (1,0): A fragments of a half reused by two quadrants, B
+      // fragments of a half by the turn. The next quadrant's fragment reads are issued ahead of the current
+      // quadrant's MFMAs.
+      bf16x8 a0[4][2], a1[4][2], b0[2][2], b1[2][2];
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks) a1[i][ks] = g3_afrag<AT>(la, wr * 128 + 64 + i * 16, ks, lane);
+        for (int ks = 0; ks < 2; ++ks) a0[i][ks] = g3_afrag<AT>(la, wr * 128 + i * 16, ks, lane);
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) b0[j][ks] = g3_bfrag<BT>(lb, wc * 64 + j * 16, ks, lane);
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) b1[j][ks] = g3_bfrag<BT>(lb, wc * 64 + 32 + j * 16, ks, lane);
       G3_PRIO_HI();
-    }
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
+      for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[4 + i][2 + j] = mfma16(a1[i][ks], b1[j][ks], acc[4 + i][2 + j]);
+          for (int j = 0; j < 2; ++j) acc[i][j] = mfma16(a0[i][ks], b0[j][ks], acc[i][j]);
+      G3_PRIO_LO();
+      if constexpr (!AT) {   // (AT: transposed A reads need the registers; load after the a0 quadrants)
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
+        for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+          for (int ks = 0; ks < 2; ++ks) a1[i][ks] = g3_afrag<AT>(la, wr * 128 + 64 + i * 16, ks, lane);
+      }
+      G3_PRIO_HI();
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[4 + i][j] = mfma16(a1[i][ks], b0[j][ks], acc[4 + i][j]);
-    G3_PRIO_LO();
-    if constexpr (AT) {
-      if (p.a_rowsum && bn == 0) {   // sum_k A[k][m]: thread = 4 m (one 8-B unit) x 8 k-rows
-        const int u = tid & 63, kg = tid >> 6;
-        const char* lh = la + (u >> 5) * (G3_T / 2);
+      for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-        for (int r = 0; r < 8; ++r) {
-          const bf16x4 v = __builtin_bit_cast(bf16x4, *(const short4v*)(lh + mn_off(kg * 8 + r, u & 31)));
+        for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int e = 0; e < 4; ++e) rsum[e] += (float)v[e];
+          for (int j = 0; j < 2; ++j) acc[i][2 + j] = mfma16(a0[i][ks], b1[j][ks], acc[i][2 + j]);
+      if constexpr (AT) {
+        G3_PRIO_LO();
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks) a1[i][ks] = g3_afrag<AT>(la, wr * 128 + 64 + i * 16, ks, lane);
+        G3_PRIO_HI();
+      }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[4 + i][2 + j] = mfma16(a1[i][ks], b1[j][ks], acc[4 + i][2 + j]);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[4 + i][j] = mfma16(a1[i][ks], b0[j][ks], acc[4 + i][j]);
+      G3_PRIO_LO();
+      if constexpr (AT) {
+        if (p.a_rowsum && T.bn == 0) {   // sum_k A[k][m]: thread = 4 m (one 8-B unit) x 8 k-rows
+          const int u = tid & 63, kg = tid >> 6;
+          const char* lh = la + (u >> 5) * (G3_T / 2);
+#pragma unroll
+          for (int r = 0; r < 8; ++r) {
+            const bf16x4 v = __builtin_bit_cast(bf16x4, *(const short4v*)(lh + mn_off(kg * 8 + r, u & 31)));
+#pragma unroll
+            for (int e = 0; e < 4; ++e) rsum[e] += (float)v[e];
+          }
         }
       }
     }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if constexpr (AT) {
-    if (p.a_rowsum && bn == 0) {
-      const int m = m0 + (tid & 63) * 4;
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        if (m + e < p.M) atomicAdd(p.a_rowsum + m + e, rsum[e]);
+    // epilogue operands into the side area, loaded before any store of this tile (the previous epilogue's reads of
+    // the side area finished before this tile's first barrier)
+    if (tid < 256) {
+      const int n = T.n0 + tid, m = T.m0 + tid;
+      sbias[tid] = (p.bias && n < p.N) ? p.bias[n] : 0.f;
+      if (EPI == SVAE_EPI_CE_STATS) slabel[tid] = m < p.M ? p.labels[m] : 0;
     }
+    // every wave's reads of the last K-tile's stage are done: it becomes the epilogue's staging area
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if constexpr (AT) {
+      if (p.a_rowsum && T.bn == 0) {
+        const int m = T.m0 + (tid & 63) * 4;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (m + e < p.M) atomicAdd(p.a_rowsum + m + e, rsum[e]);
+      }
+    }
+    g3_epilogue<EPI>(p, smem + ((g + 1) & 1) * G3_STAGE, acc, sbias, slabel, T.m0, T.n0, T.bn, T.batch, T.split, wr,
+                     wc, tid, lane);
+    relaxed = p.relaxed && T.m0 + 256 <= p.M && T.n0 + 256 <= p.N;
+    if (!has_next) break;
+    const bool prefetched = T.nk > 0;
+    t3 = t3n;
+    T = g3_tile(p, t3);
+    srcs(T, sa, sb);
+    if (!prefetched && T.nk > 0)   // (an empty split-K slice prefetched nothing)
+      g3_issue<AT, BT>(p, T.A, T.B, sa, sb, T.m0, T.n0, T.kbeg, T.kend, smem + (g & 1) * G3_STAGE, wave);
   }
-  g3_epilogue<EPI>(p, smem, acc, m0, n0, bn, batch, split, wr, wc, tid, lane);
 }
 
 // C[m][n] += sum over splits of slab[s][m][n] (slab rows of N floats); 4 columns per thread
@@ -916,7 +996,22 @@ SVAE_EXPORT int svae_gemm(const svae_gemm_desc* d, svae_stream_t stream) {
   if (impl == 3) {
     int kc3 = (d->K + d->splits - 1) / d->splits;
     p.kchunk = (kc3 + 63) / 64 * 64;
-    dim3 grid3((unsigned)blocks256);
+    // persistent above one block per CU (1 block of 8 waves fits a CU): blocks walk their tiles and prefetch the
+    // next tile's first K-tile under the current tile's epilogue. SVAE_GEMM_PERSIST=0 restores 1 block per tile.
+    static const int persist_env = [] { const char* e = getenv("SVAE_GEMM_PERSIST"); return e ? atoi(e) : 1; }();
+    static const int desync_env = [] { const char* e = getenv("SVAE_GEMM_DESYNC"); return e ? atoi(e) : -1; }();
+    static const int ncu = [] {
+      int dev = 0, n = 0;
+      if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        n = 256;
+      return n > 0 ? n : 256;
+    }();
+    p.total3 = (int)blocks256;
+    const long long nb3 = persist_env ? std::min<long long>(blocks256, ncu) : blocks256;
+    p.desync = (nb3 < blocks256 && desync_env > 0) ? desync_env : 0;   // measured: staggering does not pay
+    static const int relax_env = [] { const char* e = getenv("SVAE_GEMM_RELAX"); return e ? atoi(e) : 1; }();
+    p.relaxed = relax_env;
+    dim3 grid3((unsigned)nb3);
 #define SVAE_GEMM3_CASE(E)                                                                                   \
   case E:                                                                                                    \
     if (d->a_t) hipLaunchKernelGGL((gemm256_kernel<true, true, E>), grid3, dim3(512), 0, s, p);              \
