@@ -1,0 +1,62 @@
+"""Per-tile cycle anatomy of gemm256 from the stamps build (diagnostic):
+
+    make -C sparse-vae_amd stamps
+    SVAE_LIB=sparse-vae_amd/sparse_vae/libsvae_stamps.so python scripts/gemm_stamps.py
+For each case: median cycles per tile of the K loop and of the epilogue (blocks 0..7, tiles after the first).
+"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, 'sparse-vae_amd'))
+import torch  # noqa: E402
+from sparse_vae import kernels as K  # noqa: E402
+from sparse_vae import _native as N  # noqa: E402
+
+dev = torch.device('cuda', 0)
+bf16 = torch.bfloat16
+N.lib.svae_debug_stamps.argtypes = [ctypes.c_void_p]
+N.lib.svae_debug_stamps_clear.argtypes = []
+
+
+def stamps():
+    buf = np.zeros((8, 96, 3), dtype=np.uint64)
+    torch.cuda.synchronize()
+    assert N.lib.svae_debug_stamps(buf.ctypes.data) == 0
+    return buf.astype(np.int64)
+
+
+def report(name, fn):
+    zero = np.zeros((8, 96, 3), dtype=np.uint64)
+    N.lib.svae_debug_stamps_clear()
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    s = stamps()
+    ntiles = int((s[0, :, 0] > 0).sum())
+    loop = s[:, 1:ntiles, 1] - s[:, 1:ntiles, 0]
+    epi = s[:, 1:ntiles, 2] - s[:, 1:ntiles, 1]
+    gap = s[:, 2:ntiles, 0] - s[:, 1:ntiles - 1, 2]
+    print(f'{name:28s} tiles/block {ntiles:3d}  K-loop {np.median(loop):8.0f} cyc  epilogue {np.median(epi):7.0f} cyc  '
+          f'between {np.median(gap) if gap.size else 0:6.0f} cyc', flush=True)
+
+
+T, d, V = 32768, 512, 32768
+h = torch.randn(T, d, device=dev).to(bf16)
+W = (0.02 * torch.randn(V, d, device=dev)).to(bf16)
+bias = torch.zeros(V, device=dev)
+logits = torch.empty(T, V, dtype=bf16, device=dev)
+part = torch.empty(T, V // 128, 2, device=dev)
+labels = torch.randint(3, V, (T,), dtype=torch.int32, device=dev)
+lab = torch.empty(T, device=dev)
+report('head bf16', lambda: K.gemm(h, W, logits, T, V, d, epi=N.EPI_BF16, bias=bias))
+report('head ce_stats', lambda: K.gemm(h, W, logits, T, V, d, epi=N.EPI_CE_STATS, bias=bias, aux=part,
+                                       labels=labels, label_logit=lab))
+W1 = (0.02 * torch.randn(2048, d, device=dev)).to(bf16)
+f = torch.empty(T, 2048, dtype=bf16, device=dev)
+gp = torch.empty(T, 2048, dtype=bf16, device=dev)
+report('ffn1 bf16', lambda: K.gemm(h, W1, f, T, 2048, d, epi=N.EPI_BF16))
+report('ffn1 gelu', lambda: K.gemm(h, W1, f, T, 2048, d, epi=N.EPI_GELU, bias=bias[:2048], aux=gp, ldaux=2048))

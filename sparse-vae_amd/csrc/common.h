@@ -58,6 +58,20 @@ __device__ __forceinline__ float gelu_grad_f(float x) {
   return cdf + x * pdf;
 }
 
+// cross-lane reductions over the 4 lane groups (lane ^ 16, lane ^ 32) with VALU permlane swaps (no LDS)
+__device__ __forceinline__ float max_x16_x32(float v) {
+  auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  auto c = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(c[0]), __uint_as_float(c[1]));
+}
+__device__ __forceinline__ float sum_x16_x32(float v) {
+  auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  auto c = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(c[0]) + __uint_as_float(c[1]);
+}
+
 // GELU and GELU' together for the GEMM epilogues: Phi(x) from erfc(|x|/sqrt2) by Abramowitz-Stegun 7.1.26
 // (|erf error| <= 1.5e-7, branchless: one v_rcp, one v_exp, 7 FMAs), and phi(x) = exp(-x^2/2)/sqrt(2 pi)
 // reusing the same exponential. ~1/5 of the instructions of the erff-based pair above.

@@ -101,6 +101,10 @@ __device__ __forceinline__ bf16x8 read_frag(const char* lds, int base, int kk, i
 
 // f32 staging tile [128][128] for the epilogue: 16-B unit index XOR ((row >> 2) & 3) << 2
 __device__ __forceinline__ int cs_swz(int row, int col) { return (((col >> 2) ^ (((row >> 2) & 3) << 2)) << 2) | (col & 3); }
+// gemm256's staging (16-B writes of 8 consecutive rows per lane group): unit index XOR (row & 7)
+__device__ __forceinline__ int cs_swz8(int row, int col) { return (((col >> 2) ^ (row & 7)) << 2) | (col & 3); }
+template <bool SW8>
+__device__ __forceinline__ int cs_at(int row, int col) { return SW8 ? cs_swz8(row, col) : cs_swz(row, col); }
 
 // Tile index -> (bm, bn). group <= 1: N-fastest rows of tiles. group = G: tiles run in bands of G tile rows,
 // M-fastest inside a band, so the ~32 tiles an XCD holds at once cover a G x (32/G) patch whose A and B panels
@@ -165,7 +169,7 @@ __device__ __forceinline__ void dropout4(const GP& p, f32x4& x, int m, int n) {
 // Epilogue over 64 rows x 128 columns of the f32 staging tile cs (local rows; global row m0 + rbase + row).
 // Thread = 8 consecutive columns x 4 rows (16 threads per row): 16-B bf16 / 2 x 16-B f32 global vectors.
 // N % 4 == 0, so a thread's group is either fully inside N or holds exactly 4 valid columns ("full").
-template <int EPI, bool BIAS_DONE = false>
+template <int EPI, bool BIAS_DONE = false, bool SW8 = false>
 __device__ __forceinline__ void epilogue_half(const GP& p, const float* cs, int m0, int n0, int bn, int rbase,
                                               long long cofs, int tid, int label_pre = -1) {
   if constexpr (EPI == SVAE_EPI_F32_ATOMIC) {
@@ -174,7 +178,7 @@ __device__ __forceinline__ void epilogue_half(const GP& p, const float* cs, int 
     if (n < p.N) {
       for (int it = 0; it < 32; ++it) {
         const int row = (tid >> 7) + 2 * it, m = m0 + rbase + row;
-        if (m < p.M) atomicAdd((float*)p.C + cofs + (long long)m * p.ldc + n, cs[row * 128 + cs_swz(row, col)]);
+        if (m < p.M) atomicAdd((float*)p.C + cofs + (long long)m * p.ldc + n, cs[row * 128 + cs_at<SW8>(row, col)]);
       }
     }
     return;
@@ -197,8 +201,8 @@ __device__ __forceinline__ void epilogue_half(const GP& p, const float* cs, int 
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int c = 32 * u + 8 * qd;
-      f32x4 x0 = *(const f32x4*)(cs + row * 128 + cs_swz(row, c));
-      f32x4 x1 = *(const f32x4*)(cs + row * 128 + cs_swz(row, c + 4));
+      f32x4 x0 = *(const f32x4*)(cs + row * 128 + cs_at<SW8>(row, c));
+      f32x4 x1 = *(const f32x4*)(cs + row * 128 + cs_at<SW8>(row, c + 4));
       if (!BIAS_DONE && p.bias) {
         x0 += (n0 + c < p.N) ? *(const f32x4*)(p.bias + n0 + c) : zero;
         x1 += (n0 + c + 4 < p.N) ? *(const f32x4*)(p.bias + n0 + c + 4) : zero;
@@ -242,8 +246,8 @@ __device__ __forceinline__ void epilogue_half(const GP& p, const float* cs, int 
   for (int it = 0; it < 4; ++it) {
     const int row = (tid >> 4) + 16 * it, m = m0 + rbase + row;
     if (m >= p.M) break;
-    f32x4 x0 = *(const f32x4*)(cs + row * 128 + cs_swz(row, cc));
-    f32x4 x1 = full ? *(const f32x4*)(cs + row * 128 + cs_swz(row, cc + 4)) : zero;
+    f32x4 x0 = *(const f32x4*)(cs + row * 128 + cs_at<SW8>(row, cc));
+    f32x4 x1 = full ? *(const f32x4*)(cs + row * 128 + cs_at<SW8>(row, cc + 4)) : zero;
     const long long ci = cofs + (long long)m * p.ldc + n;
     if constexpr (EPI == SVAE_EPI_BF16) {
       store_bf16((bf16*)p.C + ci, x0 + b0, x1 + b1, full);
@@ -664,10 +668,13 @@ __device__ __forceinline__ bf16x8 g3_afrag(const char* la, int rb, int ks, int l
   else return read_frag<true>(la + (rb >> 7) * (G3_T / 2), rb & 127, ks, lane);
 }
 
-// gemm256 epilogue: 4 passes of 64 rows; staging = two [64][128] f32 halves (one 64 KiB stage of the ring, the one
-// the last K-tile was read from). The bias (bcol: this lane's 4 columns, preloaded) goes in with the staging write
-// and the CE labels are preloaded (lab: this thread's row of each pass), so no global load follows a store: the
-// passes' stores stay in flight (raw barriers, no vmcnt drain) and overlap the next tile's first K-step.
+// gemm256 accumulators are C^T fragments (MFMA operands swapped): acc[i][j] lane l holds row
+// wr*128 + 16i + (l & 15), columns wc*64 + 16j + 4(l >> 4) + (0..3) -- one row, 4 consecutive columns.
+//
+// Staged epilogue (the f32-output, rotary and GELU' epilogues, which read other tensors): 4 passes of 64 rows;
+// staging = two [64][128] f32 halves (the ring stage the last K-tile was read from), one 16-B write per fragment.
+// The bias (side area) goes in with the staging write and no global load precedes the first store, so the passes'
+// stores stay in flight (raw barriers, no vmcnt drain) into the next tile's first K-step.
 template <int EPI>
 __device__ __forceinline__ void g3_epilogue(const GP& p, char* smem, const f32x4 (&acc)[8][4], const float* sbias,
                                             const int* slab_, int m0, int n0, int bn, int batch, int split, int wr,
@@ -678,28 +685,235 @@ __device__ __forceinline__ void g3_epilogue(const GP& p, char* smem, const f32x4
 #pragma unroll
   for (int pass = 0; pass < 4; ++pass) {
     if (wr == (pass >> 1)) {
-      float bcol[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) bcol[j] = sbias[wc * 64 + j * 16 + (lane & 15)];
 #pragma unroll
       for (int ii = 0; ii < 4; ++ii) {
         const int i = (pass & 1) * 4 + ii;
+        const int row = ii * 16 + (lane & 15);
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int row = ii * 16 + 4 * (lane >> 4) + r;
-            const int col = wc * 64 + j * 16 + (lane & 15);
-            cs[(col >> 7) * 8192 + row * 128 + cs_swz(row, col & 127)] = fmaf(p.alpha, acc[i][j][r], bcol[j]);
-          }
+        for (int j = 0; j < 4; ++j) {
+          const int col = wc * 64 + j * 16 + 4 * (lane >> 4);
+          const f32x4 b4 = *(const f32x4*)(sbias + col);
+          *(f32x4*)(cs + (col >> 7) * 8192 + row * 128 + cs_swz8(row, col & 127)) = p.alpha * acc[i][j] + b4;
+        }
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    epilogue_half<EPI, true>(p, cs + half * 8192, m0, n0 + 128 * half, bn * 2 + half, pass * 64, cofs, tid & 255,
+    epilogue_half<EPI, true, true>(p, cs + half * 8192, m0, n0 + 128 * half, bn * 2 + half, pass * 64, cofs, tid & 255,
                              EPI == SVAE_EPI_CE_STATS ? slab_[pass * 64 + ((tid & 255) >> 2)] : -1);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
+  }
+}
+
+// Register epilogue (bf16 out, GELU, CE statistics): straight from the C^T fragments, no staging. Each fragment
+// is one 8-B bf16x4 store per lane (16 rows x 32 B per instruction; a row's 128-B line completes over the 4 j).
+// CE: per-row (max, sum exp) over the wave's 64 columns by permlane reductions, combined across the 4 column
+// waves through the side area into the 128-column partials ce_rows_kernel expects; the label logit is written
+// by the lane holding it.
+constexpr float G3_LOG2E = 1.4426950408889634f;
+
+__device__ __forceinline__ unsigned pack_bf16x2(float a, float b) {
+  typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(unsigned, (bf16x2v){f2bf(a), f2bf(b)});
+}
+
+// Store the bf16 of two fragments' column groups x (cols 16ja + 4g..) and y (cols 16ja + 16 + 4g..) of one row
+// as 16-B vectors: a permlane16 swap gives lane group g 8 consecutive columns (g0: 0-7, g2: 8-15, g1: 16-23,
+// g3: 24-31 of the pair), so each instruction writes 16 rows x 64 contiguous bytes.
+__device__ __forceinline__ void store_pair_bf16(bf16* row_base, int colbase, int ncols_left, const f32x4& x,
+                                                const f32x4& y, int g) {
+  const unsigned x0 = pack_bf16x2(x[0], x[1]), x1 = pack_bf16x2(x[2], x[3]);
+  const unsigned y0 = pack_bf16x2(y[0], y[1]), y1 = pack_bf16x2(y[2], y[3]);
+  const auto s0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
+  const auto s1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
+  const int c = colbase + ((g & 1) ? 16 : 0) + ((g & 2) ? 8 : 0);
+  const u32x4 w = {s0[0], s1[0], s0[1], s1[1]};
+  if (c + 8 <= ncols_left) *(u32x4*)(row_base + c) = w;
+  else if (c < ncols_left) *(u32x2*)(row_base + c) = (u32x2){w[0], w[1]};
+}
+
+template <int EPI>
+__device__ __forceinline__ void g3_reg_epilogue(const GP& p, const f32x4 (&acc)[8][4], const float* sbias,
+                                                const int* slabel, float* sstat, int m0, int n0, int bn, int batch,
+                                                int split, int wr, int wc, int tid, int lane) {
+  const long long cofs = (long long)batch * p.sC + split * p.slab;
+  const int g = lane >> 4, li = lane & 15;
+  f32x4 b4[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) b4[j] = *(const f32x4*)(sbias + wc * 64 + j * 16 + 4 * g);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int rl = wr * 128 + i * 16 + li, m = m0 + rl;
+    f32x4 v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = p.alpha * acc[i][j] + b4[j];
+    {
+      // (the permlane swaps need every lane: the bounds are applied to the stores only)
+      const bool row_ok = m < p.M;
+      const int nleft = p.N - (n0 + wc * 64);
+      bf16* crow = (bf16*)p.C + cofs + (long long)(row_ok ? m : 0) * p.ldc + n0 + wc * 64;
+      if constexpr (EPI == SVAE_EPI_GELU) {
+        f32x4 gg[4], dg[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float ge, de;
+            gelu_pair(v[j][e], ge, de);
+            gg[j][e] = ge;
+            dg[j][e] = de;
+          }
+        bf16* arow = (bf16*)p.aux + (long long)(row_ok ? m : 0) * p.ldaux + n0 + wc * 64;
+#pragma unroll
+        for (int jp = 0; jp < 2; ++jp) {
+          store_pair_bf16(crow, 32 * jp, row_ok ? nleft : 0, gg[2 * jp], gg[2 * jp + 1], g);
+          store_pair_bf16(arow, 32 * jp, row_ok ? nleft : 0, dg[2 * jp], dg[2 * jp + 1], g);
+        }
+      } else {
+#pragma unroll
+        for (int jp = 0; jp < 2; ++jp) store_pair_bf16(crow, 32 * jp, row_ok ? nleft : 0, v[2 * jp], v[2 * jp + 1], g);
+      }
+    }
+    if constexpr (EPI == SVAE_EPI_CE_STATS) {
+      const bool ragged = n0 + wc * 64 + 64 > p.N;   // wave-uniform
+      float mx = -INFINITY;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          if (ragged && n0 + wc * 64 + j * 16 + 4 * g + e >= p.N) v[j][e] = -INFINITY;
+          mx = fmaxf(mx, v[j][e]);
+        }
+      mx = max_x16_x32(mx);
+      const float mc = mx == -INFINITY ? 0.f : mx * G3_LOG2E;
+      float se = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) se += __builtin_amdgcn_exp2f(fmaf(v[j][e], G3_LOG2E, -mc));
+      se = sum_x16_x32(se);
+      if (g == 0) {
+        sstat[(rl * 4 + wc) * 2] = mx;
+        sstat[(rl * 4 + wc) * 2 + 1] = se;
+      }
+      const int lc = slabel[rl] - (n0 + wc * 64);   // label column within this wave's 64
+      if (m < p.M && lc >= 0 && lc < 64 && ((lc >> 2) & 3) == g) {
+        float x = 0.f;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (j == (lc >> 4) && e == (lc & 3)) x = v[j][e];
+        p.label_logit[m] = x;
+      }
+    }
+  }
+  if constexpr (EPI == SVAE_EPI_CE_STATS) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    const int row = tid >> 1, hf = tid & 1, m = m0 + row;   // 512 threads: (row, 128-column half)
+    if (m < p.M && n0 + 128 * hf < p.N) {
+      const float* s = sstat + (row * 4 + 2 * hf) * 2;
+      const float m1 = s[0], s1 = s[1], m2 = s[2], s2 = s[3];
+      const float mm = fmaxf(m1, m2);
+      const float e1 = m1 == -INFINITY ? 0.f : __builtin_amdgcn_exp2f((m1 - mm) * G3_LOG2E);
+      const float e2 = m2 == -INFINITY ? 0.f : __builtin_amdgcn_exp2f((m2 - mm) * G3_LOG2E);
+      float* part = (float*)p.aux + ((long long)m * p.tiles_n + bn * 2 + hf) * 2;
+      part[0] = mm;
+      part[1] = s1 * e1 + s2 * e2;
+    }
+  }
+}
+
+// Register epilogue for the epilogues that read another tensor: f32 out (+resid), f32 accumulate, dropout +
+// resid, and bf16 x GELU' (the FFN backward). The operand rows for fragment row i + 1 are loaded before row i's
+// stores are issued, so the compiler's counted waits never drain the stores (vmcnt retires in issue order).
+// f32 rows: one 16-B load / store per fragment (16 rows x 64 B per instruction); GELU': the permlane-swapped
+// 8-column layout of store_pair_bf16, with the matching 16-B aux loads.
+template <int EPI>
+__device__ __forceinline__ void g3_reg_epilogue_ld(const GP& p, const f32x4 (&acc)[8][4], const float* sbias, int m0,
+                                                   int n0, int batch, int split, int wr, int wc, int lane) {
+  const long long cofs = (long long)batch * p.sC + split * p.slab;
+  const int g = lane >> 4, li = lane & 15;
+  const int nb = n0 + wc * 64;                  // this wave's first column
+  f32x4 b4[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) b4[j] = *(const f32x4*)(sbias + wc * 64 + j * 16 + 4 * g);
+  if constexpr (EPI == SVAE_EPI_GELU_BWD) {
+    const int cs = ((g & 1) ? 16 : 0) + ((g & 2) ? 8 : 0);   // column of this lane's 8 within a 32-column pair
+    auto ld_row = [&](int i, u32x4 (&r)[2]) {
+      const int m = m0 + wr * 128 + i * 16 + li;
+#pragma unroll
+      for (int jp = 0; jp < 2; ++jp) {
+        const int n = nb + 32 * jp + cs;
+        r[jp] = (m < p.M && n + 8 <= p.N) ? *(const u32x4*)((const bf16*)p.aux + (long long)m * p.ldaux + n)
+                                          : (u32x4){0u, 0u, 0u, 0u};
+      }
+    };
+    u32x4 cur[2], nxt[2];
+    ld_row(0, cur);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if (i + 1 < 8) ld_row(i + 1, nxt);
+      const int m = m0 + wr * 128 + i * 16 + li;
+#pragma unroll
+      for (int jp = 0; jp < 2; ++jp) {
+        const f32x4 x = p.alpha * acc[i][2 * jp] + b4[2 * jp], y = p.alpha * acc[i][2 * jp + 1] + b4[2 * jp + 1];
+        float w[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const auto s = __builtin_amdgcn_permlane16_swap(__float_as_uint(x[e]), __float_as_uint(y[e]), false, false);
+          w[e] = __uint_as_float(s[0]);
+          w[4 + e] = __uint_as_float(s[1]);
+        }
+        const bf16x8 a = __builtin_bit_cast(bf16x8, cur[jp]);
+        const u32x4 o = {pack_bf16x2(w[0] * (float)a[0], w[1] * (float)a[1]), pack_bf16x2(w[2] * (float)a[2], w[3] * (float)a[3]),
+                         pack_bf16x2(w[4] * (float)a[4], w[5] * (float)a[5]), pack_bf16x2(w[6] * (float)a[6], w[7] * (float)a[7])};
+        const int n = nb + 32 * jp + cs;
+        if (m < p.M && n + 8 <= p.N) *(u32x4*)((bf16*)p.C + cofs + (long long)m * p.ldc + n) = o;
+        else if (m < p.M && n < p.N) *(u32x2*)((bf16*)p.C + cofs + (long long)m * p.ldc + n) = (u32x2){o[0], o[1]};
+      }
+      if (i + 1 < 8) {
+        cur[0] = nxt[0];
+        cur[1] = nxt[1];
+      }
+    }
+    return;
+  } else {
+    // f32 out: F32 (+resid when given), F32_ACC (+C), DROPOUT_RESID (dropout then +resid)
+    const float* src = EPI == SVAE_EPI_F32_ACC ? (const float*)p.C + cofs : p.resid;
+    const long long lds_ = EPI == SVAE_EPI_F32_ACC ? p.ldc : p.ldr;
+    const bool ld = src != nullptr;
+    auto ld_row = [&](int i, f32x4 (&r)[4]) {
+      const int m = m0 + wr * 128 + i * 16 + li;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = nb + j * 16 + 4 * g;
+        r[j] = (ld && m < p.M && n < p.N) ? *(const f32x4*)(src + (long long)m * lds_ + n) : (f32x4){0.f, 0.f, 0.f, 0.f};
+      }
+    };
+    f32x4 cur[4], nxt[4];
+    ld_row(0, cur);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if (i + 1 < 8) ld_row(i + 1, nxt);
+      const int m = m0 + wr * 128 + i * 16 + li;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = nb + j * 16 + 4 * g;
+        f32x4 x = p.alpha * acc[i][j] + b4[j];
+        if constexpr (EPI == SVAE_EPI_DROPOUT_RESID) {
+          if (p.drop_p > 0.f) dropout4(p, x, m, n);
+        }
+        x += cur[j];
+        if (m < p.M && n < p.N) *(f32x4*)((float*)p.C + cofs + (long long)m * p.ldc + n) = x;
+      }
+      if (i + 1 < 8) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) cur[j] = nxt[j];
+      }
+    }
   }
 }
 
@@ -730,14 +944,26 @@ __device__ __forceinline__ G3Tile g3_tile(const GP& p, int t3) {
 // stores issued by every wave of an interior tile's epilogue (lower bound over the epilogues): the next tile's first
 // K-step waits vmcnt(G3_EPI_STORES) instead of 0, so those stores drain under its MFMAs
 constexpr int G3_EPI_STORES = 16;
+
+#ifdef SVAE_STAMPS
+// diagnostic build only (make STAMPS=1 -> libsvae_stamps.so): s_memtime at tile start / after the K loop / after
+// the epilogue, for blocks 0..7 and their first 96 tiles
+__device__ unsigned long long svae_stamps[8][96][3];
+#define G3_STAMP(k) \
+  do { if (blockIdx.x < 8 && tid == 0 && ntile < 96) svae_stamps[blockIdx.x][ntile][k] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define G3_STAMP(k) ((void)0)
+#endif
 static_assert(G3_EPI_STORES == 16, "the first K-step's s_waitcnt literal below");
 
 template <bool AT, bool BT, int EPI>
 __global__ __launch_bounds__(512, 1) void gemm256_kernel(GP p) {
-  // 2 ring stages + a side area for the epilogue's per-tile bias (256 f32) and CE labels (256 i32); one array
-  __shared__ __attribute__((aligned(16))) char smem[2 * G3_STAGE + 2048];
+  // 2 ring stages + a side area: the epilogue's per-tile bias (256 f32), CE labels (256 i32) and CE row statistics
+  // ([256 rows][4 column waves][max, sum]); one array
+  __shared__ __attribute__((aligned(16))) char smem[2 * G3_STAGE + 2048 + 8192];
   float* sbias = (float*)(smem + 2 * G3_STAGE);
   int* slabel = (int*)(smem + 2 * G3_STAGE + 1024);
+  float* sstat = (float*)(smem + 2 * G3_STAGE + 2048);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3;
@@ -767,7 +993,10 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GP p) {
   }
 
   bool relaxed = false;   // the previous tile was interior: its epilogue issued >= G3_EPI_STORES stores per wave
+  int ntile = 0;
+  (void)ntile;
   while (true) {
+    G3_STAMP(0);
     const int t3n = t3 + nwg;
     const bool has_next = t3n < p.total3;
     float rsum[4] = {0.f, 0.f, 0.f, 0.f};
@@ -818,7 +1047,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GP p) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int j = 0; j < 2; ++j) acc[i][j] = mfma16(a0[i][ks], b0[j][ks], acc[i][j]);
+          for (int j = 0; j < 2; ++j) acc[i][j] = mfma16(b0[j][ks], a0[i][ks], acc[i][j]);
       G3_PRIO_LO();
       if constexpr (!AT) {   // (AT: transposed A reads need the registers; load after the a0 quadrants)
 #pragma unroll
@@ -832,7 +1061,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GP p) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int j = 0; j < 2; ++j) acc[i][2 + j] = mfma16(a0[i][ks], b1[j][ks], acc[i][2 + j]);
+          for (int j = 0; j < 2; ++j) acc[i][2 + j] = mfma16(b1[j][ks], a0[i][ks], acc[i][2 + j]);
       if constexpr (AT) {
         G3_PRIO_LO();
 #pragma unroll
@@ -846,13 +1075,13 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GP p) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int j = 0; j < 2; ++j) acc[4 + i][2 + j] = mfma16(a1[i][ks], b1[j][ks], acc[4 + i][2 + j]);
+          for (int j = 0; j < 2; ++j) acc[4 + i][2 + j] = mfma16(b1[j][ks], a1[i][ks], acc[4 + i][2 + j]);
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int j = 0; j < 2; ++j) acc[4 + i][j] = mfma16(a1[i][ks], b0[j][ks], acc[4 + i][j]);
+          for (int j = 0; j < 2; ++j) acc[4 + i][j] = mfma16(b0[j][ks], a1[i][ks], acc[4 + i][j]);
       G3_PRIO_LO();
       if constexpr (AT) {
         if (p.a_rowsum && T.bn == 0) {   // sum_k A[k][m]: thread = 4 m (one 8-B unit) x 8 k-rows
@@ -867,6 +1096,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GP p) {
         }
       }
     }
+    G3_STAMP(1);
     // epilogue operands into the side area, loaded before any store of this tile (the previous epilogue's reads of
     // the side area finished before this tile's first barrier)
     if (tid < 256) {
@@ -885,9 +1115,17 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GP p) {
           if (m + e < p.M) atomicAdd(p.a_rowsum + m + e, rsum[e]);
       }
     }
-    g3_epilogue<EPI>(p, smem + ((g + 1) & 1) * G3_STAGE, acc, sbias, slabel, T.m0, T.n0, T.bn, T.batch, T.split, wr,
-                     wc, tid, lane);
+    if constexpr (EPI == SVAE_EPI_BF16 || EPI == SVAE_EPI_GELU || EPI == SVAE_EPI_CE_STATS)
+      g3_reg_epilogue<EPI>(p, acc, sbias, slabel, sstat, T.m0, T.n0, T.bn, T.batch, T.split, wr, wc, tid, lane);
+    else if constexpr (EPI == SVAE_EPI_F32 || EPI == SVAE_EPI_F32_ACC || EPI == SVAE_EPI_DROPOUT_RESID ||
+                       EPI == SVAE_EPI_GELU_BWD)
+      g3_reg_epilogue_ld<EPI>(p, acc, sbias, T.m0, T.n0, T.batch, T.split, wr, wc, lane);
+    else
+      g3_epilogue<EPI>(p, smem + ((g + 1) & 1) * G3_STAGE, acc, sbias, slabel, T.m0, T.n0, T.bn, T.batch, T.split,
+                       wr, wc, tid, lane);
     relaxed = p.relaxed && T.m0 + 256 <= p.M && T.n0 + 256 <= p.N;
+    G3_STAMP(2);
+    ++ntile;
     if (!has_next) break;
     const bool prefetched = T.nk > 0;
     t3 = t3n;
@@ -1083,3 +1321,13 @@ SVAE_EXPORT int svae_gemm(const svae_gemm_desc* d, svae_stream_t stream) {
   SVAE_LAUNCH_CHECK();
   return slab ? launch_slab_reduce(d, s) : SVAE_OK;
 }
+
+#ifdef SVAE_STAMPS
+extern "C" __attribute__((visibility("default"))) int svae_debug_stamps(unsigned long long* host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(svae_stamps), sizeof(svae_stamps)) == hipSuccess ? 0 : -1;
+}
+extern "C" __attribute__((visibility("default"))) int svae_debug_stamps_clear() {
+  static unsigned long long zeros[8 * 96 * 3];
+  return hipMemcpyToSymbol(HIP_SYMBOL(svae_stamps), zeros, sizeof(zeros)) == hipSuccess ? 0 : -1;
+}
+#endif
