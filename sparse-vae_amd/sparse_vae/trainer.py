@@ -53,8 +53,7 @@ class Trainer:
         model.on_train_start()
         datamodule.prepare_data()
         datamodule.setup('fit')
-        B, L = datamodule.batch_shape()
-        [opt], [sch] = model.configure_optimizers(B * L, self.accumulate_grad_batches)
+        [opt], [sch] = model.configure_optimizers(datamodule.tokens_per_step(), self.accumulate_grad_batches)
         sched = sch['scheduler']
         model.train()
         t0 = time.time()
