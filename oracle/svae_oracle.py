@@ -18,7 +18,7 @@ __all__ = [
     'rotary', 'sparse_layout', 'sparse_mask', 'attention', 'transformer_layer', 'perceiver', 'conditional_gaussian',
     'sample_z', 'reconstruct', 'output_layer', 'robust_cross_entropy', 'marginal_kl',
     'training_step', 'radam_step', 'clip_grad_norm', 'cosine_decay', 'kl_anneal',
-    'RAdamState',
+    'RAdamState', 'prior_log_prob', 'p_of_x_given_z', 'estimate_log_prob_iw', 'test_step_iw', 'generate',
 ]
 
 
@@ -54,8 +54,15 @@ def sparse_layout(num_blocks: int, window: int) -> torch.Tensor:
 def sparse_mask(L: int, window: int) -> torch.Tensor:
     """[L, L] True where a key is NOT visible to a query under SparseAttention.__call__ (sparse_attention.py:
     75-92): outside the block layout, or above the diagonal (blocksparse softmax is_causal). Absent blocks
-    never enter the softmax; the -1e7 shift below gives them exactly zero weight, so the two agree."""
-    blk = sparse_layout(L // 32, window).repeat_interleave(32, 0).repeat_interleave(32, 1)
+    never enter the softmax; the -1e7 shift below gives them exactly zero weight, so the two agree.
+    For L % 32 != 0 (decoding prefixes) this is the key set the windowed KV cache of attention.py:107-140
+    returns: the [CLS] block, the window - 1 previous blocks and the current block up to the query."""
+    if L % 32 == 0:
+        blk = sparse_layout(L // 32, window).repeat_interleave(32, 0).repeat_interleave(32, 1)
+    else:
+        b = torch.arange(L) // 32
+        off = b[:, None] - b[None, :]
+        blk = ((off >= 0) & (off < window)) | (b[None, :] == 0)
     return ~blk | torch.ones(L, L, dtype=torch.bool).triu(1)
 
 
@@ -84,7 +91,7 @@ def attention(p: Dict[str, torch.Tensor], pre: str, q_in, k_in, v_in, pad: Optio
     scores = q @ k.transpose(-1, -2) * k.shape[-1] ** -0.5          # :83
     causal_mask = None
     if window:                                           # sparse: band + [CLS] block + causal (is_causal)
-        assert causal and q.shape[-2] % 32 == 0
+        assert causal
         causal_mask = sparse_mask(q.shape[-2], window)
     elif causal:                                         # :85-87
         ql = q.shape[-2]
@@ -284,3 +291,79 @@ def kl_anneal(kl_weight, kl_start, kl_end, max_steps, cur_step):
     if not max_steps or kl_weight >= kl_end:
         return kl_weight
     return kl_start + (kl_end - kl_start) * (cur_step / max_steps)
+
+
+# ---- evaluation (importance-weighted NLL) and generation --------------------------------------------
+
+def prior_log_prob(z):
+    """ContinuousVAE.prior_log_prob, continuous_autoencoder.py:55-57."""
+    return -0.5 * z.pow(2.0).sum(dim=-1) - math.log(math.sqrt(2 * math.pi)) * z.shape[-1]
+
+
+def p_of_x_given_z(p, hp, x, z, labels, pad):
+    """continuous_autoencoder.py:82-88: log p(x|z) summed over the sequence. x [c, B, L, d] (the expanded
+    embedding), z [c, B, 1, Z], labels [c, B, L-1]; log_softmax column 0 zeroed, so label 0 adds 0."""
+    c, B, L, d = x.shape
+    xf, zf = x.reshape(c * B, L, d), z.reshape(c * B, 1, z.shape[-1])
+    padf = pad.expand(c, B, L).reshape(c * B, L) if pad is not None else None
+    logits = reconstruct(p, xf, zf, padf, hp)[..., :-1, :]
+    log_probs = logits.log_softmax(dim=-1)
+    log_probs[..., 0] = 0.0
+    lp = log_probs.gather(dim=-1, index=labels.reshape(c * B, L - 1).unsqueeze(-1)).squeeze(-1).sum(dim=-1)
+    return lp.reshape(c, B)
+
+
+def estimate_log_prob_iw(p, hp, mu, scale, x, labels, pad, eps, num_iter):
+    """ContinuousVAE.estimate_log_prob_iw, continuous_autoencoder.py:62-80, with the rsample draws injected:
+    eps [num_samples, B, 1, Z] (chunk i uses eps[i*chunk:(i+1)*chunk]). The tensor shapes are the reference's
+    own, so its broadcasting ([chunk, B, 1] + [chunk, B]) is reproduced as is."""
+    S = eps.shape[0]
+    assert S % num_iter == 0
+    chunk = S // num_iter
+    log_ws = []
+    for it in range(num_iter):
+        z = mu + eps[it * chunk:(it + 1) * chunk] * scale                   # [chunk, B, 1, Z]
+        log_p_of_z = prior_log_prob(z)                                      # [chunk, B, 1]
+        log_q_of_z = torch.distributions.Normal(mu, scale).log_prob(z).sum(dim=-1)
+        lpx = p_of_x_given_z(p, hp, x.unsqueeze(0).expand(chunk, *x.shape), z,
+                             labels.expand(chunk, *labels.shape)[..., 1:], pad)
+        log_ws.append(log_p_of_z + lpx - log_q_of_z)
+    return torch.cat(log_ws).logsumexp(dim=0) - math.log(S)
+
+
+def test_step_iw(p, hp, ids, num_tokens, eps, num_iter, pad='auto'):
+    """TransformerVAE.test_step, transformer_vae.py:71-79 (num_samples = eps.shape[0]). Returns nll_iw."""
+    if isinstance(pad, str):
+        pad = ids.eq(0)
+    x = F.embedding(ids, p['input_layer.0.weight'])
+    enc = perceiver(p, x, pad, hp)
+    mu, logvar, scale, _ = conditional_gaussian(p, enc)
+    log_prob = estimate_log_prob_iw(p, hp, mu, scale, x, ids, pad, eps, num_iter) / num_tokens
+    return -log_prob.mean()
+
+
+def generate(p, hp, z, max_length, start_token, end_token, repetition_penalty=1.2):
+    """TransformerVAE.sample (transformer_vae.py:95-128) with GenerationState (generation.py) in its greedy
+    branch (temperature <= 0 or top_k == 1), restated without a KV cache: each step recomputes the decoder
+    over the prefix (position 0 replaced by z_projections[i](z) in every layer, as at step 1 of the cached
+    decode) and reads the last position. Sparse attention: the windowed cache's key set (sparse_mask)."""
+    B = z.shape[0]
+    out = torch.zeros(B, max_length, dtype=torch.long)
+    out[:, 0] = start_token
+    live = torch.ones(B, dtype=torch.bool)
+    idx = 1
+    while not (idx >= max_length - 1 or not live.any()):                  # generation.py:83-84
+        prefix = out[live, :idx]
+        x = F.embedding(prefix, p['input_layer.0.weight'])
+        logits = reconstruct(p, x, z[live].reshape(-1, 1, z.shape[-1]), None, hp)[:, -1]
+        if repetition_penalty > 1.0:                                        # generation.py:35-41
+            prev = out[live, max(idx - 512, 0):idx]
+            pl = logits.gather(-1, prev)
+            logits = logits.scatter(-1, prev, torch.where(pl < 0.0, pl * repetition_penalty,
+                                                          pl / repetition_penalty))
+        tok = logits.argmax(dim=-1)                                         # :44-45
+        out[live, idx] = tok
+        idx += 1
+        cont = (tok != end_token) & (idx < max_length)                      # :73-75
+        live[live.clone()] &= cont
+    return out[:, 1:]

@@ -207,7 +207,7 @@ __device__ __forceinline__ void epilogue_half(const GP& p, const float* cs, int 
         x0 += (n0 + c < p.N) ? *(const f32x4*)(p.bias + n0 + c) : zero;
         x1 += (n0 + c + 4 < p.N) ? *(const f32x4*)(p.bias + n0 + c + 4) : zero;
       }
-      if (m < p.M && n0 + c < p.N)
+      if (p.C && m < p.M && n0 + c < p.N)   // C == nullptr: statistics only (the IW-NLL evaluation)
         store_bf16((bf16*)p.C + cofs + (long long)m * p.ldc + n0 + c, x0, x1, n0 + c + 8 <= p.N);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -770,7 +770,7 @@ __device__ __forceinline__ void g3_reg_epilogue(const GP& p, const f32x4 (&acc)[
           store_pair_bf16(crow, 32 * jp, row_ok ? nleft : 0, gg[2 * jp], gg[2 * jp + 1], g);
           store_pair_bf16(arow, 32 * jp, row_ok ? nleft : 0, dg[2 * jp], dg[2 * jp + 1], g);
         }
-      } else {
+      } else if (EPI != SVAE_EPI_CE_STATS || p.C) {   // CE statistics with C == nullptr: no logits stored
 #pragma unroll
         for (int jp = 0; jp < 2; ++jp) store_pair_bf16(crow, 32 * jp, row_ok ? nleft : 0, v[2 * jp], v[2 * jp + 1], g);
       }
@@ -1163,7 +1163,7 @@ static int launch_slab_reduce(const svae_gemm_desc* d, hipStream_t s) {
 }
 
 SVAE_EXPORT int svae_gemm(const svae_gemm_desc* d, svae_stream_t stream) {
-  if (!d || !d->A || !d->B || !d->C) return SVAE_EINVAL;
+  if (!d || !d->A || !d->B || (!d->C && d->epi != SVAE_EPI_CE_STATS)) return SVAE_EINVAL;
   if (d->M <= 0 || d->N <= 0 || d->K <= 0 || d->batch <= 0 || d->splits <= 0) return SVAE_EINVAL;
   if ((d->K % 8 && !(d->a_t && d->b_t)) || d->lda % 8 || d->ldb % 8) return SVAE_EINVAL;
   if (d->a_t && d->M % 8) return SVAE_EINVAL;

@@ -34,7 +34,7 @@ def gemm(A, B, C, M, N_, K, *, a_t=False, b_t=False, lda=None, ldb=None, ldc=Non
     d.batch, d.splits = batch, splits
     d.a_t, d.b_t = int(a_t), int(b_t)
     d.epi = epi
-    d.C = C.data_ptr()
+    d.C = ptr(C)          # None: CE statistics only (no logits stored)
     d.ldc = ldc if ldc is not None else N_
     d.batch_stride_c = sC
     d.bias = ptr(bias)

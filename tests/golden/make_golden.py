@@ -179,6 +179,112 @@ def sparse_vectors(sv):
     print('sparse: written')
 
 
+def _ref_model(sv, hp, seed, window=0, emb_scale=1.0):
+    rhp = sv.TransformerVAEHparams(d_model=hp.d_model, num_heads=hp.num_heads, num_layers=hp.num_layers,
+                                   latent_depth=64, sparse_self_attention=bool(window),
+                                   attn_window_size=window or 4, kl_weight=1.0, start_token=1, end_token=2)
+    torch.manual_seed(0)
+    model = sv.TransformerVAE(rhp)
+    params = init_params(hp, seed)
+    params['input_layer.0.weight'] = params['input_layer.0.weight'] * emb_scale
+    sd = dict(params)
+    for alias in TIED_ALIASES:
+        sd[alias] = params['input_layer.0.weight']
+    model.load_state_dict(sd, strict=True)
+    for m in model.modules():
+        if isinstance(m, torch.nn.Dropout):
+            m.p = 0.0
+    model.eval()
+    return model
+
+
+# name -> (d_model, num_heads, num_layers, window, B, max_length, repetition_penalty, seed)
+GEN_CONFIGS = {
+    'gen_dense': (128, 8, 4, 0, 3, 48, 1.2, 31),
+    'gen_dense_nopen': (128, 4, 4, 0, 2, 40, 1.0, 32),
+    'gen_sparse': (128, 2, 4, 2, 2, 150, 1.2, 33),      # window 2: the KV cache shifts from position 96 on
+}
+EMB_SCALE = 10.0   # peaked logits (tied head): greedy top-1/top-2 margins far above fp32 rounding
+
+
+def generation_vectors(sv):
+    """TransformerVAE.sample (transformer_vae.py:95-128) greedy (temperature 0) with the KV cache
+    (attention.py:107-168) and GenerationState (generation.py), dense and sliding-window. The end token is
+    chosen from a first run (a token row 0 emits from step 5 on and no other row emits) so that early
+    stopping is exercised while the other rows run to max_length (and through the sliding-window cache shift)."""
+    for name, (d, H, NL, window, B, T, pen, seed) in GEN_CONFIGS.items():
+        hp = HParams(d_model=d, num_heads=H, num_layers=NL, latent_depth=64, kl_weight=1.0, attn_window=window)
+        model = _ref_model(sv, hp, seed, window, EMB_SCALE)
+        z = torch.from_numpy(portable_normal(B * 64, 'z', seed).reshape(B, 1, 64).astype(np.float32))
+        with torch.no_grad():
+            first = model.sample(T, B, z=z.clone(), temperature=0.0, repetition_penalty=pen)
+            others = set(first[1:].flatten().tolist())
+            k = next(i for i in range(4, T - 1) if int(first[0, i]) not in others)
+            end = int(first[0, k])          # row 0 stops at step k + 1; every other row runs to max_length
+            model.end_token = end
+            out = model.sample(T, B, z=z.clone(), temperature=0.0, repetition_penalty=pen)
+        rec = {'cfg': np.asarray([d, H, NL, window, B, T, seed], dtype=np.int64), 'penalty': np.float64(pen),
+               'emb_scale': np.float64(EMB_SCALE), 'start_token': np.int64(1), 'end_token': np.int64(end),
+               'z': z.numpy(), 'tokens': out.numpy().astype(np.int32), 'first_run': first.numpy().astype(np.int32)}
+        np.savez_compressed(os.path.join(HERE, name + '.npz'), **rec)
+        print(f'{name}: end={end} tokens[0,:12]={out[0, :12].tolist()}')
+
+
+def iw_vectors(sv):
+    """TransformerVAE.test_step (transformer_vae.py:71-79) -> estimate_log_prob_iw (continuous_autoencoder.py:
+    62-80) with the rsample draws injected, for chunk size 1 (num_iter = num_samples, the reference's own
+    100/100 setting) and chunk size = B (the reference's [chunk, B, 1] + [chunk, B] broadcasting)."""
+    d, H, NL, L, B, seed = 128, 8, 4, 96, 3, 41
+    hp = HParams(d_model=d, num_heads=H, num_layers=NL, latent_depth=64, kl_weight=1.0)
+    model = _ref_model(sv, hp, seed)
+    ids, lens = make_batch(B, L, True, seed + 1)
+    PaddedTensor = sys.modules['sparse_vae.core.padded_tensor'].PaddedTensor
+    from torch.distributions import Normal
+    rec = {'ids': ids.astype(np.int32), 'lens': lens, 'cfg': np.asarray([d, H, NL, L, B, seed], dtype=np.int64)}
+    for tag, S, n_iter in (('c1', 100, 100), ('cB', 6, 2)):
+        eps = torch.from_numpy(portable_normal(S * B * 64, 'eps_iw_' + tag, seed).reshape(S, B, 1, 64)
+                               .astype(np.float32))
+        state = {'i': 0}
+
+        def rsample(self, sample_shape=torch.Size()):
+            c = int(sample_shape[0])
+            e = eps[state['i']:state['i'] + c]
+            state['i'] += c
+            return self.loc + e * self.scale
+
+        Normal.rsample = rsample
+        batch = {'token_ids': PaddedTensor.from_raw(torch.from_numpy(ids.astype(np.int16))),
+                 'num_tokens': torch.from_numpy(lens), 'num_bytes': torch.from_numpy(lens)}
+        with torch.no_grad():
+            if tag == 'c1':      # the reference's test_step: num_samples = num_iter = 100 (chunk 1)
+                orig = type(model).estimate_log_prob_iw
+                captured = {}
+
+                def spy(self, *a, **k):
+                    r = orig(self, *a, **k)
+                    captured['log_prob'] = r.clone()
+                    return r
+
+                type(model).estimate_log_prob_iw = spy
+                try:
+                    nll_iw = model.test_step(batch, 0)
+                finally:
+                    type(model).estimate_log_prob_iw = orig
+                log_prob = captured['log_prob']
+                rec['nll_iw'] = np.float64(nll_iw.item())
+            else:                # chunk = B: called directly (test_step hard-codes 100/100)
+                original = batch['token_ids'].long()
+                x = model.input_layer(original)
+                posterior = model.q_of_z_given_x(model.encoder(x))
+                log_prob = model.estimate_log_prob_iw(posterior, x, original, num_samples=S, num_iter=n_iter)
+        assert state['i'] == S
+        rec[f'eps_{tag}'] = eps.numpy()
+        rec[f'num_iter_{tag}'] = np.int64(n_iter)
+        rec[f'log_prob_{tag}'] = log_prob.numpy()
+        print(f'iw {tag}: log_prob shape={tuple(log_prob.shape)} mean={log_prob.mean().item():.4f}')
+    np.savez_compressed(os.path.join(HERE, 'iw.npz'), **rec)
+
+
 def main():
     torch.set_num_threads(min(8, os.cpu_count()))
     sv = ref_stubs.import_reference()
@@ -186,6 +292,10 @@ def main():
     only = sys.argv[1:]
     if only == ['sparse']:
         sparse_vectors(sv)
+        return
+    if only == ['eval']:
+        generation_vectors(sv)
+        iw_vectors(sv)
         return
     for name, cfg in CONFIGS.items():
         if only and name not in only:

@@ -22,3 +22,26 @@ def setup(name):
     params = init_params(hp, seed)
     ids = torch.from_numpy(g['ids'].astype(np.int64))
     return g, hp, params, ids
+
+
+GEN_NAMES = ['gen_dense', 'gen_dense_nopen', 'gen_sparse']
+
+
+def setup_gen(name):
+    """A generation fixture (make_golden.generation_vectors): hparams, weights (tied embedding scaled by
+    emb_scale for peaked logits) and the latent z [B, 1, 64]."""
+    g = load(name)
+    d, H, NL, window, B, T, seed = [int(v) for v in g['cfg']]
+    hp = HParams(d_model=d, num_heads=H, num_layers=NL, latent_depth=64, kl_weight=1.0, attn_window=window)
+    params = init_params(hp, seed)
+    params['input_layer.0.weight'] = params['input_layer.0.weight'] * float(g['emb_scale'])
+    return g, hp, params, torch.from_numpy(g['z'])
+
+
+def setup_iw():
+    g = load('iw')
+    d, H, NL, L, B, seed = [int(v) for v in g['cfg']]
+    hp = HParams(d_model=d, num_heads=H, num_layers=NL, latent_depth=64, kl_weight=1.0)
+    params = init_params(hp, seed)
+    ids = torch.from_numpy(g['ids'].astype(np.int64))
+    return g, hp, params, ids
