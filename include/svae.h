@@ -210,6 +210,46 @@ int svae_attn_fwd_f32(const float* q, const float* k, const float* v, float* o, 
 int svae_layernorm_fwd_f32(const float* x, const float* w, const float* b, float* y, int32_t rows, int32_t D,
                            svae_stream_t stream);
 
+/* ---- evaluation: log p(x|z) per sequence (continuous_autoencoder.py:82-88) ---------------------------
+ * From the SVAE_EPI_CE_STATS partials of the head GEMM (which may run with C = NULL: no logits stored):
+ * out[s] = sum over the rows r of sequence s (rows s*seq .. s*seq+seq-1) with labels[r] != 0 of
+ * (label_logit[r] - logsumexp_r); labels 0 add 0 (the reference zeroes log_softmax column 0). */
+int svae_ce_seq_logprob(const float* part, int32_t ntile, const float* label_logit, const int32_t* labels,
+                        int32_t rows, int32_t seq, float* out, svae_stream_t stream);
+
+/* ---- autoregressive decoding (TransformerVAE.sample, transformer_vae.py:95-128; the KV cache of
+ * attention.py:107-168; GenerationState, generation.py). All f32. `cur` is a device int32 holding
+ * GenerationState.current_index: kernels read it at run time, so a captured step graph replays for every
+ * position. out_ids: int64 [B][T] (GenerationState.output_ids); live: uint8 [B].
+ * dec_linear: Y[M,N] = epi(X[M,K] . W[N,K]^T + bias) + resid; epi SVAE_EPI_F32 / SVAE_EPI_GELU /
+ *   SVAE_EPI_ROTARY_BF16 (rotary of rot_tab row cur-1 on columns < rot_cols, pairs within rot_d; f32 out).
+ *   K % 4 == 0, X and W 16-byte aligned.
+ * dec_attn: qkv f32 [B][ldq] = q | k | v (rotary applied); appends k, v at position cur-1 to the caches
+ *   [B][H][T][hd] and writes O[b][h*hd ..] = softmax(q k^T * scale) v over the visible keys: 0..cur-1, or with
+ *   window > 0 the sliding-window cache's set ([CLS] block, window-1 previous 32-blocks, current block).
+ * dec_embed: x[b] = table[out_ids[b][cur-1]].
+ * dec_penalty: repetition penalty on logits rows (row r is sequence row_map[r], or r): the ids
+ *   out_ids[b][max(cur-512,0) .. cur-1] get logit * penalty if < 0 else logit / penalty (generation.py:35-41).
+ * dec_sample: per live row: greedy (temperature <= 0 or top_k == 1) or temperature / top-k / nucleus top-p +
+ *   multinomial from (seed, cur, b); writes out_ids[b][cur]; clears live[b] (and decrements *live_count)
+ *   when the token is end_token or cur + 1 >= T (generation.py:43-77). V <= 32768.
+ * dec_advance: *cur += 1. */
+int svae_dec_linear(const float* X, int64_t ldx, const float* W, int64_t ldw, const float* bias, float* Y, int64_t ldy,
+                    const float* resid, int64_t ldr, int32_t M, int32_t N, int32_t K, int32_t epi, const float* rot_tab,
+                    int32_t rot_cols, int32_t rot_d, const int32_t* cur, svae_stream_t stream);
+int svae_dec_attn(const float* qkv, int64_t ldq, float* kcache, float* vcache, int32_t B, int32_t H, int32_t hd,
+                  int32_t T, const int32_t* cur, int32_t window, float scale, float* O, int64_t ldo,
+                  svae_stream_t stream);
+int svae_dec_embed(const int64_t* out_ids, int32_t T, const int32_t* cur, const float* table, float* x, int32_t B,
+                   int32_t D, svae_stream_t stream);
+int svae_dec_penalty(float* logits, int64_t ldl, int32_t rows, const int32_t* row_map, const int64_t* out_ids,
+                     int32_t T, const int32_t* cur, const uint8_t* live, float penalty, svae_stream_t stream);
+int svae_dec_sample(const float* logits, int64_t ldl, int32_t V, int32_t rows, const int32_t* row_map,
+                    int64_t* out_ids, int32_t T, const int32_t* cur, uint8_t* live, int32_t end_token,
+                    float temperature, int32_t top_k, float top_p, uint64_t seed, int32_t* live_count,
+                    svae_stream_t stream);
+int svae_dec_advance(int32_t* cur, svae_stream_t stream);
+
 /* library identification: returns a static string (build id, target arch). */
 const char* svae_version(void);
 

@@ -122,6 +122,36 @@ __global__ __launch_bounds__(256) void ce_rows_kernel(const float* __restrict__ 
   }
 }
 
+// log p(x|z) summed over each sequence (continuous_autoencoder.py:82-88): one block of 4 waves per sequence;
+// a wave finalises one row's logsumexp from the per-tile partials at a time. Label 0 rows add 0.
+__global__ __launch_bounds__(256) void ce_seq_logprob_kernel(const float* __restrict__ part, int ntile,
+                                                             const float* __restrict__ label_logit,
+                                                             const int* __restrict__ labels, int seq,
+                                                             float* __restrict__ out) {
+  __shared__ float ws[4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const long long r0 = (long long)blockIdx.x * seq;
+  float acc = 0.f;
+  for (int i = w; i < seq; i += 4) {
+    const long long row = r0 + i;
+    if (labels[row] == 0) continue;                 // wave-uniform
+    const float2* pr = (const float2*)part + row * ntile;
+    float mx = -INFINITY;
+    for (int t = lane; t < ntile; t += 64) mx = fmaxf(mx, pr[t].x);
+    mx = wave_max(mx);
+    float se = 0.f;
+    for (int t = lane; t < ntile; t += 64) {
+      const float2 v = pr[t];
+      se += (v.x == -INFINITY) ? 0.f : v.y * __expf(v.x - mx);
+    }
+    se = wave_sum(se);
+    acc += label_logit[row] - (mx + __logf(se));
+  }
+  if (lane == 0) ws[w] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) out[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
+}
+
 // Chunked mean-of-means (robust_cross_entropy): single block; writes nll and per-chunk row weights.
 __global__ __launch_bounds__(1024) void ce_reduce_kernel(const float* __restrict__ row_loss, const int* __restrict__ labels,
                                                          int rows, int seq, int nchunks, int chunk_len,
@@ -434,6 +464,15 @@ SVAE_EXPORT int svae_ce_finalize(const float* part, int32_t ntile, const float* 
                      row_loss);
   hipLaunchKernelGGL(ce_reduce_kernel, dim3(1), dim3(1024), 0, s, row_loss, labels, rows, seq, nchunks, chunk_len,
                      chunk_w, nll_out);
+  SVAE_LAUNCH_CHECK();
+  return SVAE_OK;
+}
+
+SVAE_EXPORT int svae_ce_seq_logprob(const float* part, int32_t ntile, const float* label_logit, const int32_t* labels,
+                                    int32_t rows, int32_t seq, float* out, svae_stream_t stream) {
+  if (!part || !label_logit || !labels || !out || rows <= 0 || ntile <= 0 || seq <= 0 || rows % seq) return SVAE_EINVAL;
+  hipLaunchKernelGGL(ce_seq_logprob_kernel, dim3(rows / seq), dim3(256), 0, (hipStream_t)stream, part, ntile,
+                     label_logit, labels, seq, out);
   SVAE_LAUNCH_CHECK();
   return SVAE_OK;
 }

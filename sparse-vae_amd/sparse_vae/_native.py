@@ -93,6 +93,17 @@ _SIGS = {
                           c_int64, c_int64, c_void_p, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32,
                           c_float, c_void_p],
     'svae_layernorm_fwd_f32': [c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p],
+    'svae_ce_seq_logprob': [c_void_p, c_int32, c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_void_p],
+    'svae_dec_linear': [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_int32,
+                        c_int32, c_int32, c_int32, c_void_p, c_int32, c_int32, c_void_p, c_void_p],
+    'svae_dec_attn': [c_void_p, c_int64, c_void_p, c_void_p, c_int32, c_int32, c_int32, c_int32, c_void_p, c_int32,
+                      c_float, c_void_p, c_int64, c_void_p],
+    'svae_dec_embed': [c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p],
+    'svae_dec_penalty': [c_void_p, c_int64, c_int32, c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_float,
+                         c_void_p],
+    'svae_dec_sample': [c_void_p, c_int64, c_int32, c_int32, c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_int32,
+                        c_float, c_int32, c_float, c_uint64, c_void_p, c_void_p],
+    'svae_dec_advance': [c_void_p, c_void_p],
     'svae_version': [],
 }
 

@@ -452,26 +452,10 @@ class VAEEngine:
         x_emb = ws.get('x_emb', (T, d), f32)
         K.embedding_fwd(ids32, P.f('input_layer.0.weight'), x_emb, T, d)
 
-        # ---- encoder (perceiver.py:39-50)
-        lay = []
-        z, st = self.layer_fwd('encoder.first_layer.', x_emb, B, L, L, padm, learned=N, heads=self.He, hd=64,
-                               drop_p=dropout, seed=_mix_seed(seed, 1000), tag='e0')
-        lay.append(st)
-        for j in range(hp.enc_layers - 2):
-            z, st = self.layer_fwd(f'encoder.middle_layers.{j}.', z, B, N, L, padm, cross=True, ctx=x_emb,
-                                   heads=self.He, hd=64, drop_p=dropout, seed=_mix_seed(seed, 1001 + j), tag=f'e{j + 1}')
-            lay.append(st)
-        enc, st = self.layer_fwd('encoder.bottleneck.', z, B, N, L, padm, learned=1, heads=self.He, hd=64,
-                                 drop_p=dropout, seed=_mix_seed(seed, 1999), tag='eb')
-        lay.append(st)
-        sv['enc_layers'] = lay
+        # ---- encoder (perceiver.py:39-50) + q(z|x) (conditional_gaussian.py:18)
+        enc_bf, stats, sv['enc_layers'] = self._encode(x_emb, B, L, padm, dropout, seed)
 
-        # ---- q(z|x) + reparameterise + KL (conditional_gaussian.py:18-28, continuous_autoencoder.py:42-52)
-        enc_bf = ws.get('enc_bf', (B, d))
-        K.cast_bf16(enc, enc_bf)
-        stats = ws.get('stats', (B, 2 * Z), f32)
-        K.gemm(enc_bf, P.w('q_of_z_given_x.linear.weight'), stats, B, 2 * Z, d, epi=EPI_F32,
-               bias=P.f('q_of_z_given_x.linear.bias'))
+        # ---- reparameterise + KL (conditional_gaussian.py:18-28, continuous_autoencoder.py:42-52)
         zf = ws.get('z', (B, Z), f32)
         zb = ws.get('z_bf', (B, Z))
         eps_buf = ws.get('eps', (B, Z), f32)
@@ -524,6 +508,114 @@ class VAEEngine:
         return {'loss': loss, 'nll': nll[0], 'kl': kl[0], 'train_kl': kl[1], 'raw_kl': raw_kl,
                 'mu': stats[:, :Z], 'logvar': stats[:, Z:], 'z': zf, 'eps': eps_buf,
                 'logits': logits if need_logits else None}
+
+    def _encode(self, x_emb, B, L, padm, dropout, seed):
+        """Perceiver.forward (perceiver.py:39-50) then the q(z|x) linear (conditional_gaussian.py:18): returns
+        the bf16 bottleneck [B, d], stats f32 [B, 2Z] = mu | logvar, and the layers' saved state."""
+        hp, d, ws, P = self.hp, self.d, self.ws, self.P
+        N, Z = hp.num_latents, hp.latent_depth
+        lay = []
+        z, st = self.layer_fwd('encoder.first_layer.', x_emb, B, L, L, padm, learned=N, heads=self.He, hd=64,
+                               drop_p=dropout, seed=_mix_seed(seed, 1000), tag='e0')
+        lay.append(st)
+        for j in range(hp.enc_layers - 2):
+            z, st = self.layer_fwd(f'encoder.middle_layers.{j}.', z, B, N, L, padm, cross=True, ctx=x_emb,
+                                   heads=self.He, hd=64, drop_p=dropout, seed=_mix_seed(seed, 1001 + j), tag=f'e{j + 1}')
+            lay.append(st)
+        enc, st = self.layer_fwd('encoder.bottleneck.', z, B, N, L, padm, learned=1, heads=self.He, hd=64,
+                                 drop_p=dropout, seed=_mix_seed(seed, 1999), tag='eb')
+        lay.append(st)
+        enc_bf = ws.get('enc_bf', (B, d))
+        K.cast_bf16(enc, enc_bf)
+        stats = ws.get('stats', (B, 2 * Z), f32)
+        K.gemm(enc_bf, P.w('q_of_z_given_x.linear.weight'), stats, B, 2 * Z, d, epi=EPI_F32,
+               bias=P.f('q_of_z_given_x.linear.bias'))
+        return enc_bf, stats, lay
+
+    def _inputs(self, ids, pad):
+        """ids [B, L] -> (int32 ids, uint8 key-padding mask or None) in the workspace."""
+        B, L = ids.shape
+        ids32 = self.ws.get('ids', (B, L), torch.int32)
+        ids32.copy_(ids)
+        padm = None
+        if pad is not None and pad is not False:
+            padm = self.ws.get('pad', (B, L), torch.uint8)
+            padm.copy_(ids.eq(0) if pad is True else pad)
+        return ids32, padm
+
+    def posterior(self, ids, pad=True):
+        """q(z|x) without the decoder (transformer_vae.py:73-74, :81-83): stats f32 [B, 2Z] = mu | logvar."""
+        if not ids.is_cuda:
+            raise RuntimeError('VAEEngine needs device tensors (no CPU fallback)')
+        self.P.sync_shadow()
+        B, L = ids.shape
+        ids32, padm = self._inputs(ids, pad)
+        x_emb = self.ws.get('x_emb', (B * L, self.d), f32)
+        K.embedding_fwd(ids32, self.P.f('input_layer.0.weight'), x_emb, B * L, self.d)
+        _, stats, _ = self._encode(x_emb, B, L, padm, 0.0, 0)
+        return stats
+
+    def seq_log_prob(self, x_emb, labels, z, pad=None, max_tokens=32768):
+        """log p(x|z) summed over each sequence (continuous_autoencoder.py:82-88). x_emb f32 [G, B, L, d] (the
+        embedded input; any strides — the IW estimate passes the batch expanded over G samples, copied one
+        sub-batch at a time, never materialised), labels int [G, B, L-1] (label 0 adds 0), z f32 [G, B, Z],
+        pad [G, B, L] bool key-padding mask or None. Returns f32 [G, B]. Sub-batches hold <= max_tokens tokens
+        (whole groups when B * L fits); the vocabulary GEMM keeps only its CE statistics."""
+        hp, d, ws, P = self.hp, self.d, self.ws, self.P
+        if not x_emb.is_cuda:
+            raise RuntimeError('VAEEngine needs device tensors (no CPU fallback)')
+        P.sync_shadow()
+        G, Bt, L = x_emb.shape[0], x_emb.shape[1], x_emb.shape[2]
+        V, Z = hp.vocab_size, hp.latent_depth
+        out = torch.empty(G, Bt, dtype=f32, device=P.device)
+        ntile = -(-V // 128)
+        if Bt * L <= max_tokens:
+            gstep, bstep = max(1, max_tokens // (Bt * L)), Bt
+        else:
+            gstep, bstep = 1, max(1, max_tokens // L)
+        for g0 in range(0, G, gstep):
+            g1 = min(G, g0 + gstep)
+            for b0 in range(0, Bt, bstep):
+                b1 = min(Bt, b0 + bstep)
+                ng, nb = g1 - g0, b1 - b0
+                B = ng * nb
+                T = B * L
+                padm = None
+                if pad is not None:
+                    padm = ws.get('pad', (B, L), torch.uint8)
+                    padm.view(ng, nb, L).copy_(pad[g0:g1, b0:b1])
+                lab = ws.get('labels', (B, L), torch.int32)
+                lab.view(ng, nb, L)[:, :, :-1].copy_(labels[g0:g1, b0:b1])
+                lab[:, -1] = 0
+                xe = ws.get('x_emb', (T, d), f32)
+                xe.view(ng, nb, L, d).copy_(x_emb[g0:g1, b0:b1])
+                zf = ws.get('z_f32', (B, Z), f32)
+                zf.view(ng, nb, Z).copy_(z[g0:g1, b0:b1])
+                zb = ws.get('z_bf', (B, Z))
+                K.cast_bf16(zf, zb)
+                xs, _ = self._decode(xe, zb, padm, B, L, 0.0, 0)
+                hh = self._head_hidden(xs, T)
+                part = ws.get('ce.part', (T, ntile, 2), f32)
+                lab_logit = ws.get('ce.label_logit', (T,), f32)
+                K.gemm(hh, P.w('input_layer.0.weight'), None, T, V, d, epi=EPI_CE_STATS,
+                       bias=P.f('output_layer.3.bias'), aux=part, labels=lab, label_logit=lab_logit)
+                res = ws.get('seq_lp', (B,), f32)
+                K.ce_seq_logprob(part, ntile, lab_logit, lab, T, L, res)
+                out[g0:g1, b0:b1].copy_(res.view(ng, nb))
+        return out
+
+    def _head_hidden(self, xs, T):
+        """output_layer[:3] (transformer_language_model.py:55-61): LayerNorm(GELU(Linear(x))) as the bf16
+        operand of the tied vocabulary GEMM."""
+        d, ws, P = self.d, self.ws, self.P
+        xf = ws.get('xf_bf', (T, d))
+        K.cast_bf16(xs, xf)
+        gp0 = ws.get('h0_gprime', (T, d))
+        h0 = ws.get('h0', (T, d))
+        K.gemm(xf, P.w('output_layer.0.weight'), h0, T, d, d, epi=EPI_GELU, bias=P.f('output_layer.0.bias'),
+               aux=gp0, ldaux=d)
+        hh, _ = self._ln_fwd('output_layer.2', h0, T, 'head.ln')
+        return hh
 
     def _decode(self, x_emb, zb, padm, B, L, dropout, seed):
         hp, d, ws, P = self.hp, self.d, self.ws, self.P

@@ -183,6 +183,13 @@ def ce_finalize(part, ntile, label_logit, labels, rows, seq, nchunks, chunk_len,
                                nll.data_ptr(), stream()), 'svae_ce_finalize')
 
 
+def ce_seq_logprob(part, ntile, label_logit, labels, rows, seq, out):
+    _dev(part, label_logit, labels, out)
+    assert out.dtype == f32 and out.numel() == rows // seq and out.is_contiguous()
+    check(lib.svae_ce_seq_logprob(part.data_ptr(), ntile, label_logit.data_ptr(), labels.data_ptr(), rows, seq,
+                                  out.data_ptr(), stream()), 'svae_ce_seq_logprob')
+
+
 def ce_grad(logits, ld, lse, chunk_w, labels, gscale, rows, V, seq, nchunks, chunk_len, dbias=None):
     check(lib.svae_ce_grad(logits.data_ptr(), ld, lse.data_ptr(), chunk_w.data_ptr(), labels.data_ptr(),
                            gscale.data_ptr(), ptr(dbias), rows, V, seq, nchunks, chunk_len, stream()), 'svae_ce_grad')
@@ -239,3 +246,42 @@ def attention_f32(q, k, v, o, *, B, H, Lq, Lk, hd, sq, sk, sv, so, bq, bk, bv, b
 def layernorm_fwd_f32(x, w, b, y, rows, D):
     check(lib.svae_layernorm_fwd_f32(x.data_ptr(), w.data_ptr(), b.data_ptr(), y.data_ptr(), rows, D, stream()),
           'svae_layernorm_fwd_f32')
+
+
+# ---- autoregressive decoding (f32; positions from the device scalar `cur`)
+def dec_linear(X, W, Y, M, N_, K_, *, bias=None, resid=None, epi=N.EPI_F32, rot=None, rot_cols=0, rot_d=0, cur=None,
+               ldx=None, ldw=None, ldy=None, ldr=None):
+    _dev(X, W, Y)
+    assert X.dtype == f32 and W.dtype == f32 and Y.dtype == f32
+    check(lib.svae_dec_linear(X.data_ptr(), ldx or K_, W.data_ptr(), ldw or K_, ptr(bias), Y.data_ptr(), ldy or N_,
+                              ptr(resid), ldr or N_, M, N_, K_, epi, ptr(rot), rot_cols, rot_d, ptr(cur), stream()),
+          'svae_dec_linear')
+
+
+def dec_attn(qkv, kc, vc, O, B, H, hd, T, cur, window, scale=None, ldq=None, ldo=None):
+    _dev(qkv, kc, vc, O, cur)
+    check(lib.svae_dec_attn(qkv.data_ptr(), ldq or 3 * H * hd, kc.data_ptr(), vc.data_ptr(), B, H, hd, T,
+                            cur.data_ptr(), window, hd ** -0.5 if scale is None else scale, O.data_ptr(),
+                            ldo or H * hd, stream()), 'svae_dec_attn')
+
+
+def dec_embed(out_ids, T, cur, table, x, B, D):
+    assert out_ids.dtype == torch.int64
+    check(lib.svae_dec_embed(out_ids.data_ptr(), T, cur.data_ptr(), table.data_ptr(), x.data_ptr(), B, D, stream()),
+          'svae_dec_embed')
+
+
+def dec_penalty(logits, rows, row_map, out_ids, T, cur, live, penalty):
+    check(lib.svae_dec_penalty(logits.data_ptr(), logits.stride(0), rows, ptr(row_map), out_ids.data_ptr(), T,
+                               cur.data_ptr(), ptr(live), penalty, stream()), 'svae_dec_penalty')
+
+
+def dec_sample(logits, V, rows, row_map, out_ids, T, cur, live, end_token, temperature, top_k, top_p, seed,
+               live_count=None):
+    check(lib.svae_dec_sample(logits.data_ptr(), logits.stride(0), V, rows, ptr(row_map), out_ids.data_ptr(), T,
+                              cur.data_ptr(), ptr(live), end_token, temperature, top_k, top_p,
+                              seed & 0xFFFFFFFFFFFFFFFF, ptr(live_count), stream()), 'svae_dec_sample')
+
+
+def dec_advance(cur):
+    check(lib.svae_dec_advance(cur.data_ptr(), stream()), 'svae_dec_advance')

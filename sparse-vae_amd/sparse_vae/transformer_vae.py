@@ -21,6 +21,8 @@ from .core import (ContinuousVAEHparams, ContinuousVAEHooks, ConditionalGaussian
                    TransformerHparams, TransformerLayer, VOCAB_SIZE, marginal_kl)
 from .core.padded_tensor import PaddedTensor
 from .engine import FlatParams, VAEEngine
+from .core.generation import GenerationState
+from .decoding import KVDecoder
 from . import kernels as K
 from ._native import EPI_F32, EPI_BF16
 
@@ -284,6 +286,62 @@ class TransformerVAE(ContinuousVAEHooks, LanguageModel):
         if precision == 'fp32':
             return eng.reconstruct_f32(x, z, pad)
         return eng.reconstruct(x, z, pad)
+
+    @torch.no_grad()
+    def p_of_x_given_z(self, x, z, labels, padding=None):
+        """continuous_autoencoder.py:82-88: log p(x|z) summed over the sequence, for x = input_layer(ids)
+        [..., L, d] (a PaddedTensor or plain; `padding` overrides its mask), z [..., 1, latent], labels
+        [..., L-1]. Returns [...]. Decoder + vocabulary head run in the HIP kernels; the head keeps only its CE
+        statistics (the [.., L, V] logits are never stored)."""
+        eng = self._require_engine()
+        pad = padding if padding is not None else getattr(x, 'padding', None)
+        x = x.as_raw() if isinstance(x, PaddedTensor) else x
+        lead, L, d = x.shape[:-2], x.shape[-2], x.shape[-1]
+        Z = z.shape[-1]
+        if len(lead) == 1:
+            x4, z3, l3 = x.unsqueeze(0), z.reshape(1, lead[0], Z), labels.reshape(1, lead[0], L - 1)
+        else:
+            G = 1
+            for n in lead[:-1]:
+                G *= n
+            # merge the leading dims without materialising an expanded x (view when possible)
+            x4 = x.reshape(G, lead[-1], L, d) if x.is_contiguous() else x.flatten(0, len(lead) - 2)
+            z3, l3 = z.reshape(G, lead[-1], Z), labels.reshape(G, lead[-1], L - 1)
+        p3 = pad.expand(*lead, L).reshape(x4.shape[0], x4.shape[1], L) if pad is not None else None
+        return eng.seq_log_prob(x4, l3, z3.float(), p3).reshape(lead)
+
+    @torch.no_grad()
+    def test_step(self, batch: Dict[str, Any], batch_index: int = 0):
+        """transformer_vae.py:71-79: importance-weighted NLL with 100 posterior samples (100 chunks of 1)."""
+        eng = self._require_engine()
+        ids, pad, ntok = self._batch_inputs(batch)
+        Z = self.hparams.latent_depth
+        stats = eng.posterior(ids, pad if pad is not None else False)
+        mu = stats[:, :Z].reshape(-1, 1, Z).clone()
+        posterior = Normal(mu, stats[:, Z:].exp().sqrt().reshape(-1, 1, Z))
+        x = self.embed(PaddedTensor.from_raw(ids, pad) if pad is not None else ids)
+        log_prob = self.estimate_log_prob_iw(posterior, x, ids.long(), num_samples=100, num_iter=100) / ntok
+        nll_iw = -log_prob.mean()
+        self.log('nll_iw', nll_iw, on_step=True)
+        return nll_iw
+
+    @torch.no_grad()
+    def sample(self, max_length: int, batch_size: int = 1, **kwargs):
+        """transformer_vae.py:95-128: autoregressive decoding with a KV cache (f32 kernels, one HIP graph per
+        step). kwargs: z [B, 1, latent] (default N(0, I)), and GenerationState's top_k / top_p / temperature /
+        repetition_penalty; use_graph=False steps eagerly. Returns output_ids[:, 1:] (None below kl_weight 1,
+        as in the reference)."""
+        if self.hparams.kl_weight < 1.0:
+            return None
+        eng = self._require_engine()
+        z = kwargs.pop('z', None)
+        use_graph = kwargs.pop('use_graph', True)
+        if z is None:
+            z = torch.randn(batch_size, 1, self.hparams.latent_depth, device=self.device)
+        start = self.start_token if self.start_token is not None else 1      # [CLS] (text_data_module.py:271)
+        end = self.end_token if self.end_token is not None else 2            # [SEP]
+        state = GenerationState(max_length, batch_size, start, end, device=self.device, **kwargs)
+        return KVDecoder(eng, state, z.to(self.device), use_graph=use_graph).run()
 
     @torch.no_grad()
     def embed(self, ids):
