@@ -6,7 +6,7 @@
 // captured step graph (hipGraph via torch.cuda.CUDAGraph) replays for every position.
 //
 //   svae_dec_linear:  Y[M,N] = epi(X[M,K] . W[N,K]^T + b) (+ resid): weight-streaming skinny GEMM on
-//                     v_mfma_f32_16x16x4_f32, 16 output columns per workgroup, K split over its 4 waves and
+//                     v_mfma_f32_16x16x4_f32, 16 output columns per workgroup, K split over its 16 waves and
 //                     reduced through LDS; epilogues plain / GELU / rotary at position cur-1.
 //   svae_dec_attn:    one workgroup per (sequence, head): appends k, v at position cur-1 to the cache
 //                     [B][H][T][hd] and attends over the visible keys (dense causal, or the sliding-window
@@ -24,41 +24,54 @@ using namespace svae;
 namespace {
 
 // ------------------------------------------------------------------ skinny f32 linear
+// 16 output columns x up to 64 rows per workgroup of 16 waves; the waves split K (memory-level parallelism for
+// the weight stream: a d x d weight is only N / 16 workgroups wide) and their partials meet in LDS.
 constexpr int DL_MROWS = 64;   // rows per workgroup (4 MFMA m-tiles)
+constexpr int DL_WAVES = 16;
 
 template <int EPI>
-__global__ __launch_bounds__(256) void dec_linear_kernel(const float* __restrict__ X, long long ldx,
-                                                         const float* __restrict__ W, long long ldw,
-                                                         const float* __restrict__ bias, float* __restrict__ Y,
-                                                         long long ldy, const float* __restrict__ resid, long long ldr,
-                                                         int M, int N, int K, const float* __restrict__ rot,
-                                                         int rot_cols, int rot_d, const int* __restrict__ cur) {
-  __shared__ float red[4][DL_MROWS][17];
+__global__ __launch_bounds__(1024) void dec_linear_kernel(const float* __restrict__ X, long long ldx,
+                                                          const float* __restrict__ W, long long ldw,
+                                                          const float* __restrict__ bias, float* __restrict__ Y,
+                                                          long long ldy, const float* __restrict__ resid, long long ldr,
+                                                          int M, int N, int K, const float* __restrict__ rot,
+                                                          int rot_cols, int rot_d, const int* __restrict__ cur) {
+  __shared__ float red[DL_WAVES][DL_MROWS][17];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 15, g = lane >> 4;
   const int n0 = blockIdx.x * 16, m0 = blockIdx.y * DL_MROWS;
   const int mrows = min(DL_MROWS, M - m0);
   const int mt = (mrows + 15) >> 4;
   // this wave's K range: a multiple of 16 (one float4 per lane per step)
-  const int kq = ((K + 63) / 64) * 16;
+  const int kq = ((K + 16 * DL_WAVES - 1) / (16 * DL_WAVES)) * 16;
   const int kb = wave * kq, ke = min(K, kb + kq);
   f32x4 acc[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) acc[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
   const int n = n0 + r;
   const float* wrow = W + (long long)min(n, N - 1) * ldw;
-  for (int k = kb; k < ke; k += 16) {
-    const int kk = k + 4 * g;
-    const bool kin = kk < ke;                       // K % 4 == 0: a float4 is all in or all out
-    const f32x4 w4 = (kin && n < N) ? *(const f32x4*)(wrow + kk) : (f32x4){0.f, 0.f, 0.f, 0.f};
+  const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+  for (int k = kb; k < ke; k += 32) {     // two K-steps per iteration: all loads issued before the MFMAs
+    const int kk0 = k + 4 * g, kk1 = kk0 + 16;
+    const bool in0 = kk0 < ke && n < N, in1 = kk1 < ke && n < N;
+    const f32x4 w0 = in0 ? *(const f32x4*)(wrow + kk0) : zero;
+    const f32x4 w1 = in1 ? *(const f32x4*)(wrow + kk1) : zero;
+    f32x4 x0[4], x1[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = i * 16 + r;
+      const bool mok = i < mt && m < mrows;
+      const float* xr = X + (long long)(m0 + (mok ? m : 0)) * ldx;
+      x0[i] = (mok && kk0 < ke) ? *(const f32x4*)(xr + kk0) : zero;
+      x1[i] = (mok && kk1 < ke) ? *(const f32x4*)(xr + kk1) : zero;
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       if (i < mt) {
-        const int m = i * 16 + r;
-        const f32x4 x4 = (kin && m < mrows) ? *(const f32x4*)(X + (long long)(m0 + m) * ldx + kk)
-                                            : (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int e = 0; e < 4; ++e) acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(x4[e], w4[e], acc[i], 0, 0, 0);
+        for (int e = 0; e < 4; ++e) acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(x0[i][e], w0[e], acc[i], 0, 0, 0);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(x1[i][e], w1[e], acc[i], 0, 0, 0);
       }
     }
   }
@@ -69,38 +82,40 @@ __global__ __launch_bounds__(256) void dec_linear_kernel(const float* __restrict
 #pragma unroll
       for (int e = 0; e < 4; ++e) red[wave][i * 16 + 4 * g + e][r] = acc[i][e];
   __syncthreads();
-  // epilogue: thread = (row, column pair); 64 rows x 8 pairs = 512 -> 2 per thread
+  // epilogue: thread = (row, column pair); 64 rows x 8 pairs = 512 threads
   const int p = cur ? *cur - 1 : 0;   // decode position (rotary)
+  if (tid >= DL_MROWS * 8) return;
+  const int row = tid >> 3, c = (tid & 7) * 2;
+  if (row >= mrows) return;
+  const int m = m0 + row, nn = n0 + c;
+  if (nn >= N) return;
+  float x0 = 0.f, x1 = 0.f;
 #pragma unroll
-  for (int it = 0; it < 2; ++it) {
-    const int e = tid + 256 * it, row = e >> 3, c = (e & 7) * 2;
-    if (row >= mrows) continue;
-    const int m = m0 + row, nn = n0 + c;
-    if (nn >= N) continue;
-    float x0 = red[0][row][c] + red[1][row][c] + red[2][row][c] + red[3][row][c];
-    float x1 = red[0][row][c + 1] + red[1][row][c + 1] + red[2][row][c + 1] + red[3][row][c + 1];
-    if (bias) {
-      x0 += bias[nn];
-      if (nn + 1 < N) x1 += bias[nn + 1];
-    }
-    if constexpr (EPI == SVAE_EPI_GELU) {
-      x0 = gelu_f(x0);
-      x1 = gelu_f(x1);
-    } else if constexpr (EPI == SVAE_EPI_ROTARY_BF16) {
-      if (nn < rot_cols) {
-        const float2 cs = ((const float2*)rot)[(long long)p * (rot_d / 2) + (nn % rot_d) / 2];
-        const float a = x0, b = x1;
-        x0 = a * cs.x + (-b) * cs.y;
-        x1 = b * cs.x + a * cs.y;
-      }
-    }
-    if (resid) {
-      x0 += resid[(long long)m * ldr + nn];
-      if (nn + 1 < N) x1 += resid[(long long)m * ldr + nn + 1];
-    }
-    Y[(long long)m * ldy + nn] = x0;
-    if (nn + 1 < N) Y[(long long)m * ldy + nn + 1] = x1;
+  for (int w = 0; w < DL_WAVES; ++w) {
+    x0 += red[w][row][c];
+    x1 += red[w][row][c + 1];
   }
+  if (bias) {
+    x0 += bias[nn];
+    if (nn + 1 < N) x1 += bias[nn + 1];
+  }
+  if constexpr (EPI == SVAE_EPI_GELU) {
+    x0 = gelu_f(x0);
+    x1 = gelu_f(x1);
+  } else if constexpr (EPI == SVAE_EPI_ROTARY_BF16) {
+    if (nn < rot_cols) {
+      const float2 cs = ((const float2*)rot)[(long long)p * (rot_d / 2) + (nn % rot_d) / 2];
+      const float a = x0, b = x1;
+      x0 = a * cs.x + (-b) * cs.y;
+      x1 = b * cs.x + a * cs.y;
+    }
+  }
+  if (resid) {
+    x0 += resid[(long long)m * ldr + nn];
+    if (nn + 1 < N) x1 += resid[(long long)m * ldr + nn + 1];
+  }
+  Y[(long long)m * ldy + nn] = x0;
+  if (nn + 1 < N) Y[(long long)m * ldy + nn + 1] = x1;
 }
 
 // ------------------------------------------------------------------ block reductions (256 / 1024 threads)
@@ -436,15 +451,15 @@ SVAE_EXPORT int svae_dec_linear(const float* X, int64_t ldx, const float* W, int
   hipStream_t s = (hipStream_t)stream;
   switch (epi) {
     case SVAE_EPI_F32:
-      hipLaunchKernelGGL((dec_linear_kernel<SVAE_EPI_F32>), grid, dim3(256), 0, s, X, ldx, W, ldw, bias, Y, ldy, resid,
+      hipLaunchKernelGGL((dec_linear_kernel<SVAE_EPI_F32>), grid, dim3(1024), 0, s, X, ldx, W, ldw, bias, Y, ldy, resid,
                          ldr, M, N, K, rot_tab, rot_cols, rot_d, cur);
       break;
     case SVAE_EPI_GELU:
-      hipLaunchKernelGGL((dec_linear_kernel<SVAE_EPI_GELU>), grid, dim3(256), 0, s, X, ldx, W, ldw, bias, Y, ldy, resid,
+      hipLaunchKernelGGL((dec_linear_kernel<SVAE_EPI_GELU>), grid, dim3(1024), 0, s, X, ldx, W, ldw, bias, Y, ldy, resid,
                          ldr, M, N, K, rot_tab, rot_cols, rot_d, cur);
       break;
     case SVAE_EPI_ROTARY_BF16:
-      hipLaunchKernelGGL((dec_linear_kernel<SVAE_EPI_ROTARY_BF16>), grid, dim3(256), 0, s, X, ldx, W, ldw, bias, Y, ldy,
+      hipLaunchKernelGGL((dec_linear_kernel<SVAE_EPI_ROTARY_BF16>), grid, dim3(1024), 0, s, X, ldx, W, ldw, bias, Y, ldy,
                          resid, ldr, M, N, K, rot_tab, rot_cols, rot_d, cur);
       break;
     default:
