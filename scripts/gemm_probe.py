@@ -68,7 +68,38 @@ def shape_cases():
               f'{2.0 * M * N_ * K_ / ms / 1e9:7.1f} TF/s', flush=True)
 
 
+def epi_cases():
+    """Same shape, different epilogues: the cost of each epilogue over the plain bf16 store."""
+    for (M, N_, K_) in [(32768, 512, 2048), (32768, 2048, 512), (32768, 1536, 512)]:
+        A = torch.randn(M, K_, device=dev).to(bf16)
+        B = torch.randn(N_, K_, device=dev).to(bf16)
+        Cb = torch.empty(M, N_, device=dev, dtype=bf16)
+        Cf = torch.empty(M, N_, device=dev, dtype=f32)
+        R = torch.randn(M, N_, device=dev, dtype=f32)
+        aux = torch.randn(M, N_, device=dev).to(bf16)
+        bias = torch.randn(N_, device=dev)
+        rot = torch.randn(512, 256, 2, device=dev)
+        cases = {
+            'bf16': lambda: K.gemm(A, B, Cb, M, N_, K_, epi=N.EPI_BF16, bias=bias),
+            'f32': lambda: K.gemm(A, B, Cf, M, N_, K_, epi=N.EPI_F32, bias=bias),
+            'f32+resid': lambda: K.gemm(A, B, Cf, M, N_, K_, epi=N.EPI_F32, bias=bias, resid=R, ldr=N_),
+            'drop+resid': lambda: K.gemm(A, B, Cf, M, N_, K_, epi=N.EPI_DROPOUT_RESID, resid=R, ldr=N_, drop_p=0.1,
+                                         seed=5),
+            'gelu+aux': lambda: K.gemm(A, B, Cb, M, N_, K_, epi=N.EPI_GELU, bias=bias, aux=aux, ldaux=N_),
+            'gelu_bwd': lambda: K.gemm(A, B, Cb, M, N_, K_, epi=N.EPI_GELU_BWD, aux=aux, ldaux=N_),
+            'rotary': lambda: K.gemm(A, B, Cb, M, N_, K_, epi=N.EPI_ROTARY_BF16, bias=bias, rot=rot, rot_cols=min(N_, 1024),
+                                     rot_d=512, rot_seq=512),
+        }
+        for name, fn in cases.items():
+            ms = timeit(fn)
+            print(f'epi M={M} N={N_} K={K_} {name:11s} {ms * 1e3:8.1f} us {2.0 * M * N_ * K_ / ms / 1e9:7.1f} TF/s',
+                  flush=True)
+
+
 if __name__ == '__main__':
+    if len(sys.argv) > 1 and sys.argv[1] == 'epi':
+        epi_cases()
+        sys.exit(0)
     print('SVAE_GEMM_GROUP =', os.environ.get('SVAE_GEMM_GROUP'), 'SVAE_GEMM_EXPT =', os.environ.get('SVAE_GEMM_EXPT'))
     head_cases()
     if len(sys.argv) > 1 and sys.argv[1] == 'all':

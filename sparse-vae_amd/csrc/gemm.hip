@@ -706,7 +706,7 @@ __device__ __forceinline__ void g3_epilogue(const GP& p, char* smem, const f32x4
   }
 }
 
-// Register epilogue (bf16 out, GELU, CE statistics): straight from the C^T fragments, no staging. Each fragment
+// Register epilogue (bf16 out, GELU, rotary, CE statistics): straight from the C^T fragments, no staging. Each fragment
 // is one 8-B bf16x4 store per lane (16 rows x 32 B per instruction; a row's 128-B line completes over the 4 j).
 // CE: per-row (max, sum exp) over the wave's 64 columns by permlane reductions, combined across the 4 column
 // waves through the side area into the 128-column partials ce_rows_kernel expects; the label logit is written
@@ -748,6 +748,12 @@ __device__ __forceinline__ void g3_reg_epilogue(const GP& p, const f32x4 (&acc)[
     f32x4 v[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) v[j] = p.alpha * acc[i][j] + b4[j];
+    if constexpr (EPI == SVAE_EPI_ROTARY_BF16) {
+      // a lane's 4 consecutive columns are two whole (2i, 2i+1) rotary pairs: rotate in registers
+      const int mr = m < p.M ? m : 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) rotary4(p, v[j], mr, n0 + wc * 64 + j * 16 + 4 * g);
+    }
     {
       // (the permlane swaps need every lane: the bounds are applied to the stores only)
       const bool row_ok = m < p.M;
@@ -829,6 +835,7 @@ __device__ __forceinline__ void g3_reg_epilogue(const GP& p, const f32x4 (&acc)[
 // Register epilogue for the epilogues that read another tensor: f32 out (+resid), f32 accumulate, dropout +
 // resid, and bf16 x GELU' (the FFN backward). The operand rows for fragment row i + 1 are loaded before row i's
 // stores are issued, so the compiler's counted waits never drain the stores (vmcnt retires in issue order).
+// (A two-row-ahead variant measured no faster in the step.)
 // f32 rows: one 16-B load / store per fragment (16 rows x 64 B per instruction); GELU': the permlane-swapped
 // 8-column layout of store_pair_bf16, with the matching 16-B aux loads.
 template <int EPI>
@@ -1115,7 +1122,8 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GP p) {
           if (m + e < p.M) atomicAdd(p.a_rowsum + m + e, rsum[e]);
       }
     }
-    if constexpr (EPI == SVAE_EPI_BF16 || EPI == SVAE_EPI_GELU || EPI == SVAE_EPI_CE_STATS)
+    if constexpr (EPI == SVAE_EPI_BF16 || EPI == SVAE_EPI_GELU || EPI == SVAE_EPI_CE_STATS ||
+                  EPI == SVAE_EPI_ROTARY_BF16)
       g3_reg_epilogue<EPI>(p, acc, sbias, slabel, sstat, T.m0, T.n0, T.bn, T.batch, T.split, wr, wc, tid, lane);
     else if constexpr (EPI == SVAE_EPI_F32 || EPI == SVAE_EPI_F32_ACC || EPI == SVAE_EPI_DROPOUT_RESID ||
                        EPI == SVAE_EPI_GELU_BWD)
