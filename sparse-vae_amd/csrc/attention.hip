@@ -92,16 +92,14 @@ __device__ __forceinline__ void dma_rows(const bf16* g, long long ld, int row0, 
                                          int lane) {
   using T = Tile<HDP>;
   constexpr int NI = 64 * T::PITCH / 1024;   // wave instructions per tile: 8 (HDP 64) / 16 (HDP 128)
-  const __amdgpu_buffer_rsrc_t rsrc =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(g + (long long)row0 * ld), 0, 0x7FFFFFF0, 0x00020000);
+  const u32x4 rsrc = buffer_rsrc(g + (long long)row0 * ld, 0x7FFFFFF0u);
 #pragma unroll
   for (int i = 0; i < NI / 4; ++i) {
     const int inst = w * (NI / 4) + i;
     const int byte = inst * 1024 + lane * 16;
     const int r = byte / T::PITCH, c = ((byte % T::PITCH) >> 4) ^ (r & (T::NCH - 1));
     const bool ok = row0 + r < nrows && c * 8 < hd;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void*)(lds + inst * 1024), 16,
-                                             ok ? (r * (int)ld + c * 8) * 2 : 0x7FFFFFF0, 0, 0, 0);
+    dma16_lds(rsrc, lds + inst * 1024, ok ? (r * (int)ld + c * 8) * 2 : 0x7FFFFFF0);
   }
 }
 
@@ -114,21 +112,44 @@ constexpr float LOG2E = 1.4426950408889634f;
 
 // ===================================================================================== forward
 // One block = 128 queries of one (batch, head): 4 waves x 32 queries (two 16-query MFMA column tiles), so
-// every K fragment and V^T fragment read from LDS feeds two MFMAs. Softmax in the exp2 domain with the raw
+// every K fragment and V^T fragment read from LDS feeds two MFMAs. K/V tiles arrive by LDS-DMA NS - 1 tiles
+// ahead (a 4-stage ring for hd <= 64) with one counted wait + barrier per tile. Softmax in the exp2 domain with the raw
 // (unscaled) running max: p = exp2(s c - m c), c = scale log2(e). Masks only on edge tiles (causal diagonal,
 // ragged end, padded keys present); causal tiles entirely above a wave's queries are skipped.
+// s_waitcnt vmcnt(n) for a run-time n (the immediate must be a constant): n = vector-memory ops allowed to stay in
+// flight (vmcnt retires in issue order, so this waits for everything older than the n youngest).
+__device__ __forceinline__ void wait_vmcnt(int n) {
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+    case 16: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+    case 17: asm volatile("s_waitcnt vmcnt(17)" ::: "memory"); break;
+    case 32: asm volatile("s_waitcnt vmcnt(32)" ::: "memory"); break;
+    case 34: asm volatile("s_waitcnt vmcnt(34)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
+
 template <int HDP>
 __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AP p) {
   using T = Tile<HDP>;
   constexpr int NKK = HDP / 32, NT = HDP / 16;
-  __shared__ __attribute__((aligned(16))) char smem[4 * T::BYTES + 128];
+  // K/V ring: NS stages of (K, V) tiles, filled NS - 1 key tiles ahead (one tile of compute is shorter than the
+  // HBM latency of the next tile); the key-padding bytes ride along in a [NS][64] ring
+  constexpr int NS = HDP == 64 ? 4 : 2;
+  constexpr int DMA_OPS = 2 * (64 * T::PITCH / 1024) / 4;   // buffer_load_lds per wave per (K, V) tile
+  __shared__ __attribute__((aligned(16))) char smem[NS * 2 * T::BYTES + NS * 64 * 4];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, li = lane & 15;
   const int q0 = blockIdx.x * 128, h = blockIdx.y, b = blockIdx.z;
   const bf16* Q = p.q + b * p.bq + (long long)h * p.hd;
   const bf16* K = p.k + b * p.bk + (long long)h * p.hd;
   const bf16* V = p.v + b * p.bv + (long long)h * p.hd;
   const unsigned char* pad = p.pad ? p.pad + (long long)b * p.Lk : nullptr;
-  unsigned char* pm = (unsigned char*)(smem + 4 * T::BYTES);
+  // key-padding ring: one dword per key (LDS-DMA writes a dword slot per lane; the byte is its low 8 bits)
+  unsigned* pm = (unsigned*)(smem + NS * 2 * T::BYTES);
 
   const int qw = q0 + 32 * w;
   bf16x8 qf[2][NKK];
@@ -154,61 +175,81 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AP p) {
   const int kt1 = max(1, band_lo(q0, p.window) / 64);
   const int nvisit = 1 + max(0, ntiles - kt1);
   const int lo_w = band_lo(qw, p.window);          // this wave's 32 queries share one 32-block
-
-  unsigned char rpm = 0;
-  dma_rows<HDP>(K, p.sk, 0, p.Lk, p.hd, smem, w, lane);
-  dma_rows<HDP>(V, p.sv, 0, p.Lk, p.hd, smem + T::BYTES, w, lane);
-  if (tid < 64) pm[tid] = (pad && tid < p.Lk) ? pad[tid] : 0;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  // vector-memory ops one tile issue adds per wave: the K and V pieces, and for wave 0 the key-padding bytes
+  // (DMA'd into the [NS][64] ring like the tiles: no register round trip, no compiler-visible load to wait for)
+  const int ops = DMA_OPS + ((pad && w == 0) ? 1 : 0);
+  const u32x4 prs = buffer_rsrc(pad ? (const void*)pad : (const void*)p.q, pad ? (unsigned)p.Lk : 0u);
+  auto issue = [&](int it2) {
+    const int kn = (it2 == 0 ? 0 : kt1 + it2 - 1) * 64;
+    char* nb = smem + (it2 % NS) * 2 * T::BYTES;
+    dma_rows<HDP>(K, p.sk, kn, p.Lk, p.hd, nb, w, lane);
+    dma_rows<HDP>(V, p.sv, kn, p.Lk, p.hd, nb + T::BYTES, w, lane);
+    if (pad && w == 0) dma1_lds(prs, pm + (it2 % NS) * 64, kn + lane < p.Lk ? kn + lane : 0x7FFFFFF0);
+  };
+  if (!pad && tid < NS * 64) pm[tid] = 0;
+  // Consume the Q fragments before the ring starts, so the compiler's wait for them (it cannot see the DMA)
+  // is not a vmcnt(0) inside the loop.
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int kk = 0; kk < NKK; ++kk) asm volatile("" ::"v"(__builtin_bit_cast(u32x4, qf[j][kk])));
+#pragma unroll
+  for (int s2 = 0; s2 < NS - 1; ++s2)
+    if (s2 < nvisit) issue(s2);
 
   for (int it = 0; it < nvisit; ++it) {
     const int kt = it == 0 ? 0 : kt1 + it - 1;
-    const int buf = it & 1;
-    const char* Ks = smem + buf * 2 * T::BYTES;
+    const int st = it % NS;
+    const char* Ks = smem + st * 2 * T::BYTES;
     const char* Vs = Ks + T::BYTES;
-    const unsigned char* pms = pm + buf * 64;
-    const bool more = it + 1 < nvisit;
-    if (more) {   // next tile straight into the other buffer (its readers finished before the last barrier)
-      const int kn = (it == 0 ? kt1 : kt + 1) * 64;
-      char* nb = smem + (buf ^ 1) * 2 * T::BYTES;
-      dma_rows<HDP>(K, p.sk, kn, p.Lk, p.hd, nb, w, lane);
-      dma_rows<HDP>(V, p.sv, kn, p.Lk, p.hd, nb + T::BYTES, w, lane);
-      if (tid < 64) rpm = (pad && kn + tid < p.Lk) ? pad[kn + tid] : 0;
-    }
+    const unsigned* pms = pm + st * 64;
+    wait_vmcnt(min(NS - 2, nvisit - 1 - it) * ops);   // this wave's pieces of tile it have landed
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();   // everyone's have; stage (it - 1) % NS is free (a raw barrier: __syncthreads
+                                    // would also drain the younger tiles' DMA with its vmcnt(0))
+    if (it + NS - 1 < nvisit) issue(it + NS - 1);
     const int kbase = kt * 64;
     if ((!p.causal || kbase <= qw + 31) && (kbase < SBLK || kbase + 63 >= lo_w)) {
       // S^T = K . Q^T : s[j][st][r] = score(key = kbase + 16st + 4g + r, query = qw + 16j + li)
       f32x4 s[2][4];
 #pragma unroll
-      for (int st = 0; st < 4; ++st) {
-        s[0][st] = (f32x4){0.f, 0.f, 0.f, 0.f};
-        s[1][st] = s[0][st];
+      for (int sx = 0; sx < 4; ++sx) {
+        s[0][sx] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        s[1][sx] = s[0][sx];
 #pragma unroll
         for (int kk = 0; kk < NKK; ++kk) {
-          const bf16x8 kf = *(const bf16x8*)(Ks + T::off(16 * st + li, g + 4 * kk));
-          s[0][st] = mfma16(kf, qf[0][kk], s[0][st]);
-          s[1][st] = mfma16(kf, qf[1][kk], s[1][st]);
+          const bf16x8 kf = *(const bf16x8*)(Ks + T::off(16 * sx + li, g + 4 * kk));
+          s[0][sx] = mfma16(kf, qf[0][kk], s[0][sx]);
+          s[1][sx] = mfma16(kf, qf[1][kk], s[1][sx]);
         }
       }
-      const bool pad_any = p.pad && __builtin_amdgcn_ballot_w64(pms[lane] != 0) != 0;
+      const bool pad_any = pad && __builtin_amdgcn_ballot_w64((pms[lane] & 0xFFu) != 0) != 0;
       if (pad_any || kbase + 64 > p.Lk || (p.causal && kbase + 63 > qw) || (kbase + 63 >= SBLK && kbase < lo_w)) {
+        // this lane's key-padding bits for its 16 keys (keys 16sx + 4g + r) gathered once
+        unsigned pbits = 0;
+        if (pad_any) {
+#pragma unroll
+          for (int sx = 0; sx < 4; ++sx)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) pbits |= ((pms[16 * sx + 4 * g + r] & 0xFFu) ? 1u : 0u) << (4 * sx + r);
+        }
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
-          for (int st = 0; st < 4; ++st)
+          for (int sx = 0; sx < 4; ++sx)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-              const int kl = 16 * st + 4 * g + r, key = kbase + kl;
-              if (key >= p.Lk || pms[kl] || (p.causal && key > qw + 16 * j + li) || (key >= SBLK && key < lo_w))
-                s[j][st][r] = -INFINITY;
+              const int kl = 16 * sx + 4 * g + r, key = kbase + kl;
+              if (key >= p.Lk || ((pbits >> (4 * sx + r)) & 1u) || (p.causal && key > qw + 16 * j + li) ||
+                  (key >= SBLK && key < lo_w))
+                s[j][sx][r] = -INFINITY;
             }
       }
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         float mx = -INFINITY;
 #pragma unroll
-        for (int st = 0; st < 4; ++st) mx = fmaxf(fmaxf(mx, fmaxf(s[j][st][0], s[j][st][1])), fmaxf(s[j][st][2], s[j][st][3]));
+        for (int sx = 0; sx < 4; ++sx) mx = fmaxf(fmaxf(mx, fmaxf(s[j][sx][0], s[j][sx][1])), fmaxf(s[j][sx][2], s[j][sx][3]));
         mx = max_x16_x32(mx);
         const float mn = fmaxf(m[j], mx);
         const float alpha = __builtin_amdgcn_exp2f((m[j] - mn) * c);
@@ -218,11 +259,11 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AP p) {
         for (int t = 0; t < NT; ++t) o[j][t] *= alpha;
         const float mc = mn * c;
 #pragma unroll
-        for (int st = 0; st < 4; ++st)
+        for (int sx = 0; sx < 4; ++sx)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const float pv = __builtin_amdgcn_exp2f(fmaf(s[j][st][r], c, -mc));
-            s[j][st][r] = pv;
+            const float pv = __builtin_amdgcn_exp2f(fmaf(s[j][sx][r], c, -mc));
+            s[j][sx][r] = pv;
             ls[j] += pv;
           }
       }
@@ -241,9 +282,6 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AP p) {
         }
       }
     }
-    if (more && tid < 64) pm[(buf ^ 1) * 64 + tid] = rpm;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
   }
 
 #pragma unroll

@@ -33,6 +33,35 @@ __device__ __forceinline__ short4v lds_read_tr(const void* lds_addr) {
       (__attribute__((address_space(3))) short4v*)(uintptr_t)(lds_addr));
 }
 
+// LDS-DMA of 16 B per lane (buffer_load_dwordx4 ... lds) into lds_base + 16 * lane, from rsrc + voff (bytes;
+// out-of-range offsets land as zeros). Issued through inline asm on purpose: the compiler's wait-count pass
+// would otherwise treat every later ds_read_b64_tr_b16 as a possible reader of the DMA destination and put a
+// vmcnt(0) in front of it, draining the prefetched tiles of every ring that uses transposed LDS reads. The
+// callers wait for the DMA explicitly (counted s_waitcnt vmcnt + barrier) before reading a stage.
+// rsrc: the 4 descriptor words (base lo, base hi, num_records, flags), wave-uniform.
+__device__ __forceinline__ u32x4 buffer_rsrc(const void* base, unsigned num_records) {
+  const uint64_t a = (uint64_t)(uintptr_t)base;
+  return (u32x4){(unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)a),
+                 (unsigned)__builtin_amdgcn_readfirstlane((int)((unsigned)(a >> 32) & 0xFFFFu)), num_records,
+                 0x00020000u};
+}
+__device__ __forceinline__ void dma16_lds(const u32x4& rsrc, const void* lds_base, int voff) {
+  const int m = __builtin_amdgcn_readfirstlane((int)(unsigned)(uintptr_t)lds_base);
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
+               :
+               : "s"(m), "v"(voff), "s"(rsrc)
+               : "memory", "m0");
+}
+
+// 1 B per lane (buffer_load_ubyte ... lds) into lds_base + lane, same conventions as dma16_lds.
+__device__ __forceinline__ void dma1_lds(const u32x4& rsrc, const void* lds_base, int voff) {
+  const int m = __builtin_amdgcn_readfirstlane((int)(unsigned)(uintptr_t)lds_base);
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_ubyte %1, %2, 0 offen lds"
+               :
+               : "s"(m), "v"(voff), "s"(rsrc)
+               : "memory", "m0");
+}
+
 __device__ __forceinline__ bf16x8 cat44(short4v lo, short4v hi) {
   typedef short short8v __attribute__((ext_vector_type(8)));
   short8v s = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};

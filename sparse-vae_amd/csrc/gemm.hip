@@ -437,7 +437,7 @@ template <bool TRANS>
 __device__ __forceinline__ void issue_tile2(const bf16* __restrict__ g, long long ld, int row0, int nrows, int k0,
                                             int kend, char* lds_tile, int wave, int lane) {
   const bf16* base = TRANS ? g + (long long)k0 * ld + row0 : g + (long long)row0 * ld + k0;
-  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, 0x7FFFFFF0, 0x00020000);
+  const u32x4 rsrc = buffer_rsrc(base, 0x7FFFFFF0u);
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int inst = wave * 2 + j;
@@ -455,8 +455,7 @@ __device__ __forceinline__ void issue_tile2(const bf16* __restrict__ g, long lon
       off = (kr * (int)ld + v * 8) * 2;
       ok = (k0 + kr < kend) && (row0 + v * 8 < nrows);
     }
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void*)(lds_tile + inst * 1024), 16,
-                                             ok ? off : 0x7FFFFFF0, 0, 0, 0);
+    dma16_lds(rsrc, lds_tile + inst * 1024, ok ? off : 0x7FFFFFF0);
   }
 }
 
@@ -635,12 +634,11 @@ __device__ __forceinline__ G3Src g3_src_mn(long long ld, int col0, int ncols, in
 
 template <bool MN>
 __device__ __forceinline__ void g3_issue_one(const bf16* tile_base, const G3Src& src, int krem, char* dst, int wave) {
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)tile_base, 0, 0x7FFFFFF0, 0x00020000);
+  const u32x4 rs = buffer_rsrc(tile_base, 0x7FFFFFF0u);
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int off = (krem >= 64 || src.kq[i] < krem) ? src.off[i] : 0x7FFFFFF0;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(dst + (wave * 4 + i) * 1024),
-                                             16, off, 0, 0, 0);
+    dma16_lds(rs, dst + (wave * 4 + i) * 1024, off);
   }
 }
 
