@@ -354,7 +354,7 @@ __global__ __launch_bounds__(256, HDP == 64 ? 2 : 1) void attn_bwd_kernel(AP p) 
   char* QO = smem;                                  // [buf][Q, dO] tiles
   char* Ks = smem + 4 * T::BYTES;                   // 128 key rows
   char* dSs = smem + 6 * T::BYTES;                  // 128 key rows x 64 queries
-  float* cst = (float*)(smem + 6 * T::BYTES + 2 * TS::BYTES);   // [buf][-lse/scale, -delta][64]
+  float* cst = (float*)(smem + 6 * T::BYTES + 2 * TS::BYTES);   // [buf][lse, delta][64] (DMA'd with the tile)
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, li = lane & 15;
   const int kb = blockIdx.x, k0 = kb * BWD_KEYS, h = blockIdx.y, b = blockIdx.z;
@@ -401,23 +401,21 @@ __global__ __launch_bounds__(256, HDP == 64 ? 2 : 1) void attn_bwd_kernel(AP p) 
   const int band_end = p.window > 0 && kw >= SBLK ? kw + SBLK * p.window : 0x7FFFFFFF;   // first query past kw's band
   float* part = p.dq_part + ((long long)kb * p.B + b) * p.Lq * p.H * p.hd + (long long)h * p.hd;
   const long long ldp = (long long)p.H * p.hd;
+  // On a full query tile (all 64 queries < Lq, hd == HDP) every wave issues exactly DQ_STORES dQ-partial stores
+  // after the next tile's DMA, so the end-of-tile wait can leave exactly those in flight (vmcnt retires in
+  // issue order); edge tiles wait for everything.
+  constexpr int DQ_STORES = NT * 4;
 
-  float rc = 0.f;
+  // the row constants (lse, delta) of a query tile ride along with its Q / dO DMA into cst[buf][lse | delta]
+  const u32x4 lser = buffer_rsrc(lse, (unsigned)p.Lq * 4u), der = buffer_rsrc(delta, (unsigned)p.Lq * 4u);
   auto fetch = [&](int qb, int buf) {
     dma_rows<HDP>(Q, p.sq, qb, p.Lq, p.hd, QO + buf * 2 * T::BYTES, w, lane);
     dma_rows<HDP>(dO, p.sdo, qb, p.Lq, p.hd, QO + buf * 2 * T::BYTES + T::BYTES, w, lane);
-    if (tid < 128) {
-      const int q = qb + (tid & 63);
-      rc = q < p.Lq ? (tid < 64 ? -lse[q] * inv_scale : -delta[q]) : 0.f;
-    }
+    const int qo = qb + lane < p.Lq ? (qb + lane) * 4 : 0x7FFFFFF0;
+    if (w == 0) dma4_lds(lser, cst + buf * 128, qo);
+    else if (w == 1) dma4_lds(der, cst + buf * 128 + 64, qo);
   };
-  auto commit = [&](int buf) {
-    if (tid < 128) cst[buf * 128 + tid] = rc;
-  };
-  if (qt0 < nqt) {
-    fetch(qt0 * 64, 0);
-    commit(0);
-  }
+  if (qt0 < nqt) fetch(qt0 * 64, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
@@ -439,8 +437,8 @@ __global__ __launch_bounds__(256, HDP == 64 ? 2 : 1) void attn_bwd_kernel(AP p) 
         for (int kk = 0; kk < NKK; ++kk) kf[j][kk] = *(const bf16x8*)(Ks + T::off(32 * w + 16 * j + li, g + 4 * kk));
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
-        const f32x4 sl = *(const f32x4*)(nl + 16 * t + 4 * g);
-        const f32x4 dl = *(const f32x4*)(nl + 64 + 16 * t + 4 * g);
+        const f32x4 sl = *(const f32x4*)(nl + 16 * t + 4 * g) * -inv_scale;   // -lse / scale
+        const f32x4 dl = -*(const f32x4*)(nl + 64 + 16 * t + 4 * g);          // -delta
         s[0][t] = sl; s[1][t] = sl;
         dp[0][t] = dl; dp[1][t] = dl;
 #pragma unroll
@@ -499,7 +497,8 @@ __global__ __launch_bounds__(256, HDP == 64 ? 2 : 1) void attn_bwd_kernel(AP p) 
 #pragma unroll
         for (int t = 0; t < 4; ++t) *(bf16x4*)(dSs + TS::uoff(32 * w + 16 * j + li, 4 * t + g)) = z;
     }
-    __syncthreads();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();   // dS^T complete (a raw barrier: __syncthreads' vmcnt(0) would drain the DMA)
     // partial dQ[q = qb + 16w + 4g + r][d = 16u + li] = sum over the block's 128 keys of dS[q][key] K[key][d]
     f32x4 dq[NT];
 #pragma unroll
@@ -529,9 +528,11 @@ __global__ __launch_bounds__(256, HDP == 64 ? 2 : 1) void attn_bwd_kernel(AP p) 
         }
       }
     }
-    if (more) commit(buf ^ 1);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    // the next tile's DMA (issued before this tile's stores) has landed; on full tiles the stores stay in flight
+    if (qb + 64 <= p.Lq && p.hd == HDP) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DQ_STORES) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
   }
 
   // epilogue: dK (scaled, inverse rotary) and dV for key = kw + 16j + li, dims 16u + 4g + (0..3)

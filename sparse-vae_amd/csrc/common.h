@@ -53,7 +53,17 @@ __device__ __forceinline__ void dma16_lds(const u32x4& rsrc, const void* lds_bas
                : "memory", "m0");
 }
 
-// 1 B per lane (buffer_load_ubyte ... lds) into lds_base + lane, same conventions as dma16_lds.
+// 4 B per lane (buffer_load_dword ... lds) into lds_base + 4 * lane, same conventions as dma16_lds.
+__device__ __forceinline__ void dma4_lds(const u32x4& rsrc, const void* lds_base, int voff) {
+  const int m = __builtin_amdgcn_readfirstlane((int)(unsigned)(uintptr_t)lds_base);
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dword %1, %2, 0 offen lds"
+               :
+               : "s"(m), "v"(voff), "s"(rsrc)
+               : "memory", "m0");
+}
+
+// 1 B per lane (buffer_load_ubyte ... lds) into a dword slot per lane (lds_base + 4 * lane; the byte is the low
+// 8 bits of the slot), same conventions as dma16_lds.
 __device__ __forceinline__ void dma1_lds(const u32x4& rsrc, const void* lds_base, int voff) {
   const int m = __builtin_amdgcn_readfirstlane((int)(unsigned)(uintptr_t)lds_base);
   asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_ubyte %1, %2, 0 offen lds"
