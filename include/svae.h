@@ -223,7 +223,8 @@ int svae_ce_seq_logprob(const float* part, int32_t ntile, const float* label_log
  * position. out_ids: int64 [B][T] (GenerationState.output_ids); live: uint8 [B].
  * dec_linear: Y[M,N] = epi(X[M,K] . W[N,K]^T + bias) + resid; epi SVAE_EPI_F32 / SVAE_EPI_GELU /
  *   SVAE_EPI_ROTARY_BF16 (rotary of rot_tab row cur-1 on columns < rot_cols, pairs within rot_d; f32 out).
- *   K % 4 == 0, X and W 16-byte aligned.
+ *   K % 4 == 0, X and W 16-byte aligned. part_ws (f32, part_elems floats, may be NULL): split-K partials for
+ *   narrow N (the library picks the split count that fits; NULL = no split).
  * dec_attn: qkv f32 [B][ldq] = q | k | v (rotary applied); appends k, v at position cur-1 to the caches
  *   [B][H][T][hd] and writes O[b][h*hd ..] = softmax(q k^T * scale) v over the visible keys: 0..cur-1, or with
  *   window > 0 the sliding-window cache's set ([CLS] block, window-1 previous 32-blocks, current block).
@@ -236,7 +237,8 @@ int svae_ce_seq_logprob(const float* part, int32_t ntile, const float* label_log
  * dec_advance: *cur += 1. */
 int svae_dec_linear(const float* X, int64_t ldx, const float* W, int64_t ldw, const float* bias, float* Y, int64_t ldy,
                     const float* resid, int64_t ldr, int32_t M, int32_t N, int32_t K, int32_t epi, const float* rot_tab,
-                    int32_t rot_cols, int32_t rot_d, const int32_t* cur, svae_stream_t stream);
+                    int32_t rot_cols, int32_t rot_d, const int32_t* cur, float* part_ws, int64_t part_elems,
+                    svae_stream_t stream);
 int svae_dec_attn(const float* qkv, int64_t ldq, float* kcache, float* vcache, int32_t B, int32_t H, int32_t hd,
                   int32_t T, const int32_t* cur, int32_t window, float scale, float* O, int64_t ldo,
                   svae_stream_t stream);

@@ -50,7 +50,7 @@ __device__ __forceinline__ void dma16_lds(const u32x4& rsrc, const void* lds_bas
   asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
                :
                : "s"(m), "v"(voff), "s"(rsrc)
-               : "memory", "m0");
+               : "memory");  // (m0 is reserved: the compiler sets it before each of its own uses)
 }
 
 // 4 B per lane (buffer_load_dword ... lds) into lds_base + 4 * lane, same conventions as dma16_lds.
@@ -59,7 +59,7 @@ __device__ __forceinline__ void dma4_lds(const u32x4& rsrc, const void* lds_base
   asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dword %1, %2, 0 offen lds"
                :
                : "s"(m), "v"(voff), "s"(rsrc)
-               : "memory", "m0");
+               : "memory");  // (m0 is reserved: the compiler sets it before each of its own uses)
 }
 
 // 1 B per lane (buffer_load_ubyte ... lds) into a dword slot per lane (lds_base + 4 * lane; the byte is the low
@@ -69,7 +69,7 @@ __device__ __forceinline__ void dma1_lds(const u32x4& rsrc, const void* lds_base
   asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_ubyte %1, %2, 0 offen lds"
                :
                : "s"(m), "v"(voff), "s"(rsrc)
-               : "memory", "m0");
+               : "memory");  // (m0 is reserved: the compiler sets it before each of its own uses)
 }
 
 __device__ __forceinline__ bf16x8 cat44(short4v lo, short4v hi) {

@@ -6,8 +6,9 @@
 // captured step graph (hipGraph via torch.cuda.CUDAGraph) replays for every position.
 //
 //   svae_dec_linear:  Y[M,N] = epi(X[M,K] . W[N,K]^T + b) (+ resid): weight-streaming skinny GEMM on
-//                     v_mfma_f32_16x16x4_f32, 16 output columns per workgroup, K split over its 16 waves and
-//                     reduced through LDS; epilogues plain / GELU / rotary at position cur-1.
+//                     v_mfma_f32_16x16x4_f32, 16 output columns per workgroup, K split over its 16 waves (LDS
+//                     reduction) and, for narrow N, over workgroups (partials + an ordered finalize); epilogues
+//                     plain / GELU / rotary at position cur-1.
 //   svae_dec_attn:    one workgroup per (sequence, head): appends k, v at position cur-1 to the cache
 //                     [B][H][T][hd] and attends over the visible keys (dense causal, or the sliding-window
 //                     cache's key set: [CLS] block + window-1 previous blocks + the current block).
@@ -24,36 +25,71 @@ using namespace svae;
 namespace {
 
 // ------------------------------------------------------------------ skinny f32 linear
-// 16 output columns x up to 64 rows per workgroup of 16 waves; the waves split K (memory-level parallelism for
-// the weight stream: a d x d weight is only N / 16 workgroups wide) and their partials meet in LDS.
+// 16 output columns x up to 64 rows per workgroup of 16 waves; the waves split the workgroup's K range and meet in
+// LDS. Narrow outputs (a d x d weight is only N / 16 = 32 workgroups wide) also split K over workgroups
+// (gridDim.z = splits): each writes its partial sums to a caller-owned workspace and a finalize pass adds the
+// splits in a fixed order and applies the epilogue (deterministic, no atomics).
 constexpr int DL_MROWS = 64;   // rows per workgroup (4 MFMA m-tiles)
 constexpr int DL_WAVES = 16;
 
+struct DL {
+  const float* X; long long ldx;
+  const float* W; long long ldw;
+  const float* bias;
+  float* Y; long long ldy;
+  const float* resid; long long ldr;
+  int M, N, K, kslice;
+  const float* rot; int rot_cols, rot_d;
+  const int* cur;
+  float* part;        // [splits][M][N] partial sums (split-K), or nullptr
+};
+
 template <int EPI>
-__global__ __launch_bounds__(1024) void dec_linear_kernel(const float* __restrict__ X, long long ldx,
-                                                          const float* __restrict__ W, long long ldw,
-                                                          const float* __restrict__ bias, float* __restrict__ Y,
-                                                          long long ldy, const float* __restrict__ resid, long long ldr,
-                                                          int M, int N, int K, const float* __restrict__ rot,
-                                                          int rot_cols, int rot_d, const int* __restrict__ cur) {
+__device__ __forceinline__ void dl_epilogue(const DL& p, int m, int nn, float x0, float x1, int pos) {
+  if (p.bias) {
+    x0 += p.bias[nn];
+    if (nn + 1 < p.N) x1 += p.bias[nn + 1];
+  }
+  if constexpr (EPI == SVAE_EPI_GELU) {
+    x0 = gelu_f(x0);
+    x1 = gelu_f(x1);
+  } else if constexpr (EPI == SVAE_EPI_ROTARY_BF16) {
+    if (nn < p.rot_cols) {
+      const float2 cs = ((const float2*)p.rot)[(long long)pos * (p.rot_d / 2) + (nn % p.rot_d) / 2];
+      const float a = x0, b = x1;
+      x0 = a * cs.x + (-b) * cs.y;
+      x1 = b * cs.x + a * cs.y;
+    }
+  }
+  if (p.resid) {
+    x0 += p.resid[(long long)m * p.ldr + nn];
+    if (nn + 1 < p.N) x1 += p.resid[(long long)m * p.ldr + nn + 1];
+  }
+  p.Y[(long long)m * p.ldy + nn] = x0;
+  if (nn + 1 < p.N) p.Y[(long long)m * p.ldy + nn + 1] = x1;
+}
+
+template <int EPI>
+__global__ __launch_bounds__(1024) void dec_linear_kernel(DL p) {
   __shared__ float red[DL_WAVES][DL_MROWS][17];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 15, g = lane >> 4;
-  const int n0 = blockIdx.x * 16, m0 = blockIdx.y * DL_MROWS;
-  const int mrows = min(DL_MROWS, M - m0);
+  const int n0 = blockIdx.x * 16, m0 = blockIdx.y * DL_MROWS, split = blockIdx.z;
+  const int mrows = min(DL_MROWS, p.M - m0);
   const int mt = (mrows + 15) >> 4;
-  // this wave's K range: a multiple of 16 (one float4 per lane per step)
-  const int kq = ((K + 16 * DL_WAVES - 1) / (16 * DL_WAVES)) * 16;
-  const int kb = wave * kq, ke = min(K, kb + kq);
+  // this wave's K range inside the split's: a multiple of 16 (one float4 per lane per step)
+  const int sb = split * p.kslice, se = min(p.K, sb + p.kslice);
+  const int kq = ((se - sb + 16 * DL_WAVES - 1) / (16 * DL_WAVES)) * 16;
+  const int kb = sb + wave * kq, ke = min(se, kb + kq);
   f32x4 acc[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) acc[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
   const int n = n0 + r;
-  const float* wrow = W + (long long)min(n, N - 1) * ldw;
+  const float* wrow = p.W + (long long)min(n, p.N - 1) * p.ldw;
   const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
   for (int k = kb; k < ke; k += 32) {     // two K-steps per iteration: all loads issued before the MFMAs
     const int kk0 = k + 4 * g, kk1 = kk0 + 16;
-    const bool in0 = kk0 < ke && n < N, in1 = kk1 < ke && n < N;
+    const bool in0 = kk0 < ke && n < p.N, in1 = kk1 < ke && n < p.N;
     const f32x4 w0 = in0 ? *(const f32x4*)(wrow + kk0) : zero;
     const f32x4 w1 = in1 ? *(const f32x4*)(wrow + kk1) : zero;
     f32x4 x0[4], x1[4];
@@ -61,7 +97,7 @@ __global__ __launch_bounds__(1024) void dec_linear_kernel(const float* __restric
     for (int i = 0; i < 4; ++i) {
       const int m = i * 16 + r;
       const bool mok = i < mt && m < mrows;
-      const float* xr = X + (long long)(m0 + (mok ? m : 0)) * ldx;
+      const float* xr = p.X + (long long)(m0 + (mok ? m : 0)) * p.ldx;
       x0[i] = (mok && kk0 < ke) ? *(const f32x4*)(xr + kk0) : zero;
       x1[i] = (mok && kk1 < ke) ? *(const f32x4*)(xr + kk1) : zero;
     }
@@ -83,39 +119,40 @@ __global__ __launch_bounds__(1024) void dec_linear_kernel(const float* __restric
       for (int e = 0; e < 4; ++e) red[wave][i * 16 + 4 * g + e][r] = acc[i][e];
   __syncthreads();
   // epilogue: thread = (row, column pair); 64 rows x 8 pairs = 512 threads
-  const int p = cur ? *cur - 1 : 0;   // decode position (rotary)
   if (tid >= DL_MROWS * 8) return;
   const int row = tid >> 3, c = (tid & 7) * 2;
   if (row >= mrows) return;
   const int m = m0 + row, nn = n0 + c;
-  if (nn >= N) return;
+  if (nn >= p.N) return;
   float x0 = 0.f, x1 = 0.f;
 #pragma unroll
   for (int w = 0; w < DL_WAVES; ++w) {
     x0 += red[w][row][c];
     x1 += red[w][row][c + 1];
   }
-  if (bias) {
-    x0 += bias[nn];
-    if (nn + 1 < N) x1 += bias[nn + 1];
+  if (p.part) {
+    float* pp = p.part + ((long long)split * p.M + m) * p.N + nn;
+    pp[0] = x0;
+    if (nn + 1 < p.N) pp[1] = x1;
+    return;
   }
-  if constexpr (EPI == SVAE_EPI_GELU) {
-    x0 = gelu_f(x0);
-    x1 = gelu_f(x1);
-  } else if constexpr (EPI == SVAE_EPI_ROTARY_BF16) {
-    if (nn < rot_cols) {
-      const float2 cs = ((const float2*)rot)[(long long)p * (rot_d / 2) + (nn % rot_d) / 2];
-      const float a = x0, b = x1;
-      x0 = a * cs.x + (-b) * cs.y;
-      x1 = b * cs.x + a * cs.y;
-    }
+  dl_epilogue<EPI>(p, m, nn, x0, x1, p.cur ? *p.cur - 1 : 0);
+}
+
+// split-K finalize: thread = (row, column pair), the splits added in order, then the epilogue
+template <int EPI>
+__global__ __launch_bounds__(256) void dec_linear_finalize_kernel(DL p, int splits) {
+  const int half = (p.N + 1) / 2;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= p.M * half) return;
+  const int m = i / half, nn = (i % half) * 2;
+  float x0 = 0.f, x1 = 0.f;
+  for (int s2 = 0; s2 < splits; ++s2) {
+    const float* pp = p.part + ((long long)s2 * p.M + m) * p.N + nn;
+    x0 += pp[0];
+    if (nn + 1 < p.N) x1 += pp[1];
   }
-  if (resid) {
-    x0 += resid[(long long)m * ldr + nn];
-    if (nn + 1 < N) x1 += resid[(long long)m * ldr + nn + 1];
-  }
-  Y[(long long)m * ldy + nn] = x0;
-  if (nn + 1 < N) Y[(long long)m * ldy + nn + 1] = x1;
+  dl_epilogue<EPI>(p, m, nn, x0, x1, p.cur ? *p.cur - 1 : 0);
 }
 
 // ------------------------------------------------------------------ block reductions (256 / 1024 threads)
@@ -443,28 +480,37 @@ __global__ void dec_advance_kernel(int* cur) { *cur += 1; }
 SVAE_EXPORT int svae_dec_linear(const float* X, int64_t ldx, const float* W, int64_t ldw, const float* bias, float* Y,
                                 int64_t ldy, const float* resid, int64_t ldr, int32_t M, int32_t N, int32_t K,
                                 int32_t epi, const float* rot_tab, int32_t rot_cols, int32_t rot_d, const int32_t* cur,
-                                svae_stream_t stream) {
+                                float* part_ws, int64_t part_elems, svae_stream_t stream) {
   if (!X || !W || !Y || M <= 0 || N <= 0 || K <= 0 || K % 4 || ldx % 4 || ldw % 4) return SVAE_EINVAL;
   if (((uintptr_t)X | (uintptr_t)W) & 15) return SVAE_EINVAL;
   if (epi == SVAE_EPI_ROTARY_BF16 && (!rot_tab || !cur || rot_d <= 0 || rot_d % 2 || rot_cols % 2)) return SVAE_EINVAL;
-  dim3 grid((N + 15) / 16, (M + DL_MROWS - 1) / DL_MROWS);
+  if (epi != SVAE_EPI_F32 && epi != SVAE_EPI_GELU && epi != SVAE_EPI_ROTARY_BF16) return SVAE_EINVAL;
+  const int cols = (N + 15) / 16, mblk = (M + DL_MROWS - 1) / DL_MROWS;
+  // split K over workgroups until ~512 workgroups are in flight (slices of >= 256 K-elements), if a workspace
+  // of splits * M * N floats was given
+  int splits = 1;
+  while (splits < 16 && (long long)cols * mblk * splits * 2 <= 512 && K / (splits * 2) >= 256 &&
+         part_ws && (long long)splits * 2 * M * N <= part_elems)
+    splits *= 2;
+  DL p;
+  p.X = X; p.ldx = ldx; p.W = W; p.ldw = ldw; p.bias = bias; p.Y = Y; p.ldy = ldy; p.resid = resid; p.ldr = ldr;
+  p.M = M; p.N = N; p.K = K; p.kslice = ((K + splits - 1) / splits + 15) / 16 * 16;
+  p.rot = rot_tab; p.rot_cols = rot_cols; p.rot_d = rot_d; p.cur = cur;
+  p.part = splits > 1 ? part_ws : nullptr;
+  dim3 grid(cols, mblk, splits);
   hipStream_t s = (hipStream_t)stream;
+  const int fin_blocks = (M * ((N + 1) / 2) + 255) / 256;
+#define SVAE_DL_CASE(E)                                                                               \
+  case E:                                                                                             \
+    hipLaunchKernelGGL((dec_linear_kernel<E>), grid, dim3(1024), 0, s, p);                            \
+    if (splits > 1) hipLaunchKernelGGL((dec_linear_finalize_kernel<E>), dim3(fin_blocks), dim3(256), 0, s, p, splits); \
+    break;
   switch (epi) {
-    case SVAE_EPI_F32:
-      hipLaunchKernelGGL((dec_linear_kernel<SVAE_EPI_F32>), grid, dim3(1024), 0, s, X, ldx, W, ldw, bias, Y, ldy, resid,
-                         ldr, M, N, K, rot_tab, rot_cols, rot_d, cur);
-      break;
-    case SVAE_EPI_GELU:
-      hipLaunchKernelGGL((dec_linear_kernel<SVAE_EPI_GELU>), grid, dim3(1024), 0, s, X, ldx, W, ldw, bias, Y, ldy, resid,
-                         ldr, M, N, K, rot_tab, rot_cols, rot_d, cur);
-      break;
-    case SVAE_EPI_ROTARY_BF16:
-      hipLaunchKernelGGL((dec_linear_kernel<SVAE_EPI_ROTARY_BF16>), grid, dim3(1024), 0, s, X, ldx, W, ldw, bias, Y, ldy,
-                         resid, ldr, M, N, K, rot_tab, rot_cols, rot_d, cur);
-      break;
-    default:
-      return SVAE_EINVAL;
+    SVAE_DL_CASE(SVAE_EPI_F32)
+    SVAE_DL_CASE(SVAE_EPI_GELU)
+    SVAE_DL_CASE(SVAE_EPI_ROTARY_BF16)
   }
+#undef SVAE_DL_CASE
   SVAE_LAUNCH_CHECK();
   return SVAE_OK;
 }

@@ -95,7 +95,7 @@ _SIGS = {
     'svae_layernorm_fwd_f32': [c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p],
     'svae_ce_seq_logprob': [c_void_p, c_int32, c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_void_p],
     'svae_dec_linear': [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_int32,
-                        c_int32, c_int32, c_int32, c_void_p, c_int32, c_int32, c_void_p, c_void_p],
+                        c_int32, c_int32, c_int32, c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_int64, c_void_p],
     'svae_dec_attn': [c_void_p, c_int64, c_void_p, c_void_p, c_int32, c_int32, c_int32, c_int32, c_void_p, c_int32,
                       c_float, c_void_p, c_int64, c_void_p],
     'svae_dec_embed': [c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p],

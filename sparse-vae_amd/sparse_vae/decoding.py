@@ -41,6 +41,7 @@ class KVDecoder:
         self.x, self.xin, self.h, self.x1 = e(B, d), e(B, d), e(B, d), e(B, d)
         self.qkv, self.O, self.f = e(B, 3 * d), e(B, d), e(B, 4 * d)
         self.h0, self.hh, self.logits = e(B, d), e(B, d), e(B, V)
+        self.part = e(16 * B * 4 * d)          # split-K partials of the narrow linears (<= 16 splits)
         self.use_graph = use_graph
         self.graph = None
 
@@ -52,13 +53,14 @@ class KVDecoder:
         K.layernorm_fwd_f32(x_in, P.f(pre + 'attn_layer_norm.weight'), P.f(pre + 'attn_layer_norm.bias'), self.h, B, d)
         # q | k | v weights and biases are adjacent in the arena: one [3d, d] operand; rotary on q and k
         K.dec_linear(self.h, P.f(a + 'q_linear.weight'), self.qkv, B, 3 * d, d, bias=P.f(a + 'q_linear.bias'),
-                     epi=EPI_ROTARY_BF16, rot=self.rot, rot_cols=2 * d, rot_d=d, cur=st.cur)
+                     epi=EPI_ROTARY_BF16, rot=self.rot, rot_cols=2 * d, rot_d=d, cur=st.cur, part=self.part)
         K.dec_attn(self.qkv, self.kc[i], self.vc[i], self.O, B, self.H, self.hd, self.T, st.cur, self.window)
         K.dec_linear(self.O, P.f(a + 'output_linear.weight'), self.x1, B, d, d, bias=P.f(a + 'output_linear.bias'),
-                     resid=x_in)
+                     resid=x_in, part=self.part)
         K.layernorm_fwd_f32(self.x1, P.f(pre + 'ffn_layer_norm.weight'), P.f(pre + 'ffn_layer_norm.bias'), self.h, B, d)
-        K.dec_linear(self.h, P.f(pre + 'ffn.0.weight'), self.f, B, 4 * d, d, bias=P.f(pre + 'ffn.0.bias'), epi=EPI_GELU)
-        K.dec_linear(self.f, P.f(pre + 'ffn.2.weight'), x_out, B, d, 4 * d, resid=self.x1)
+        K.dec_linear(self.h, P.f(pre + 'ffn.0.weight'), self.f, B, 4 * d, d, bias=P.f(pre + 'ffn.0.bias'), epi=EPI_GELU,
+                     part=self.part)
+        K.dec_linear(self.f, P.f(pre + 'ffn.2.weight'), x_out, B, d, 4 * d, resid=self.x1, part=self.part)
 
     def _step(self, first):
         P, B, d, st = self.P, self.B, self.d, self.st
@@ -74,7 +76,7 @@ class KVDecoder:
                 self._layer(i, self.x, self.x)
         # output_layer (transformer_language_model.py:55-63)
         K.dec_linear(self.x, P.f('output_layer.0.weight'), self.h0, B, d, d, bias=P.f('output_layer.0.bias'),
-                     epi=EPI_GELU)
+                     epi=EPI_GELU, part=self.part)
         K.layernorm_fwd_f32(self.h0, P.f('output_layer.2.weight'), P.f('output_layer.2.bias'), self.hh, B, d)
         K.dec_linear(self.hh, P.f('input_layer.0.weight'), self.logits, B, self.V, d, bias=P.f('output_layer.3.bias'))
         # GenerationState.process_logits (generation.py:30-77) on all rows; dead rows are skipped in-kernel

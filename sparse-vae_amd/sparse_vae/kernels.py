@@ -250,12 +250,13 @@ def layernorm_fwd_f32(x, w, b, y, rows, D):
 
 # ---- autoregressive decoding (f32; positions from the device scalar `cur`)
 def dec_linear(X, W, Y, M, N_, K_, *, bias=None, resid=None, epi=N.EPI_F32, rot=None, rot_cols=0, rot_d=0, cur=None,
-               ldx=None, ldw=None, ldy=None, ldr=None):
+               ldx=None, ldw=None, ldy=None, ldr=None, part=None):
+    """part: optional f32 workspace for split-K partials (the library splits narrow outputs when it fits)."""
     _dev(X, W, Y)
     assert X.dtype == f32 and W.dtype == f32 and Y.dtype == f32
     check(lib.svae_dec_linear(X.data_ptr(), ldx or K_, W.data_ptr(), ldw or K_, ptr(bias), Y.data_ptr(), ldy or N_,
-                              ptr(resid), ldr or N_, M, N_, K_, epi, ptr(rot), rot_cols, rot_d, ptr(cur), stream()),
-          'svae_dec_linear')
+                              ptr(resid), ldr or N_, M, N_, K_, epi, ptr(rot), rot_cols, rot_d, ptr(cur), ptr(part),
+                              part.numel() if part is not None else 0, stream()), 'svae_dec_linear')
 
 
 def dec_attn(qkv, kc, vc, O, B, H, hd, T, cur, window, scale=None, ldq=None, ldo=None):
