@@ -1,0 +1,61 @@
+"""Time the flash attention kernels alone at the C2 decoder shape (B=64, H=8, L=512, hd=64, q|k|v interleaved).
+
+    python scripts/attn_probe.py
+"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, 'sparse-vae_amd'))
+import torch  # noqa: E402
+from sparse_vae import kernels as K  # noqa: E402
+
+dev = torch.device('cuda', 0)
+
+
+def timeit(fn, reps=20):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps * 1e3
+
+
+def main():
+    for B, L, causal in [(64, 512, True), (64, 512, False), (16, 512, True), (256, 512, True), (64, 1024, True)]:
+      for with_o32 in (True, False):
+        H, hd = 8, 64
+        if not with_o32 and (B, L) != (64, 512):
+            continue
+        d = H * hd
+        qkv = torch.randn(B * L, 3 * d, device=dev).bfloat16()
+        o = torch.empty(B * L, d, device=dev).bfloat16()
+        o32 = torch.empty(B * L, d, device=dev)
+        lse = torch.empty(B, H, L, device=dev)
+        kw = dict(B=B, H=H, Lq=L, Lk=L, hd=hd, sq=3 * d, sk=3 * d, sv=3 * d, so=d, bq=L * 3 * d, bk=L * 3 * d,
+                  bv=L * 3 * d, bo=L * d, causal=causal, o32=o32 if with_o32 else None, so32=d, bo32=L * d)
+        fwd = lambda: K.attention(qkv, qkv[:, d:], qkv[:, 2 * d:], o, lse, **kw)
+        t = timeit(fwd)
+        fl = 4.0 * B * H * L * L * hd * (0.5 if causal else 1.0)
+        dout = torch.randn(B * L, d, device=dev).bfloat16()
+        dqkv = torch.empty(B * L, 3 * d, device=dev).bfloat16()
+        delta = torch.empty(B, H, L, device=dev)
+        part = torch.empty(K.attn_dq_part_elems(B, H, L, L, hd), device=dev)
+        bwd = lambda: K.attention(qkv, qkv[:, d:], qkv[:, 2 * d:], o, lse, backward=True, dout=dout, sdo=d, bdo=L * d,
+                                  delta=delta, dq_bf=dqkv, ldq_bf=3 * d, dk=dqkv[:, d:], dv=dqkv[:, 2 * d:], sdk=3 * d,
+                                  sdv=3 * d, bdk=L * 3 * d, bdv=L * 3 * d, dq_part=part, **kw)
+        if not with_o32:
+            print(f'B={B:4d} L={L:5d} causal={int(causal)} no-o32 fwd {t:8.1f} us', flush=True)
+            continue
+        tb = timeit(bwd)
+        print(f'B={B:4d} L={L:5d} causal={int(causal)}  fwd {t:8.1f} us {fl / t / 1e6:7.1f} TF/s   '
+              f'bwd(+delta+dq) {tb:8.1f} us {2.5 * fl / tb / 1e6:7.1f} TF/s', flush=True)
+
+
+if __name__ == '__main__':
+    main()

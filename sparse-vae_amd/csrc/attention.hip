@@ -110,10 +110,12 @@ __device__ __forceinline__ bf16x8 pack8(const f32x4& a, const f32x4& b) {
 
 constexpr float LOG2E = 1.4426950408889634f;
 
+
 // ===================================================================================== forward
 // One block = 128 queries of one (batch, head): 4 waves x 32 queries (two 16-query MFMA column tiles), so
-// every K fragment and V^T fragment read from LDS feeds two MFMAs. K/V tiles arrive by LDS-DMA NS - 1 tiles
-// ahead (a 4-stage ring for hd <= 64) with one counted wait + barrier per tile. Softmax in the exp2 domain with the raw
+// every K fragment and V^T fragment read from LDS feeds two MFMAs. K/V tiles arrive by LDS-DMA one tile ahead
+// (asm-issued, so the compiler adds no drain before the transposed V reads) with one counted wait + barrier per
+// tile; 3 blocks per CU for hd <= 64. Softmax in the exp2 domain with the raw
 // (unscaled) running max: p = exp2(s c - m c), c = scale log2(e). Masks only on edge tiles (causal diagonal,
 // ragged end, padded keys present); causal tiles entirely above a wave's queries are skipped.
 // s_waitcnt vmcnt(n) for a run-time n (the immediate must be a constant): n = vector-memory ops allowed to stay in
@@ -134,12 +136,13 @@ __device__ __forceinline__ void wait_vmcnt(int n) {
 }
 
 template <int HDP>
-__global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AP p) {
+__global__ __launch_bounds__(256, HDP == 64 ? 3 : 2) void attn_fwd_kernel(AP p) {
   using T = Tile<HDP>;
   constexpr int NKK = HDP / 32, NT = HDP / 16;
-  // K/V ring: NS stages of (K, V) tiles, filled NS - 1 key tiles ahead (one tile of compute is shorter than the
-  // HBM latency of the next tile); the key-padding bytes ride along in a [NS][64] ring
-  constexpr int NS = HDP == 64 ? 4 : 2;
+  // K/V ring: NS stages of (K, V) tiles filled NS - 1 key tiles ahead; the key-padding bytes ride along in an
+  // [NS][64] ring. Measured at the C2 shape (hd 64): 2 stages at 3 blocks / CU (33 KB LDS, <= 170 VGPRs) beat
+  // 3 or 4 stages at 2 blocks / CU (73.5 vs 78.4 / 92 us): blocks in flight, not prefetch depth, set the time.
+  constexpr int NS = 2;
   constexpr int DMA_OPS = 2 * (64 * T::PITCH / 1024) / 4;   // buffer_load_lds per wave per (K, V) tile
   __shared__ __attribute__((aligned(16))) char smem[NS * 2 * T::BYTES + NS * 64 * 4];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, li = lane & 15;
@@ -187,15 +190,16 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AP p) {
     if (pad && w == 0) dma1_lds(prs, pm + (it2 % NS) * 64, kn + lane < p.Lk ? kn + lane : 0x7FFFFFF0);
   };
   if (!pad && tid < NS * 64) pm[tid] = 0;
-  // Consume the Q fragments before the ring starts, so the compiler's wait for them (it cannot see the DMA)
-  // is not a vmcnt(0) inside the loop.
+#pragma unroll
+  for (int s2 = 0; s2 < NS - 1; ++s2)
+    if (s2 < nvisit) issue(s2);
+  // Consume the Q fragments here (after the ring's first DMA is in flight, so the two latencies overlap): the
+  // compiler cannot see the DMA, so its wait for them is a vmcnt(0); here that costs nothing (tile 0 is needed
+  // next anyway), inside the loop it would drain the ring.
 #pragma unroll
   for (int j = 0; j < 2; ++j)
 #pragma unroll
     for (int kk = 0; kk < NKK; ++kk) asm volatile("" ::"v"(__builtin_bit_cast(u32x4, qf[j][kk])));
-#pragma unroll
-  for (int s2 = 0; s2 < NS - 1; ++s2)
-    if (s2 < nvisit) issue(s2);
 
   for (int it = 0; it < nvisit; ++it) {
     const int kt = it == 0 ? 0 : kt1 + it - 1;
