@@ -14,6 +14,7 @@ Numerics: GEMM/attention operands bf16 with f32 accumulation; residual stream, L
 mu/logvar, KL, softmax statistics and all gradients of the residual stream in f32.
 """
 import math
+import os
 from collections import OrderedDict
 
 import torch
@@ -167,15 +168,26 @@ class FlatParams:
 
 # ---------------------------------------------------------------------------------------- workspace
 class Workspace:
+    """Named device buffers reused across steps. A buffer still being read by the weight-gradient stream is
+    fenced: get() makes the caller's stream wait for that read before handing the buffer out again."""
+
     def __init__(self, device):
         self.device = device
         self.bufs = {}
+        self.busy = {}      # storage data_ptr -> event recorded after the last side-stream read
+
+    def fence(self, t):
+        ev = self.busy.pop(t.untyped_storage().data_ptr(), None)
+        if ev is not None:
+            torch.cuda.current_stream().wait_event(ev)
 
     def get(self, name, shape, dtype=bf16, zero=False):
         t = self.bufs.get(name)
         if t is None or t.shape != torch.Size(shape) or t.dtype != dtype:
             t = torch.empty(shape, dtype=dtype, device=self.device)
             self.bufs[name] = t
+        if self.busy:
+            self.fence(t)
         if zero:
             t.zero_()
         return t
@@ -214,6 +226,13 @@ class VAEEngine:
         self.window = getattr(hp, 'attn_window', 0)     # decoder self-attention: 0 dense, > 0 sliding window
         self.saved = None
         self.probe = None      # list -> HIP events around each vocab-head GEMM launch (bench roofline)
+        # SVAE_DW_STREAM=1: weight-gradient GEMMs on a second stream, off the dX critical path of the backward
+        # (they feed nothing else in it). Measured at C2: 15.33 vs 15.37 ms/step -- the overlap is eaten by
+        # contention (LayerNorm backward 35 -> 85 us beside a GEMM, the head dW doubled beside the head dX), so
+        # the default keeps one stream.
+        self.side = None
+        if flat.device.type == 'cuda' and os.environ.get('SVAE_DW_STREAM', '0') != '0':
+            self.side = torch.cuda.Stream(device=flat.device)
 
     # ------------------------------------------------------------------ helpers
     def rot(self, L, window=0):
@@ -241,12 +260,27 @@ class VAEEngine:
         wg = self.P.grad[self.P.offsets[name + '.weight'][0]:][:2 * D]   # [weight | bias] grads (adjacent)
         K.layernorm_bwd(dy, x, self.P.f(name + '.weight'), mean, rstd, dres, dx, dx_bf, wg, rows, D, part)
 
-    def _dw(self, dY, X, wname, rows, n_out, n_in, ldy=None, ldx=None, bias=None):
+    def _dw(self, dY, X, wname, rows, n_out, n_in, ldy=None, ldx=None, bias=None, on_side=True):
         bg = None
         if bias is not None:
             off = self.P.offsets[bias][0]
             bg = self.P.grad[off:off + n_out]
-        K.linear_dw(dY, X, self.P.g(wname), rows, n_out, n_in, ldy, ldx, bgrad=bg)
+        side = self.side if on_side else None
+        if side is None:
+            K.linear_dw(dY, X, self.P.g(wname), rows, n_out, n_in, ldy, ldx, bgrad=bg)
+            return
+        side.wait_stream(torch.cuda.current_stream())       # dY (and X) are written
+        with torch.cuda.stream(side):
+            K.linear_dw(dY, X, self.P.g(wname), rows, n_out, n_in, ldy, ldx, bgrad=bg)
+        ev = torch.cuda.Event()
+        ev.record(side)
+        self.ws.busy[dY.untyped_storage().data_ptr()] = ev   # the next writer of dY's buffer waits for this read
+
+    def join_side(self):
+        """The caller's stream waits for every weight-gradient GEMM issued so far."""
+        if self.side is not None:
+            torch.cuda.current_stream().wait_stream(self.side)
+            self.ws.busy.clear()
 
     def _db(self, dY, bname, rows, cols, ld=None):
         off = self.P.offsets[bname][0]
@@ -704,7 +738,14 @@ class VAEEngine:
         """Gradients of loss = nll + kl_weight * kl into the flat gradient arena (accumulating). `ready(end)`
         is called each time the arena prefix [0, end) holds final gradients (data-parallel bucketing)."""
         sv, hp, d, ws, P = self.saved, self.hp, self.d, self.ws, self.P
-        ready = ready or (lambda end: None)
+        if ready is None:
+            ready = lambda end: None        # noqa: E731
+        else:                               # a bucket's gradients must be complete before its all-reduce
+            user_ready = ready
+
+            def ready(end):
+                self.join_side()
+                user_ready(end)
         if sv is None:
             raise RuntimeError('backward() without a saved forward')
         B, L = sv['B'], sv['L']
@@ -716,7 +757,8 @@ class VAEEngine:
         # ---- head
         logits = sv['logits']
         K.ce_grad(logits, V, sv['lse'], sv['chunk_w'], sv['labels'], gs[0:1], T, V, L, sv['nchunks'], sv['chunk_len'])
-        self._dw(logits, sv['hh'], 'input_layer.0.weight', T, V, d, bias='output_layer.3.bias')
+        # (the vocabulary-head dW stays in order: next to the equally large head dX it only contends)
+        self._dw(logits, sv['hh'], 'input_layer.0.weight', T, V, d, bias='output_layer.3.bias', on_side=False)
         dhh = ws.get('b.dhh', (T, d))
         K.gemm(logits, P.wT('input_layer.0.weight', V, d), dhh, T, d, V, epi=EPI_BF16)
         dh0 = ws.get('b.dh0', (T, d), f32)
@@ -772,11 +814,14 @@ class VAEEngine:
         if st0['resid']:   # L == num_latents: the first layer keeps its residual (transformer_layer.py:49)
             tmp = ws.get('b.dfirst', (T, d), f32)
             self.layer_bwd(st0, dcur, tmp)
+            self.join_side()        # the tied weight's head gradient (side stream) before the scatter-add
             K.embedding_bwd(sv['ids32'], tmp, P.g('input_layer.0.weight'), T, d)
         else:
             self.layer_bwd(st0, dcur, dx_emb, dx_accumulate=True)
 
         ready(P.end('encoder.first_layer.ffn_layer_norm.bias'))
         # ---- embedding (tied with the head weight)
+        self.join_side()            # the tied weight's head gradient (side stream) before the scatter-add
         K.embedding_bwd(sv['ids32'], dx_emb, P.g('input_layer.0.weight'), T, d)
         ready(P.n_live)
+        self.join_side()

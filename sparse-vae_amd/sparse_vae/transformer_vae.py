@@ -253,7 +253,7 @@ class TransformerVAE(ContinuousVAEHooks, LanguageModel):
         g = gloss.reshape(()).to(torch.float32)
         if self._dp is not None:
             g = g / self._dp['world']
-        eng.backward(g, self._kl_weight_used, ready=self._dp_ready)
+        eng.backward(g, self._kl_weight_used, ready=self._dp_ready if self._dp is not None else None)
         self._dp_finish()
         self._norm_valid = False
 
