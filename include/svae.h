@@ -159,11 +159,11 @@ int svae_reparam_kl_bwd(const float* stats, const float* eps, const float* dz, c
  * Row r is position (r % seq) of its sequence; label 0 = ignore_index. The sequence positions are cut
  * into nchunks chunks of chunk_len (torch.chunk semantics) and nll = mean over chunks of the per-chunk
  * mean loss. finalize: lse[rows], row_loss[rows], chunk_w[nchunks] (= 1 / (count_c * nchunks)),
- * nll_out[1]. grad: in place, logits -> gscale[0] * chunk_w[c] * (softmax - onehot) in bf16 (0 for
+ * nll_out[1]; red_ws: f32 workspace of >= 1024 floats (per-block chunk partials, added in a fixed order). grad: in place, logits -> gscale[0] * chunk_w[c] * (softmax - onehot) in bf16 (0 for
  * ignored rows); dbias (optional, f32 [V]) += column sums of dlogits (output-bias gradient). nchunks <= 8. */
 int svae_ce_finalize(const float* part, int32_t ntile, const float* label_logit, const int32_t* labels,
                      int32_t rows, int32_t seq, int32_t nchunks, int32_t chunk_len, float* lse, float* row_loss,
-                     float* chunk_w, float* nll_out, svae_stream_t stream);
+                     float* chunk_w, float* nll_out, float* red_ws, svae_stream_t stream);
 int svae_ce_grad(void* logits, int64_t ld, const float* lse, const float* chunk_w, const int32_t* labels,
                  const float* gscale, float* dbias, int32_t rows, int32_t V, int32_t seq, int32_t nchunks,
                  int32_t chunk_len, svae_stream_t stream);
@@ -209,6 +209,13 @@ int svae_attn_fwd_f32(const float* q, const float* k, const float* v, float* o, 
                       svae_stream_t stream);
 int svae_layernorm_fwd_f32(const float* x, const float* w, const float* b, float* y, int32_t rows, int32_t D,
                            svae_stream_t stream);
+
+/* ---- mutual-information log (transformer_vae.py:59-61, math_utils.py:51-58) ---------------------------
+ * out[0] = kl[0] - marginal_kl(q), q = N(mu, exp(logvar)) from stats [B][2Z] (mu | logvar), with S posterior
+ * samples per sequence: eps f32 [S][B][Z] or NULL (counter-based normals from seed). ws: f32 workspace of
+ * >= 2 * S * B floats. Log-only diagnostic (not in the loss). */
+int svae_mutual_info(const float* stats, const float* eps, uint64_t seed, const float* kl, int32_t B, int32_t Z,
+                     int32_t S, float* ws, float* out, svae_stream_t stream);
 
 /* ---- evaluation: log p(x|z) per sequence (continuous_autoencoder.py:82-88) ---------------------------
  * From the SVAE_EPI_CE_STATS partials of the head GEMM (which may run with C = NULL: no logits stored):

@@ -152,23 +152,105 @@ __global__ __launch_bounds__(256) void ce_seq_logprob_kernel(const float* __rest
   if (threadIdx.x == 0) out[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
 }
 
-// Chunked mean-of-means (robust_cross_entropy): single block; writes nll and per-chunk row weights.
-__global__ __launch_bounds__(1024) void ce_reduce_kernel(const float* __restrict__ row_loss, const int* __restrict__ labels,
-                                                         int rows, int seq, int nchunks, int chunk_len,
-                                                         float* __restrict__ chunk_w, float* __restrict__ nll_out) {
-  __shared__ float ssum[32][8];
-  __shared__ float scnt[32][8];
+// ------------------------------------------------------------------ marginal KL (mutual-information log)
+// math_utils.py:51-58: S posterior samples x[s][i] = mu_i + eps * scale_i; log q_j(x) summed over the latent;
+// marginal[s][i] = logsumexp_j log q_j(x[s][i]) - log B. One block per (s, i), a thread per posterior j; the block
+// also sums x^2. Partials go to ws[s*B + i] (marginal) and ws[S*B + s*B + i] (sum x^2); mi_final reduces them in
+// a fixed order: mi = kl - (sample_prob - mean(marginal)), sample_prob = -0.5 (mean sum x^2 + Z log 2 pi).
+__global__ __launch_bounds__(256) void mi_marginal_kernel(const float* __restrict__ stats, const float* __restrict__ eps,
+                                                          unsigned long long seed, int B, int Z,
+                                                          float* __restrict__ ws) {
+  extern __shared__ float xs[];            // [Z] the sample
+  __shared__ float red[8];
+  const int si = blockIdx.x, i = si % B, tid = threadIdx.x;
+  const int lane = tid & 63, w = tid >> 6;
+  float sq = 0.f;
+  for (int z = tid; z < Z; z += 256) {
+    const float mu = stats[(long long)i * 2 * Z + z];
+    const float sd = sqrtf(__expf(stats[(long long)i * 2 * Z + Z + z]));
+    float e;
+    if (eps) {
+      e = eps[(long long)si * Z + z];
+    } else {
+      const unsigned long long idx = ((unsigned long long)si * Z + z) * 2ull;
+      const float u1 = rand_uniform(seed, idx), u2 = rand_uniform(seed, idx + 1);
+      e = sqrtf(-2.f * __logf(u1)) * __cosf(6.283185307179586f * u2);
+    }
+    const float x = mu + e * sd;
+    xs[z] = x;
+    sq += x * x;
+  }
+  __syncthreads();
+  // log q_j(x) = sum_z -(x - mu)^2 / (2 var) - log(sd) - log(sqrt(2 pi)); a thread's j's fold into an online
+  // logsumexp (m, e), then the block combines the 256 pairs
+  const float lsq2pi = 0.91893853320467274f;   // log(sqrt(2 pi))
+  float m = -INFINITY, e = 0.f;
+  for (int j = tid; j < B; j += 256) {
+    const float* st = stats + (long long)j * 2 * Z;
+    float acc = 0.f;
+    for (int z = 0; z < Z; ++z) {
+      const float lv = st[Z + z];
+      const float d = xs[z] - st[z];
+      acc += -(d * d) * (0.5f * __expf(-lv)) - 0.5f * lv - lsq2pi;
+    }
+    const float nm = fmaxf(m, acc);
+    e = e * __expf(m - nm) + __expf(acc - nm);
+    m = nm;
+  }
+  float mx = wave_max(m);
+  if (lane == 0) red[w] = mx;
+  __syncthreads();
+  mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  __syncthreads();
+  float se = wave_sum(m == -INFINITY ? 0.f : e * __expf(m - mx));
+  sq = wave_sum(sq);
+  if (lane == 0) { red[w] = se; red[4 + w] = sq; }
+  __syncthreads();
+  if (tid == 0) {
+    ws[si] = mx + __logf(red[0] + red[1] + red[2] + red[3]) - __logf((float)B);
+    ws[gridDim.x + si] = red[4] + red[5] + red[6] + red[7];
+  }
+}
+
+__global__ __launch_bounds__(256) void mi_final_kernel(const float* __restrict__ ws, int n, int Z,
+                                                       const float* __restrict__ kl, float* __restrict__ out) {
+  __shared__ float red[8];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  float m = 0.f, q = 0.f;
+  for (int k = tid; k < n; k += 256) { m += ws[k]; q += ws[n + k]; }
+  m = wave_sum(m);
+  q = wave_sum(q);
+  if (lane == 0) { red[w] = m; red[4 + w] = q; }
+  __syncthreads();
+  if (tid == 0) {
+    const float mm = (red[0] + red[1] + red[2] + red[3]) / n;
+    const float qq = (red[4] + red[5] + red[6] + red[7]) / n;
+    const float sample_prob = -0.5f * (qq + Z * 1.8378770664093453f);   // log(2 pi)
+    out[0] = kl[0] - (sample_prob - mm);
+  }
+}
+
+// Chunked mean-of-means (robust_cross_entropy): CE_RED_BLOCKS blocks write per-chunk (sum, count) partials, one
+// small block adds them in a fixed order and writes nll and the per-chunk row weights (deterministic).
+constexpr int CE_RED_BLOCKS = 64;
+
+__global__ __launch_bounds__(1024) void ce_reduce_part_kernel(const float* __restrict__ row_loss,
+                                                              const int* __restrict__ labels, int rows, int seq,
+                                                              int nchunks, int chunk_len, float* __restrict__ part) {
+  __shared__ float ssum[16][8];
+  __shared__ float scnt[16][8];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;   // 16 waves
   float s[8], c[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) { s[k] = 0.f; c[k] = 0.f; }
-  for (int r = threadIdx.x; r < rows; r += 1024) {
+  for (int r = blockIdx.x * 1024 + threadIdx.x; r < rows; r += CE_RED_BLOCKS * 1024) {
     const int pos = r % seq;
     const int ch = min(pos / chunk_len, nchunks - 1);
+    const float l = row_loss[r];
     if (labels[r] != 0) {
 #pragma unroll
       for (int k = 0; k < 8; ++k)
-        if (k == ch) { s[k] += row_loss[r]; c[k] += 1.f; }
+        if (k == ch) { s[k] += l; c[k] += 1.f; }
     }
   }
 #pragma unroll
@@ -178,14 +260,28 @@ __global__ __launch_bounds__(1024) void ce_reduce_kernel(const float* __restrict
     for (int k = 0; k < 8; ++k) { ssum[wave][k] = s[k]; scnt[wave][k] = c[k]; }
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
+  if (threadIdx.x < 16) {
+    const int k = threadIdx.x & 7;
+    float t = 0.f;
+    for (int w = 0; w < 16; ++w) t += threadIdx.x < 8 ? ssum[w][k] : scnt[w][k];
+    part[blockIdx.x * 16 + threadIdx.x] = t;
+  }
+}
+
+__global__ __launch_bounds__(64) void ce_reduce_final_kernel(const float* __restrict__ part, int nchunks,
+                                                             float* __restrict__ chunk_w, float* __restrict__ nll_out) {
+  __shared__ float mean[8];
+  const int k = threadIdx.x;
+  if (k < nchunks) {
+    float ts = 0.f, tc = 0.f;
+    for (int b = 0; b < CE_RED_BLOCKS; ++b) { ts += part[b * 16 + k]; tc += part[b * 16 + 8 + k]; }
+    mean[k] = ts / tc;
+    chunk_w[k] = 1.0f / (tc * (float)nchunks);
+  }
+  __syncthreads();
+  if (k == 0) {
     float nll = 0.f;
-    for (int k = 0; k < nchunks; ++k) {
-      float ts = 0.f, tc = 0.f;
-      for (int w = 0; w < 16; ++w) { ts += ssum[w][k]; tc += scnt[w][k]; }
-      nll += ts / tc;
-      chunk_w[k] = 1.0f / (tc * (float)nchunks);
-    }
+    for (int j = 0; j < nchunks; ++j) nll += mean[j];
     nll_out[0] = nll / nchunks;
   }
 }
@@ -456,14 +552,26 @@ SVAE_EXPORT int svae_reparam_kl_bwd(const float* stats, const float* eps, const 
 
 SVAE_EXPORT int svae_ce_finalize(const float* part, int32_t ntile, const float* label_logit, const int32_t* labels,
                                  int32_t rows, int32_t seq, int32_t nchunks, int32_t chunk_len, float* lse,
-                                 float* row_loss, float* chunk_w, float* nll_out, svae_stream_t stream) {
-  if (!part || !label_logit || !labels || !lse || !row_loss || !chunk_w || !nll_out) return SVAE_EINVAL;
+                                 float* row_loss, float* chunk_w, float* nll_out, float* red_ws, svae_stream_t stream) {
+  if (!part || !label_logit || !labels || !lse || !row_loss || !chunk_w || !nll_out || !red_ws) return SVAE_EINVAL;
   if (rows <= 0 || ntile <= 0 || seq <= 0 || nchunks <= 0 || nchunks > 8 || chunk_len <= 0) return SVAE_EINVAL;
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(ce_rows_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, part, ntile, label_logit, labels, rows, lse,
                      row_loss);
-  hipLaunchKernelGGL(ce_reduce_kernel, dim3(1), dim3(1024), 0, s, row_loss, labels, rows, seq, nchunks, chunk_len,
-                     chunk_w, nll_out);
+  hipLaunchKernelGGL(ce_reduce_part_kernel, dim3(CE_RED_BLOCKS), dim3(1024), 0, s, row_loss, labels, rows, seq, nchunks,
+                     chunk_len, red_ws);
+  hipLaunchKernelGGL(ce_reduce_final_kernel, dim3(1), dim3(64), 0, s, red_ws, nchunks, chunk_w, nll_out);
+  SVAE_LAUNCH_CHECK();
+  return SVAE_OK;
+}
+
+SVAE_EXPORT int svae_mutual_info(const float* stats, const float* eps, uint64_t seed, const float* kl, int32_t B,
+                                 int32_t Z, int32_t S, float* ws, float* out, svae_stream_t stream) {
+  if (!stats || !kl || !ws || !out || B <= 0 || Z <= 0 || S <= 0 || Z > 4096) return SVAE_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(mi_marginal_kernel, dim3(S * B), dim3(256), (size_t)Z * sizeof(float), s, stats, eps,
+                     (unsigned long long)seed, B, Z, ws);
+  hipLaunchKernelGGL(mi_final_kernel, dim3(1), dim3(256), 0, s, ws, S * B, Z, kl, out);
   SVAE_LAUNCH_CHECK();
   return SVAE_OK;
 }

@@ -77,7 +77,7 @@ _SIGS = {
                             c_void_p, c_int32, c_int32, c_void_p],
     'svae_reparam_kl_bwd': [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p],
     'svae_ce_finalize': [c_void_p, c_int32, c_void_p, c_void_p, c_int32, c_int32, c_int32, c_int32, c_void_p,
-                         c_void_p, c_void_p, c_void_p, c_void_p],
+                         c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     'svae_ce_grad': [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_int32,
                      c_int32, c_int32, c_void_p],
     'svae_dropout_bwd_cast': [c_void_p, c_void_p, c_float, c_uint64, c_int64, c_int32, c_int64, c_void_p],
@@ -104,6 +104,8 @@ _SIGS = {
     'svae_dec_sample': [c_void_p, c_int64, c_int32, c_int32, c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_int32,
                         c_float, c_int32, c_float, c_uint64, c_void_p, c_void_p],
     'svae_dec_advance': [c_void_p, c_void_p],
+    'svae_mutual_info': [c_void_p, c_void_p, c_uint64, c_void_p, c_int32, c_int32, c_int32, c_void_p, c_void_p,
+                         c_void_p],
     'svae_version': [],
 }
 

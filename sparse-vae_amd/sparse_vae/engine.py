@@ -540,7 +540,7 @@ class VAEEngine:
         loss = nll[0] + kl_weight * kl[0]                                          # transformer_vae.py:55
         self.saved = sv
         return {'loss': loss, 'nll': nll[0], 'kl': kl[0], 'train_kl': kl[1], 'raw_kl': raw_kl,
-                'mu': stats[:, :Z], 'logvar': stats[:, Z:], 'z': zf, 'eps': eps_buf,
+                'mu': stats[:, :Z], 'logvar': stats[:, Z:], 'stats': stats, 'kl_buf': kl, 'z': zf, 'eps': eps_buf,
                 'logits': logits if need_logits else None}
 
     def _encode(self, x_emb, B, L, padm, dropout, seed):
@@ -576,6 +576,20 @@ class VAEEngine:
             padm = self.ws.get('pad', (B, L), torch.uint8)
             padm.copy_(ids.eq(0) if pad is True else pad)
         return ids32, padm
+
+    def mutual_info(self, out, eps=None, num_samples=10):
+        """kl - marginal_kl(q) for the step's posterior (transformer_vae.py:59-61, math_utils.py:51-58) in one
+        fused kernel pair; eps [num_samples, B, Z] f32 or None (drawn in-kernel from a torch-RNG seed).
+        Returns a fresh 0-d f32 tensor (the step's workspace is reused by the next step)."""
+        stats = out['stats']
+        B, Z = stats.shape[0], stats.shape[1] // 2
+        if eps is not None:
+            eps = eps.to(stats.device, f32).reshape(num_samples, B, Z).contiguous()
+        ws = self.ws.get('mi_ws', (2 * num_samples * B,), f32)
+        res = torch.empty((), dtype=f32, device=stats.device)
+        seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+        K.mutual_info(stats, out['kl_buf'], B, Z, seed, res, ws, eps=eps, S=num_samples)
+        return res
 
     def posterior(self, ids, pad=True):
         """q(z|x) without the decoder (transformer_vae.py:73-74, :81-83): stats f32 [B, 2Z] = mu | logvar."""

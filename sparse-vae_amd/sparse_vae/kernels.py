@@ -177,10 +177,24 @@ def reparam_bwd(stats, eps, dz, ntok, gkl, dstats, B, Z):
                                   dstats.data_ptr(), B, Z, stream()), 'svae_reparam_kl_bwd')
 
 
+_ce_red = {}
+
+
 def ce_finalize(part, ntile, label_logit, labels, rows, seq, nchunks, chunk_len, lse, row_loss, chunk_w, nll):
+    red = _ce_red.get(part.device)
+    if red is None:
+        red = _ce_red[part.device] = torch.empty(1024, dtype=f32, device=part.device)
     check(lib.svae_ce_finalize(part.data_ptr(), ntile, label_logit.data_ptr(), labels.data_ptr(), rows, seq,
                                nchunks, chunk_len, lse.data_ptr(), row_loss.data_ptr(), chunk_w.data_ptr(),
-                               nll.data_ptr(), stream()), 'svae_ce_finalize')
+                               nll.data_ptr(), red.data_ptr(), stream()), 'svae_ce_finalize')
+
+
+def mutual_info(stats, kl, B, Z, seed, out, ws, eps=None, S=10):
+    """out[0] = kl[0] - marginal_kl (math_utils.py:51-58) over S posterior samples; eps [S, B, Z] or in-kernel."""
+    _dev(stats, kl, out, ws)
+    assert ws.numel() >= 2 * S * B
+    check(lib.svae_mutual_info(stats.data_ptr(), ptr(eps), seed & 0xFFFFFFFFFFFFFFFF, kl.data_ptr(), B, Z, S,
+                               ws.data_ptr(), out.data_ptr(), stream()), 'svae_mutual_info')
 
 
 def ce_seq_logprob(part, ntile, label_logit, labels, rows, seq, out):

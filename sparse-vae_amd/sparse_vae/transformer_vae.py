@@ -18,7 +18,7 @@ from torch import nn
 from torch.distributions.normal import Normal
 
 from .core import (ContinuousVAEHparams, ContinuousVAEHooks, ConditionalGaussian, LanguageModel, Perceiver,
-                   TransformerHparams, TransformerLayer, VOCAB_SIZE, marginal_kl)
+                   TransformerHparams, TransformerLayer, VOCAB_SIZE)
 from .core.padded_tensor import PaddedTensor
 from .engine import FlatParams, VAEEngine
 from .core.generation import GenerationState
@@ -211,9 +211,10 @@ class TransformerVAE(ContinuousVAEHooks, LanguageModel):
         return ids, pad, ntok
 
     def training_step(self, batch: Dict[str, Any], batch_index: int = 0, stage: str = 'train', eps=None,
-                      dropout: Optional[float] = None):
-        """transformer_vae.py:42-66. `eps` (injected N(0,1) noise [B,1,latent]) and `dropout` override the
-        in-kernel noise / the nn.Dropout(0.1) rate for parity runs."""
+                      dropout: Optional[float] = None, eps_marginal=None):
+        """transformer_vae.py:42-66. `eps` (injected N(0,1) noise [B,1,latent]), `eps_marginal` (the 10
+        marginal_kl draws [10,B,1,latent]) and `dropout` override the in-kernel noise / the nn.Dropout(0.1) rate
+        for parity runs."""
         eng = self._require_engine()
         ids, pad, ntok = self._batch_inputs(batch)
         train = stage == 'train' and self.training
@@ -229,7 +230,8 @@ class TransformerVAE(ContinuousVAEHooks, LanguageModel):
         mu, logvar = out['mu'].view(-1, 1, self.hparams.latent_depth), out['logvar'].view(-1, 1, self.hparams.latent_depth)
         scale = logvar.exp().sqrt()
         if ids.shape[0] > 1 and self.hparams.get('log_mutual_info', True):
-            self.log(stage + '_mc_mutual_info', out['kl'] - marginal_kl(mu, scale))   # transformer_vae.py:59-61
+            # transformer_vae.py:59-61: kl - marginal_kl(posterior), fused (engine.mutual_info)
+            self.log(stage + '_mc_mutual_info', eng.mutual_info(out, eps=eps_marginal))
         if stage == 'train':
             loss = _StepFn.apply(self._anchor, self, out['loss'])
             return {'loss': loss, 'posterior': Normal(loc=mu.detach(), scale=scale.detach())}

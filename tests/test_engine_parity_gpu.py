@@ -102,3 +102,42 @@ def test_sparse_step_matches_oracle(name, window):
     print(f'[{name} w{window}] loss {loss:.6f} ref {ref["loss"].item():.6f}\n' + msg)
     assert worst[0][0] > 0.98, msg
     assert all(0.95 < r < 1.05 for _, r, _ in worst), msg
+
+
+@pytest.mark.parametrize('name', ['tiny_pad', 'small6_pad', 'c2shape'])
+def test_mutual_info_matches_oracle(name):
+    """The fused mutual-information log (engine.mutual_info: kl - marginal_kl, transformer_vae.py:59-61) with the
+    fixture's 10 marginal draws injected. Against oracle.marginal_kl on the engine's own mu/logvar: 1e-4 rel
+    (same f32 inputs, different summation order); against the reference's logged value: 2e-2 (the posterior
+    comes out of the bf16 encoder)."""
+    g, hp, params, ids = setup(name)
+    ntok = torch.from_numpy(g['lens'])
+    eps10 = torch.from_numpy(g['eps10'])
+    flat, eng = _build(hp, params)
+    out = eng.forward(ids.cuda(), ntok.cuda(), eps=torch.from_numpy(g['eps']).cuda(), dropout=0.0,
+                      kl_weight=float(g['kl_weight']))
+    mi = eng.mutual_info(out, eps=eps10.cuda()).item()
+    mu = out['mu'].double().cpu().view(-1, 1, 64)
+    scale = out['logvar'].double().cpu().exp().sqrt().view(-1, 1, 64)
+    want = out['kl'].item() - oracle.marginal_kl(mu, scale, eps10.double()).item()
+    assert abs(mi - want) < 1e-4 * max(1.0, abs(want)), (mi, want)
+    assert abs(mi - float(g['mutual_info'])) < 2e-2 * max(1.0, abs(float(g['mutual_info']))), (mi, g['mutual_info'])
+
+
+def test_mutual_info_in_kernel_draws():
+    """eps=None draws the 10 x B x Z normals in-kernel (counter-based Box-Muller). The estimator's mean over 300
+    seeds matches the mean over 300 torch.randn draws through the oracle within 6 standard errors."""
+    g, hp, params, ids = setup('tiny_pad')
+    flat, eng = _build(hp, params)
+    out = eng.forward(ids.cuda(), torch.from_numpy(g['lens']).cuda(), eps=torch.from_numpy(g['eps']).cuda(),
+                      dropout=0.0, kl_weight=float(g['kl_weight']))
+    torch.manual_seed(3)
+    ours = torch.stack([eng.mutual_info(out) for _ in range(300)]).double().cpu()
+    mu = out['mu'].double().cpu().view(-1, 1, 64)
+    scale = out['logvar'].double().cpu().exp().sqrt().view(-1, 1, 64)
+    kl = out['kl'].item()
+    theirs = torch.stack([kl - oracle.marginal_kl(mu, scale, torch.randn((10,) + tuple(mu.shape), dtype=torch.float64))
+                          for _ in range(300)])
+    assert torch.isfinite(ours).all() and ours.std() > 0
+    se = ((ours.var() + theirs.var()) / 300).sqrt().item()
+    assert abs(ours.mean().item() - theirs.mean().item()) < 6 * se + 1e-6, (ours.mean(), theirs.mean(), se)
