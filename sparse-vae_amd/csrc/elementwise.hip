@@ -289,6 +289,12 @@ __global__ __launch_bounds__(64) void ce_reduce_final_kernel(const float* __rest
 // dlogits = g * w_chunk * (softmax - onehot), in place on bf16 logits, fused with the output-bias gradient
 // db[v] += sum_rows dlogits[row][v] (the reference's autograd sums it separately). Block = 256 threads x 8
 // columns = a 2048-column strip, walking `rows_per_block` rows: every row is one contiguous 4 KiB read+write.
+// logits are read once and dlogits are consumed by the next GEMMs from HBM (2 GiB at C2, far beyond the caches):
+// nontemporal loads/stores (797 vs 869 us in the C2 step, scripts/ce_probe.py and scripts/_ab_run.sh); 2 rows in
+// flight per thread measured best (4: 814, 8: 818 us)
+#define CE_U 2
+#define CE_LOAD(p) __builtin_nontemporal_load(p)
+#define CE_STORE(v, p) __builtin_nontemporal_store(v, p)
 __global__ __launch_bounds__(256) void ce_grad_kernel(bf16* __restrict__ logits, long long ld, const float* __restrict__ lse,
                                                       const float* __restrict__ chunk_w, const int* __restrict__ labels,
                                                       const float* __restrict__ gscale, float* __restrict__ dbias, int rows,
@@ -299,15 +305,15 @@ __global__ __launch_bounds__(256) void ce_grad_kernel(bf16* __restrict__ logits,
   const float g = gscale[0];
   float db[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if (c0 < V) {
-    // 4 rows per iteration with all loads issued before any store (the stores would otherwise order the next
+    // CE_U rows per iteration with all loads issued before any store (the stores would otherwise order the next
     // row's load behind them: one HBM round trip per row)
-    for (int row = r0; row < r1; row += 4) {
-      bf16x8 v[4];
+    for (int row = r0; row < r1; row += CE_U) {
+      bf16x8 v[CE_U];
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
-        if (row + u < r1) v[u] = *(const bf16x8*)(logits + (long long)(row + u) * ld + c0);
+      for (int u = 0; u < CE_U; ++u)
+        if (row + u < r1) v[u] = CE_LOAD((const bf16x8*)(logits + (long long)(row + u) * ld + c0));
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < CE_U; ++u) {
         const int rr = row + u;
         if (rr >= r1) break;
         bf16x8* ptr = (bf16x8*)(logits + (long long)rr * ld + c0);
@@ -328,7 +334,7 @@ __global__ __launch_bounds__(256) void ce_grad_kernel(bf16* __restrict__ logits,
             o[e] = f2bf(d);
           }
         }
-        *ptr = o;
+        CE_STORE(o, ptr);
       }
     }
     if (dbias) {

@@ -719,6 +719,7 @@ __device__ __forceinline__ unsigned pack_bf16x2(float a, float b) {
 // Store the bf16 of two fragments' column groups x (cols 16ja + 4g..) and y (cols 16ja + 16 + 4g..) of one row
 // as 16-B vectors: a permlane16 swap gives lane group g 8 consecutive columns (g0: 0-7, g2: 8-15, g1: 16-23,
 // g3: 24-31 of the pair), so each instruction writes 16 rows x 64 contiguous bytes.
+template <bool NT = false>
 __device__ __forceinline__ void store_pair_bf16(bf16* row_base, int colbase, int ncols_left, const f32x4& x,
                                                 const f32x4& y, int g) {
   const unsigned x0 = pack_bf16x2(x[0], x[1]), x1 = pack_bf16x2(x[2], x[3]);
@@ -727,8 +728,10 @@ __device__ __forceinline__ void store_pair_bf16(bf16* row_base, int colbase, int
   const auto s1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
   const int c = colbase + ((g & 1) ? 16 : 0) + ((g & 2) ? 8 : 0);
   const u32x4 w = {s0[0], s1[0], s0[1], s1[1]};
-  if (c + 8 <= ncols_left) *(u32x4*)(row_base + c) = w;
-  else if (c < ncols_left) *(u32x2*)(row_base + c) = (u32x2){w[0], w[1]};
+  if (c + 8 <= ncols_left) {
+    if constexpr (NT) __builtin_nontemporal_store(w, (u32x4*)(row_base + c));
+    else *(u32x4*)(row_base + c) = w;
+  } else if (c < ncols_left) *(u32x2*)(row_base + c) = (u32x2){w[0], w[1]};
 }
 
 template <int EPI>
@@ -776,7 +779,8 @@ __device__ __forceinline__ void g3_reg_epilogue(const GP& p, const f32x4 (&acc)[
         }
       } else if (EPI != SVAE_EPI_CE_STATS || p.C) {   // CE statistics with C == nullptr: no logits stored
 #pragma unroll
-        for (int jp = 0; jp < 2; ++jp) store_pair_bf16(crow, 32 * jp, row_ok ? nleft : 0, v[2 * jp], v[2 * jp + 1], g);
+        for (int jp = 0; jp < 2; ++jp)   // vocab logits (2 GiB at C2): nontemporal, 1444 -> 1322 us
+          store_pair_bf16<EPI == SVAE_EPI_CE_STATS>(crow, 32 * jp, row_ok ? nleft : 0, v[2 * jp], v[2 * jp + 1], g);
       }
     }
     if constexpr (EPI == SVAE_EPI_CE_STATS) {
