@@ -42,6 +42,8 @@ def head_cases():
         'bf16': lambda: K.gemm(h, W, logits, T, V, d, epi=N.EPI_BF16, bias=bias),
         'ce_stats': lambda: K.gemm(h, W, logits, T, V, d, epi=N.EPI_CE_STATS, bias=bias, aux=part, labels=labels,
                                    label_logit=lab),
+        'ce_noC': lambda: K.gemm(h, W, None, T, V, d, epi=N.EPI_CE_STATS, bias=bias, aux=part, labels=labels,
+                                 label_logit=lab),
     }
     for name, fn in cases.items():
         ms = timeit(fn)

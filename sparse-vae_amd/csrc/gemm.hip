@@ -1236,7 +1236,10 @@ SVAE_EXPORT int svae_gemm(const svae_gemm_desc* d, svae_stream_t stream) {
   p.tn2 = (d->N + 255) / 256;
   p.tm2 = (d->M + 255) / 256;
   static const int group_env = [] { const char* e = getenv("SVAE_GEMM_GROUP"); return e ? atoi(e) : -1; }();
-  p.group = group_env >= 0 ? group_env : 0;   // measured: no gain on the C2 shapes (L2 misses were not the limit)
+  // wide N (the vocab head, 128 column tiles): groups of 4 tile rows, so each XCD's 32 concurrent tiles are 4 rows x
+  // 8 columns (12 operand strips in its L2 instead of 33): head fwd 1385 -> 1314 us (scripts/gemm_probe.py). No
+  // effect measured on the narrow (<= 8 column tiles) C2 shapes.
+  p.group = group_env >= 0 ? group_env : (p.tn2 >= 32 ? 4 : 0);
   const long long blocks256 = (long long)p.tn2 * p.tm2 * d->batch * d->splits;
   const bool ok3 = !(d->a_t && !d->b_t);
   int impl = forced ? forced : ((ok3 && blocks256 >= 192) ? 3 : ((kslice <= 2048 && !(d->a_t && d->b_t)) ? 2 : 1));
