@@ -1261,7 +1261,8 @@ SVAE_EXPORT int svae_gemm(const svae_gemm_desc* d, svae_stream_t stream) {
     const long long nb3 = persist_env ? std::min<long long>(blocks256, ncu) : blocks256;
     p.desync = (nb3 < blocks256 && desync_env > 0) ? desync_env : 0;   // measured: staggering does not pay
     static const int relax_env = [] { const char* e = getenv("SVAE_GEMM_RELAX"); return e ? atoi(e) : 1; }();
-    p.relaxed = relax_env;
+    // (the CE-statistics epilogue without a logits store issues too few stores for the counted first wait)
+    p.relaxed = relax_env && !(d->epi == SVAE_EPI_CE_STATS && !d->C);
     dim3 grid3((unsigned)nb3);
 #define SVAE_GEMM3_CASE(E)                                                                                   \
   case E:                                                                                                    \
