@@ -156,6 +156,16 @@ __device__ __forceinline__ void xcd_block(int& x, int& y, int& z) {
 #endif
 }
 
+#ifdef SVAE_STAMPS
+// diagnostic build only (make stamps): s_memtime at block start / after the first K/V tile's wait / after the key
+// loop / at the end, for the first 1024 hardware block ids, plus the block's tile count and query tile
+__device__ unsigned long long svae_attn_stamps[1024][6];
+#define ATTN_STAMP(k, v) \
+  do { if (lin_id < 1024 && threadIdx.x == 0) svae_attn_stamps[lin_id][k] = (v); } while (0)
+#else
+#define ATTN_STAMP(k, v) ((void)0)
+#endif
+
 #ifndef ATTN_NS
 #define ATTN_NS 2   // (3 stages with the XCD order: 70.7 vs 67.5 us)
 #endif
@@ -174,6 +184,10 @@ __global__ __launch_bounds__(256, HDP == 64 ? 3 : 2) void attn_fwd_kernel(AP p) 
   int bx, h, b;
   xcd_block(bx, h, b);
   const int q0 = bx * 128;
+#ifdef SVAE_STAMPS
+  const int lin_id = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+  ATTN_STAMP(0, __builtin_amdgcn_s_memtime());
+#endif
   const bf16* Q = p.q + b * p.bq + (long long)h * p.hd;
   const bf16* K = p.k + b * p.bk + (long long)h * p.hd;
   const bf16* V = p.v + b * p.bv + (long long)h * p.hd;
@@ -239,6 +253,9 @@ __global__ __launch_bounds__(256, HDP == 64 ? 3 : 2) void attn_fwd_kernel(AP p) 
     __builtin_amdgcn_s_barrier();   // everyone's have; stage (it - 1) % NS is free (a raw barrier: __syncthreads
                                     // would also drain the younger tiles' DMA with its vmcnt(0))
     if (it + NS - 1 < nvisit) issue(it + NS - 1);
+#ifdef SVAE_STAMPS
+    if (it == 0) ATTN_STAMP(1, __builtin_amdgcn_s_memtime());
+#endif
     const int kbase = kt * 64;
     if ((!p.causal || kbase <= qw + 31) && (kbase < SBLK || kbase + 63 >= lo_w)) {
       // S^T = K . Q^T : s[j][st][r] = score(key = kbase + 16st + 4g + r, query = qw + 16j + li)
@@ -319,6 +336,11 @@ __global__ __launch_bounds__(256, HDP == 64 ? 3 : 2) void attn_fwd_kernel(AP p) 
     }
   }
 
+#ifdef SVAE_STAMPS
+  ATTN_STAMP(2, __builtin_amdgcn_s_memtime());
+  ATTN_STAMP(4, (unsigned long long)nvisit);
+  ATTN_STAMP(5, (unsigned long long)bx);
+#endif
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const float lsum = sum_x16_x32(ls[j]);
@@ -338,6 +360,9 @@ __global__ __launch_bounds__(256, HDP == 64 ? 3 : 2) void attn_fwd_kernel(AP p) 
       if (g == 0) p.lse[((long long)b * p.H + h) * p.Lq + qrow] = m[j] * p.scale + __logf(lsum);
     }
   }
+#ifdef SVAE_STAMPS
+  ATTN_STAMP(3, __builtin_amdgcn_s_memtime());
+#endif
 }
 
 // ===================================================================================== backward
@@ -699,3 +724,9 @@ SVAE_EXPORT int64_t svae_attn_dq_part_elems(int32_t B, int32_t H, int32_t Lq, in
   if (B <= 0 || H <= 0 || Lq <= 0 || Lk <= 0 || hd <= 0) return 0;
   return (int64_t)((Lk + BWD_KEYS - 1) / BWD_KEYS) * B * Lq * H * hd;
 }
+
+#ifdef SVAE_STAMPS
+extern "C" __attribute__((visibility("default"))) int svae_debug_attn_stamps(unsigned long long* host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(svae_attn_stamps), sizeof(svae_attn_stamps)) == hipSuccess ? 0 : -1;
+}
+#endif
