@@ -184,12 +184,16 @@ __device__ __forceinline__ float block_sum(float v, float* sh) {
 // ------------------------------------------------------------------ decode attention
 // grid (H, B), 256 threads. qkv f32 [B][ldq] with q | k | v (rotary already applied to q, k); caches
 // [B][H][T][hd] f32; O [B][ldo]. Dynamic LDS: one score per visible key.
-__global__ __launch_bounds__(256) void dec_attn_kernel(const float* __restrict__ qkv, long long ldq,
+// 16 waves per (sequence, head): the P.V sweep runs 16 key groups (hd = 64) in parallel, so a workgroup keeps 4x
+// more cache rows in flight than with 4 waves (the sweep is load-latency bound)
+constexpr int DA_THREADS = 1024, DA_WAVES = DA_THREADS / 64;
+
+__global__ __launch_bounds__(DA_THREADS) void dec_attn_kernel(const float* __restrict__ qkv, long long ldq,
                                                        float* __restrict__ kc, float* __restrict__ vc, int H, int hd,
                                                        int T, const int* __restrict__ cur, int window, float scale,
                                                        float* __restrict__ O, long long ldo) {
   extern __shared__ float sc[];
-  __shared__ float qs[128], ks[128], vs[128], red[16], osum[256];
+  __shared__ float qs[128], ks[128], vs[128], red[2 * DA_WAVES], osum[DA_THREADS];
   const int h = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
   const int d = H * hd;
   const int p = *cur - 1;
@@ -215,7 +219,7 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(const float* __restrict__
     n = p + 1;
   }
   float mx = -INFINITY;
-  for (int t = tid; t < n; t += 256) {
+  for (int t = tid; t < n; t += DA_THREADS) {
     const int j = t < n1 ? t : lo2 + (t - n1);
     const float* kr = (j == p) ? ks : kc + cbase + (long long)j * hd;
     float s = 0.f;
@@ -227,16 +231,16 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(const float* __restrict__
     sc[t] = s;
     mx = fmaxf(mx, s);
   }
-  mx = block_max<4>(mx, red);
+  mx = block_max<DA_WAVES>(mx, red);
   float se = 0.f;
-  for (int t = tid; t < n; t += 256) {
+  for (int t = tid; t < n; t += DA_THREADS) {
     const float e = __expf(sc[t] - mx);
     sc[t] = e;
     se += e;
   }
-  se = block_sum<4>(se, red + 8);
+  se = block_sum<DA_WAVES>(se, red + DA_WAVES);
   // O[c] = sum_t sc[t] v[key(t)][c]: thread = (column c, key group gi)
-  const int G = 256 / hd, c = tid % hd, gi = tid / hd;
+  const int G = DA_THREADS / hd, c = tid % hd, gi = tid / hd;
   float acc = 0.f;
   if (gi < G) {
     for (int t = gi; t < n; t += G) {
@@ -521,7 +525,7 @@ SVAE_EXPORT int svae_dec_attn(const float* qkv, int64_t ldq, float* kcache, floa
   if (!qkv || !kcache || !vcache || !cur || !O || B <= 0 || H <= 0 || T <= 0) return SVAE_EINVAL;
   if (hd <= 0 || hd > 128 || hd % 4 || window < 0 || T > 32768) return SVAE_EINVAL;
   if ((((uintptr_t)kcache | (uintptr_t)vcache) & 15) || ldq % 4) return SVAE_EINVAL;
-  hipLaunchKernelGGL(dec_attn_kernel, dim3(H, B), dim3(256), (size_t)T * sizeof(float), (hipStream_t)stream, qkv, ldq,
+  hipLaunchKernelGGL(dec_attn_kernel, dim3(H, B), dim3(DA_THREADS), (size_t)T * sizeof(float), (hipStream_t)stream, qkv, ldq,
                      kcache, vcache, H, hd, T, cur, window, scale, O, ldo);
   SVAE_LAUNCH_CHECK();
   return SVAE_OK;
