@@ -366,10 +366,12 @@ __global__ __launch_bounds__(256, HDP == 64 ? 3 : 2) void attn_fwd_kernel(AP p) 
 }
 
 // ===================================================================================== backward
-// delta[b][h][q] = sum_d dO . O   (16 lanes per (q, h) row)
+// delta[b][h][q] = sum_d dO . O   (LPR = hd / 8 lanes per (q, h) row: 8 for hd <= 64, 16 for hd <= 128, so no
+// lane idles)
+template <int LPR>
 __global__ __launch_bounds__(256) void attn_delta_kernel(AP p) {
-  const int gid = blockIdx.x * 16 + (threadIdx.x >> 4);
-  const int li = threadIdx.x & 15;
+  const int gid = blockIdx.x * (256 / LPR) + (threadIdx.x / LPR);
+  const int li = threadIdx.x % LPR;
   const int total = p.B * p.Lq * p.H;
   if (gid >= total) return;
   const int h = gid % p.H, q = (gid / p.H) % p.Lq, b = gid / (p.H * p.Lq);
@@ -377,7 +379,7 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(AP p) {
   float s = 0.f;
   if (p.o32) {
     const float* O = p.o32 + b * p.bo32 + (long long)q * p.so32 + (long long)h * p.hd;
-    for (int d = li * 8; d < p.hd; d += 128) {
+    for (int d = li * 8; d < p.hd; d += 8 * LPR) {
       const bf16x8 c = *(const bf16x8*)(dO + d);
       const f32x4 a0 = *(const f32x4*)(O + d), a1 = *(const f32x4*)(O + d + 4);
 #pragma unroll
@@ -385,14 +387,14 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(AP p) {
     }
   } else {
     const bf16* O = p.o + b * p.bo + (long long)q * p.so + (long long)h * p.hd;
-    for (int d = li * 8; d < p.hd; d += 128) {
+    for (int d = li * 8; d < p.hd; d += 8 * LPR) {
       const bf16x8 a = *(const bf16x8*)(O + d), c = *(const bf16x8*)(dO + d);
 #pragma unroll
       for (int e = 0; e < 8; ++e) s += (float)a[e] * (float)c[e];
     }
   }
 #pragma unroll
-  for (int o = 8; o > 0; o >>= 1) s += __shfl_xor(s, o, 16);
+  for (int o = LPR / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, LPR);
   if (li == 0) ((float*)p.delta)[((long long)b * p.H + h) * p.Lq + q] = s;
 }
 
@@ -710,7 +712,8 @@ SVAE_EXPORT int svae_attn_bwd(const svae_attn_desc* d, svae_stream_t stream) {
   if (d->dq_bf && d->rot_tab && d->rot_d != d->H * d->hd) return SVAE_EINVAL;
   hipStream_t s = (hipStream_t)stream;
   const int rows = d->B * d->Lq * d->H;
-  hipLaunchKernelGGL(attn_delta_kernel, dim3((rows + 15) / 16), dim3(256), 0, s, p);
+  if (d->hd <= 64) hipLaunchKernelGGL(attn_delta_kernel<8>, dim3((rows + 31) / 32), dim3(256), 0, s, p);
+  else hipLaunchKernelGGL(attn_delta_kernel<16>, dim3((rows + 15) / 16), dim3(256), 0, s, p);
   dim3 grid((d->Lk + BWD_KEYS - 1) / BWD_KEYS, d->H, d->B);
   if (d->hd <= 64) hipLaunchKernelGGL(attn_bwd_kernel<64>, grid, dim3(256), 0, s, p);
   else hipLaunchKernelGGL(attn_bwd_kernel<128>, grid, dim3(256), 0, s, p);
