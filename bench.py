@@ -77,35 +77,50 @@ def step(model, opt, sched, batch):
     return out
 
 
-def cpu_baseline(cfg, seconds_budget=25.0):
-    """The oracle's fp32 fwd+bwd on the host cores, on a bounded sample (batch 8 of the same model)."""
+def host_cores():
+    """CPUs this process may use: the affinity mask, capped by the cgroup CPU quota when one is set (a GPU box
+    shares its host; the quota, not the machine's CPU count, is what the process gets)."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        with open('/sys/fs/cgroup/cpu.max') as f:
+            quota, period = f.read().split()[:2]
+        if quota != 'max':
+            n = min(n, max(1, int(int(quota) / int(period))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def cpu_baseline(cfg):
+    """The oracle's fp32 fwd+bwd on the host cores on the config's own batch: one warm-up step at
+    batch 2 (thread pool, allocator), then ONE timed step at the full per-GPU batch (C2: 64 x 512 tokens, ~10-30
+    s on 8-16 cores)."""
     import oracle
     from oracle.params import portable_ids
-    threads = min(len(os.sched_getaffinity(0)), 16)
+    threads = host_cores()
     torch.set_num_threads(threads)
     hp = oracle.HParams(d_model=cfg['d'], num_heads=cfg['heads'], num_layers=cfg['layers'])
     params = {k: v.requires_grad_(True) for k, v in oracle.init_params(hp, 0, test_init=False).items()}
-    B, L = 8, cfg['L']
-    ids = torch.from_numpy(portable_ids((B, L), 11))
-    ntok = torch.full((B,), L, dtype=torch.int64)
-    eps = torch.randn(B, 1, 64)
-    times = []
-    t_all = time.time()
-    for i in range(4):
+    L = cfg['L']
+
+    def run(B):
+        ids = torch.from_numpy(portable_ids((B, L), 11))
+        ntok = torch.full((B,), L, dtype=torch.int64)
+        eps = torch.randn(B, 1, 64)
         t0 = time.time()
         out = oracle.training_step(params, hp, ids, ntok, eps)
         out['loss'].backward()
         for p in params.values():
             p.grad = None
-        times.append(time.time() - t0)
-        if time.time() - t_all > seconds_budget:
-            break
-    steady = times[1:] if len(times) > 1 else times
-    dt = sum(steady) / len(steady)
+        return time.time() - t0
+
+    run(2)
+    B = cfg['B']
+    dt = run(B)
     return {'value': round(B * L / dt, 1), 'unit': 'tokens/s', 'cores': threads, 'kind': 'port',
             'sample': f'oracle/ (torch fp32 CPU restatement, golden-pinned) fwd+bwd of the {cfg["layers"]}L '
-                      f'd{cfg["d"]} model at batch {B} x {L} tokens, mean of {len(steady)} step(s) after 1 warmup '
-                      f'({dt:.2f} s/step)'}
+                      f'd{cfg["d"]} model on one full batch {B} x {L} tokens ({dt:.2f} s) after a batch-2 warm-up, '
+                      f'{threads} threads (affinity mask capped by the cgroup CPU quota)'}
 
 
 def parity_check(device):

@@ -156,14 +156,24 @@ int svae_reparam_kl_bwd(const float* stats, const float* eps, const float* dz, c
 
 /* ---- cross entropy over materialised bf16 logits (robust_cross_entropy, language_model.py:161-170) --
  * part: f32 [rows][ntile][2] (max, sumexp) from SVAE_EPI_CE_STATS; label_logit f32 [rows].
- * Row r is position (r % seq) of its sequence; label 0 = ignore_index. The sequence positions are cut
- * into nchunks chunks of chunk_len (torch.chunk semantics) and nll = mean over chunks of the per-chunk
- * mean loss. finalize: lse[rows], row_loss[rows], chunk_w[nchunks] (= 1 / (count_c * nchunks)),
- * nll_out[1]; red_ws: f32 workspace of >= 1024 floats (per-block chunk partials, added in a fixed order). grad: in place, logits -> gscale[0] * chunk_w[c] * (softmax - onehot) in bf16 (0 for
- * ignored rows); dbias (optional, f32 [V]) += column sums of dlogits (output-bias gradient). nchunks <= 8. */
+ * Row r is position (r % seq) of its sequence (rows % seq == 0); label 0 = ignore_index. The sequence
+ * positions are cut into nchunks chunks of chunk_len (torch.chunk along the sequence dim, :168; the last
+ * chunk runs to the end of the sequence) and nll = mean over chunks of the per-chunk mean loss (a single
+ * F.cross_entropy when nchunks == 1, :164-165). 1 <= nchunks <= 1024, (nchunks - 1) * chunk_len < seq.
+ * finalize: lse[rows], row_loss[rows] (lse - label logit, 0 for ignored rows), chunk_w[nchunks]
+ * (= 1 / (count_c * nchunks)), nll_out[1]; red_ws: f32 workspace of svae_ce_red_ws_elems(nchunks) floats
+ * (per-block chunk partials, added in a fixed order: deterministic).
+ * weighted_nll: the same chunked mean with F.cross_entropy's class weights (the val_bpb metric,
+ * language_model.py:106-110): per chunk sum tok_w[y] * row_loss / sum tok_w[y]; tok_w f32 [V].
+ * grad: in place, logits -> gscale[0] * chunk_w[c] * (softmax - onehot) in bf16 (0 for ignored rows);
+ * dbias (optional, f32 [V]) += column sums of dlogits (output-bias gradient). */
 int svae_ce_finalize(const float* part, int32_t ntile, const float* label_logit, const int32_t* labels,
                      int32_t rows, int32_t seq, int32_t nchunks, int32_t chunk_len, float* lse, float* row_loss,
                      float* chunk_w, float* nll_out, float* red_ws, svae_stream_t stream);
+int svae_ce_weighted_nll(const float* row_loss, const int32_t* labels, const float* tok_w, int32_t rows,
+                         int32_t seq, int32_t nchunks, int32_t chunk_len, float* out, float* red_ws,
+                         svae_stream_t stream);
+int32_t svae_ce_red_ws_elems(int32_t nchunks);
 int svae_ce_grad(void* logits, int64_t ld, const float* lse, const float* chunk_w, const int32_t* labels,
                  const float* gscale, float* dbias, int32_t rows, int32_t V, int32_t seq, int32_t nchunks,
                  int32_t chunk_len, svae_stream_t stream);
@@ -194,6 +204,11 @@ int svae_extract_rows(float* x, int64_t ld, int32_t rows, int32_t mod, int32_t D
 int svae_sumsq(const float* g, int64_t n, float* part, int32_t nblk, svae_stream_t stream);
 int svae_radam(float* p, void* pbf, const float* g, float* m, float* v, int64_t n, const float* part,
                int32_t nblk, const float* scal, float* norm_out, svae_stream_t stream);
+/* In-place clip_grad_norm_ of a micro-step that no optimiser step follows (gradient accumulation): g *=
+ * min(1, max_norm / (norm + 1e-6)) with norm from the sumsq partials; norm_out[0] = norm (may be NULL).
+ * n % 4 == 0, g 16-byte aligned. */
+int svae_clip_grad(float* g, int64_t n, const float* part, int32_t nblk, float max_norm, float* norm_out,
+                   svae_stream_t stream);
 
 /* ---- fp32 kernel mode (argmax-reconstruction parity; TransformerVAE.reconstruct in exact f32) ---------
  * svae_gemm_f32: C[M,N] = epi(A[M,K] . W[N,K]^T) on f32-input MFMA; epi in {SVAE_EPI_F32 (+bias, +resid),

@@ -179,14 +179,15 @@ def reconstruct(p, x, z, pad, hp, dropout_masks=None):
     return output_layer(p, x)
 
 
-def robust_cross_entropy(logits, labels):
+def robust_cross_entropy(logits, labels, weight=None):
     """language_model.py:161-170: one F.cross_entropy(ignore_index=0) when numel <= 2**30, else the
-    mean of per-sequence-chunk means (torch.chunk along the sequence dim)."""
+    mean of per-sequence-chunk means (torch.chunk along the sequence dim). `weight`: F.cross_entropy's class
+    weights (the val_bpb metric passes the per-token byte counts, language_model.py:106-110)."""
     chunks = -(-logits.numel() // 2 ** 30)
     if chunks == 1:
-        return F.cross_entropy(logits.flatten(end_dim=1), labels.flatten(), ignore_index=0)
+        return F.cross_entropy(logits.flatten(end_dim=1), labels.flatten(), ignore_index=0, weight=weight)
     return torch.stack([
-        F.cross_entropy(lc.flatten(end_dim=1), yc.flatten(), ignore_index=0)
+        F.cross_entropy(lc.flatten(end_dim=1), yc.flatten(), ignore_index=0, weight=weight)
         for lc, yc in zip(logits.chunk(chunks, dim=-2), labels.chunk(chunks, dim=-1))
     ]).mean()
 

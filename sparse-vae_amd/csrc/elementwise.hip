@@ -230,56 +230,58 @@ __global__ __launch_bounds__(256) void mi_final_kernel(const float* __restrict__
   }
 }
 
-// Chunked mean-of-means (robust_cross_entropy): CE_RED_BLOCKS blocks write per-chunk (sum, count) partials, one
-// small block adds them in a fixed order and writes nll and the per-chunk row weights (deterministic).
+// Chunked mean-of-means (robust_cross_entropy, language_model.py:163-170): grid (CE_RED_BLOCKS, nchunks); block
+// (b, c) sums the loss and count of chunk c's rows (positions c*chunk_len .. of every sequence; the last chunk runs
+// to the end of the sequence) into part[c][b]; one small block adds them in a fixed order and writes nll and the
+// per-chunk row weights (deterministic). tok_w (optional, f32 [V]): per-target class weights, F.cross_entropy's
+// `weight` (the val_bpb metric, language_model.py:106-110): sum w[y] l / sum w[y] per chunk.
 constexpr int CE_RED_BLOCKS = 64;
+constexpr int CE_MAX_CHUNKS = 1024;
 
-__global__ __launch_bounds__(1024) void ce_reduce_part_kernel(const float* __restrict__ row_loss,
-                                                              const int* __restrict__ labels, int rows, int seq,
-                                                              int nchunks, int chunk_len, float* __restrict__ part) {
-  __shared__ float ssum[16][8];
-  __shared__ float scnt[16][8];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;   // 16 waves
-  float s[8], c[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) { s[k] = 0.f; c[k] = 0.f; }
-  for (int r = blockIdx.x * 1024 + threadIdx.x; r < rows; r += CE_RED_BLOCKS * 1024) {
-    const int pos = r % seq;
-    const int ch = min(pos / chunk_len, nchunks - 1);
-    const float l = row_loss[r];
-    if (labels[r] != 0) {
-#pragma unroll
-      for (int k = 0; k < 8; ++k)
-        if (k == ch) { s[k] += l; c[k] += 1.f; }
+__global__ __launch_bounds__(256) void ce_reduce_part_kernel(const float* __restrict__ row_loss,
+                                                             const int* __restrict__ labels,
+                                                             const float* __restrict__ tok_w, int rows, int seq,
+                                                             int nchunks, int chunk_len, float* __restrict__ part) {
+  __shared__ float red[8];
+  const int ch = blockIdx.y;
+  const int p0 = ch * chunk_len;
+  const int clen = ch == nchunks - 1 ? seq - p0 : chunk_len;
+  const int n = (rows / seq) * clen;
+  float s = 0.f, c = 0.f;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += CE_RED_BLOCKS * 256) {
+    const int r = (i / clen) * seq + p0 + i % clen;
+    const int lab = labels[r];
+    if (lab != 0) {
+      const float w = tok_w ? tok_w[lab] : 1.f;
+      s += w * row_loss[r];
+      c += w;
     }
   }
-#pragma unroll
-  for (int k = 0; k < 8; ++k) { s[k] = wave_sum(s[k]); c[k] = wave_sum(c[k]); }
-  if (lane == 0) {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) { ssum[wave][k] = s[k]; scnt[wave][k] = c[k]; }
-  }
+  s = wave_sum(s);
+  c = wave_sum(c);
+  if ((threadIdx.x & 63) == 0) { red[threadIdx.x >> 6] = s; red[4 + (threadIdx.x >> 6)] = c; }
   __syncthreads();
-  if (threadIdx.x < 16) {
-    const int k = threadIdx.x & 7;
-    float t = 0.f;
-    for (int w = 0; w < 16; ++w) t += threadIdx.x < 8 ? ssum[w][k] : scnt[w][k];
-    part[blockIdx.x * 16 + threadIdx.x] = t;
+  if (threadIdx.x == 0) {
+    float* o = part + ((long long)ch * CE_RED_BLOCKS + blockIdx.x) * 2;
+    o[0] = (red[0] + red[1]) + (red[2] + red[3]);
+    o[1] = (red[4] + red[5]) + (red[6] + red[7]);
   }
 }
 
-__global__ __launch_bounds__(64) void ce_reduce_final_kernel(const float* __restrict__ part, int nchunks,
-                                                             float* __restrict__ chunk_w, float* __restrict__ nll_out) {
-  __shared__ float mean[8];
-  const int k = threadIdx.x;
-  if (k < nchunks) {
+__global__ __launch_bounds__(256) void ce_reduce_final_kernel(const float* __restrict__ part, int nchunks,
+                                                              float* __restrict__ chunk_w, float* __restrict__ nll_out) {
+  __shared__ float mean[CE_MAX_CHUNKS];
+  for (int k = threadIdx.x; k < nchunks; k += 256) {
     float ts = 0.f, tc = 0.f;
-    for (int b = 0; b < CE_RED_BLOCKS; ++b) { ts += part[b * 16 + k]; tc += part[b * 16 + 8 + k]; }
+    for (int b = 0; b < CE_RED_BLOCKS; ++b) {
+      ts += part[((long long)k * CE_RED_BLOCKS + b) * 2];
+      tc += part[((long long)k * CE_RED_BLOCKS + b) * 2 + 1];
+    }
     mean[k] = ts / tc;
-    chunk_w[k] = 1.0f / (tc * (float)nchunks);
+    if (chunk_w) chunk_w[k] = 1.0f / (tc * (float)nchunks);
   }
   __syncthreads();
-  if (k == 0) {
+  if (threadIdx.x == 0) {
     float nll = 0.f;
     for (int j = 0; j < nchunks; ++j) nll += mean[j];
     nll_out[0] = nll / nchunks;
@@ -511,6 +513,30 @@ __global__ __launch_bounds__(256) void radam_kernel(float* __restrict__ p, bf16*
   }
 }
 
+// In-place clip_grad_norm_ (language_model.py:120-122) for a micro-step that is not followed by an optimiser step
+// (gradient accumulation): g *= min(1, max_norm / (norm + 1e-6)), norm from the svae_sumsq partials.
+__global__ __launch_bounds__(256) void clip_scale_kernel(float* __restrict__ g, long long n, const float* __restrict__ part,
+                                                         int nblk, float max_norm, float* __restrict__ norm_out) {
+  __shared__ float red[4];
+  __shared__ float s_coef;
+  float s = 0.f;
+  for (int i = threadIdx.x; i < nblk; i += 256) s += part[i];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float norm = sqrtf(red[0] + red[1] + red[2] + red[3]);
+    s_coef = fminf(1.0f, max_norm / (norm + 1e-6f));
+    if (blockIdx.x == 0 && norm_out) norm_out[0] = norm;
+  }
+  __syncthreads();
+  const float coef = s_coef;
+  if (coef == 1.0f) return;                  // block-uniform: nothing to scale
+  const long long n4 = n / 4;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long long)gridDim.x * 256)
+    ((f32x4*)g)[i] = ((const f32x4*)g)[i] * coef;
+}
+
 inline int grid_for(long long work, int per_block, int cap = 4096) {
   long long g = (work + per_block - 1) / per_block;
   if (g < 1) g = 1;
@@ -560,16 +586,35 @@ SVAE_EXPORT int svae_ce_finalize(const float* part, int32_t ntile, const float* 
                                  int32_t rows, int32_t seq, int32_t nchunks, int32_t chunk_len, float* lse,
                                  float* row_loss, float* chunk_w, float* nll_out, float* red_ws, svae_stream_t stream) {
   if (!part || !label_logit || !labels || !lse || !row_loss || !chunk_w || !nll_out || !red_ws) return SVAE_EINVAL;
-  if (rows <= 0 || ntile <= 0 || seq <= 0 || nchunks <= 0 || nchunks > 8 || chunk_len <= 0) return SVAE_EINVAL;
+  if (rows <= 0 || ntile <= 0 || seq <= 0 || rows % seq || nchunks <= 0 || nchunks > CE_MAX_CHUNKS ||
+      chunk_len <= 0 || (long long)(nchunks - 1) * chunk_len >= seq)
+    return SVAE_EINVAL;
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(ce_rows_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, part, ntile, label_logit, labels, rows, lse,
                      row_loss);
-  hipLaunchKernelGGL(ce_reduce_part_kernel, dim3(CE_RED_BLOCKS), dim3(1024), 0, s, row_loss, labels, rows, seq, nchunks,
-                     chunk_len, red_ws);
-  hipLaunchKernelGGL(ce_reduce_final_kernel, dim3(1), dim3(64), 0, s, red_ws, nchunks, chunk_w, nll_out);
+  hipLaunchKernelGGL(ce_reduce_part_kernel, dim3(CE_RED_BLOCKS, nchunks), dim3(256), 0, s, row_loss, labels,
+                     (const float*)nullptr, rows, seq, nchunks, chunk_len, red_ws);
+  hipLaunchKernelGGL(ce_reduce_final_kernel, dim3(1), dim3(256), 0, s, red_ws, nchunks, chunk_w, nll_out);
   SVAE_LAUNCH_CHECK();
   return SVAE_OK;
 }
+
+SVAE_EXPORT int svae_ce_weighted_nll(const float* row_loss, const int32_t* labels, const float* tok_w, int32_t rows,
+                                     int32_t seq, int32_t nchunks, int32_t chunk_len, float* out, float* red_ws,
+                                     svae_stream_t stream) {
+  if (!row_loss || !labels || !tok_w || !out || !red_ws) return SVAE_EINVAL;
+  if (rows <= 0 || seq <= 0 || rows % seq || nchunks <= 0 || nchunks > CE_MAX_CHUNKS || chunk_len <= 0 ||
+      (long long)(nchunks - 1) * chunk_len >= seq)
+    return SVAE_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(ce_reduce_part_kernel, dim3(CE_RED_BLOCKS, nchunks), dim3(256), 0, s, row_loss, labels, tok_w, rows,
+                     seq, nchunks, chunk_len, red_ws);
+  hipLaunchKernelGGL(ce_reduce_final_kernel, dim3(1), dim3(256), 0, s, red_ws, nchunks, (float*)nullptr, out);
+  SVAE_LAUNCH_CHECK();
+  return SVAE_OK;
+}
+
+SVAE_EXPORT int32_t svae_ce_red_ws_elems(int32_t nchunks) { return nchunks * CE_RED_BLOCKS * 2; }
 
 SVAE_EXPORT int svae_mutual_info(const float* stats, const float* eps, uint64_t seed, const float* kl, int32_t B,
                                  int32_t Z, int32_t S, float* ws, float* out, svae_stream_t stream) {
@@ -671,6 +716,15 @@ SVAE_EXPORT int svae_radam(float* p, void* pbf, const float* g, float* m, float*
   if (((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15 || ((uintptr_t)pbf & 7)) return SVAE_EINVAL;
   hipLaunchKernelGGL(radam_kernel, dim3(grid_for(n / 4, 256, 2048)), dim3(256), 0, (hipStream_t)stream, p, (bf16*)pbf, g, m,
                      v, n, part, nblk, scal, norm_out);
+  SVAE_LAUNCH_CHECK();
+  return SVAE_OK;
+}
+
+SVAE_EXPORT int svae_clip_grad(float* g, int64_t n, const float* part, int32_t nblk, float max_norm, float* norm_out,
+                               svae_stream_t stream) {
+  if (!g || !part || n <= 0 || n % 4 || nblk <= 0 || ((uintptr_t)g & 15)) return SVAE_EINVAL;
+  hipLaunchKernelGGL(clip_scale_kernel, dim3(grid_for(n / 4, 256, 2048)), dim3(256), 0, (hipStream_t)stream, g, n, part,
+                     nblk, max_norm, norm_out);
   SVAE_LAUNCH_CHECK();
   return SVAE_OK;
 }

@@ -78,6 +78,10 @@ _SIGS = {
     'svae_reparam_kl_bwd': [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p],
     'svae_ce_finalize': [c_void_p, c_int32, c_void_p, c_void_p, c_int32, c_int32, c_int32, c_int32, c_void_p,
                          c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+    'svae_ce_weighted_nll': [c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_int32, c_int32, c_void_p, c_void_p,
+                             c_void_p],
+    'svae_ce_red_ws_elems': [c_int32],
+    'svae_clip_grad': [c_void_p, c_int64, c_void_p, c_int32, c_float, c_void_p, c_void_p],
     'svae_ce_grad': [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_int32,
                      c_int32, c_int32, c_void_p],
     'svae_dropout_bwd_cast': [c_void_p, c_void_p, c_float, c_uint64, c_int64, c_int32, c_int64, c_void_p],

@@ -76,6 +76,23 @@ class LanguageModel(_Base, ABC):
     def log(self, name, value, *args, **kwargs):
         self.logged[name] = value
 
+    def setup(self, stage: Optional[str] = None):
+        """language_model.py:57-66: take the datamodule's tokenizer and per-token byte counts (the class weights of
+        the val_bpb metric, registered in half precision as in the reference) and the [CLS]/[SEP] ids."""
+        tr = getattr(self, '_trainer', None)
+        dm = getattr(tr, 'datamodule', None) if tr is not None else getattr(self, 'datamodule', None)
+        if dm is None:
+            return
+        bpt = getattr(dm, 'bytes_per_token', None)
+        if bpt is not None:
+            self.token_weights = bpt.half()
+        tok = getattr(dm, '_tokenizer', None)       # synthetic data has no tokenizer: [CLS]=1 / [SEP]=2 stay
+        if tok is not None:
+            self.tokenizer = tok
+            if not self.start_token and not self.end_token:
+                vocab = tok.get_vocab()
+                self.start_token, self.end_token = vocab['[CLS]'], vocab['[SEP]']
+
     def initialize_weights(self):
         """language_model.py:80-96: N(0, init_scale) for Embedding/Linear weights, zero biases, LayerNorm
         untouched (learned queries keep their randn init)."""

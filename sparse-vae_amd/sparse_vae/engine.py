@@ -526,22 +526,29 @@ class VAEEngine:
             e1 = torch.cuda.Event(enable_timing=True)
             e1.record()
             probe.append((e0, e1))
-        numel = B * (L - 1) * V
-        chunks = -(-numel // CE_CHUNK_NUMEL)
-        chunk_len = -(-(L - 1) // chunks)
-        nchunks = -(-(L - 1) // chunk_len)
+        nchunks, chunk_len = K.ce_chunking(B, L, V, CE_CHUNK_NUMEL)
         lse = ws.get('ce.lse', (T,), f32)
         row_loss = ws.get('ce.row_loss', (T,), f32)
-        chunk_w = ws.get('ce.chunk_w', (8,), f32)
+        chunk_w = ws.get('ce.chunk_w', (max(8, nchunks),), f32)
         nll = ws.get('nll', (1,), f32)
         K.ce_finalize(part, ntile, lab_logit, labels, T, L, nchunks, chunk_len, lse, row_loss, chunk_w, nll)
         sv.update(xf=xf, gp0=gp0, h0=h0, hh=hh, ln_h=ln_h, logits=logits, lse=lse, chunk_w=chunk_w,
-                  nchunks=nchunks, chunk_len=chunk_len, labels=labels, ids32=ids32, ntok=ntok64, x_emb=x_emb)
+                  nchunks=nchunks, chunk_len=chunk_len, labels=labels, ids32=ids32, ntok=ntok64, x_emb=x_emb,
+                  row_loss=row_loss)
         loss = nll[0] + kl_weight * kl[0]                                          # transformer_vae.py:55
         self.saved = sv
         return {'loss': loss, 'nll': nll[0], 'kl': kl[0], 'train_kl': kl[1], 'raw_kl': raw_kl,
                 'mu': stats[:, :Z], 'logvar': stats[:, Z:], 'stats': stats, 'kl_buf': kl, 'z': zf, 'eps': eps_buf,
                 'logits': logits if need_logits else None}
+
+    def weighted_nll(self, tok_w):
+        """robust_cross_entropy(logits, labels, weight=tok_w) of the last forward (language_model.py:106-110, the
+        val_bpb numerator) from its per-row losses: per chunk sum w[y] l / sum w[y], mean over chunks."""
+        sv = self.saved
+        out = torch.empty(1, dtype=f32, device=self.P.device)
+        B, L = sv['B'], sv['L']
+        K.ce_weighted_nll(sv['row_loss'], sv['labels'], tok_w, B * L, L, sv['nchunks'], sv['chunk_len'], out)
+        return out[0]
 
     def _encode(self, x_emb, B, L, padm, dropout, seed):
         """Perceiver.forward (perceiver.py:39-50) then the q(z|x) linear (conditional_gaussian.py:18): returns

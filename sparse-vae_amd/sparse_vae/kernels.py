@@ -177,16 +177,42 @@ def reparam_bwd(stats, eps, dz, ntok, gkl, dstats, B, Z):
                                   dstats.data_ptr(), B, Z, stream()), 'svae_reparam_kl_bwd')
 
 
+def ce_red_ws(device, nchunks):
+    """f32 workspace of the chunked-CE reductions (grown on demand)."""
+    n = max(1024, lib.svae_ce_red_ws_elems(nchunks))
+    t = _ce_red.get(device)
+    if t is None or t.numel() < n:
+        t = _ce_red[device] = torch.empty(n, dtype=f32, device=device)
+    return t
+
+
 _ce_red = {}
 
 
 def ce_finalize(part, ntile, label_logit, labels, rows, seq, nchunks, chunk_len, lse, row_loss, chunk_w, nll):
-    red = _ce_red.get(part.device)
-    if red is None:
-        red = _ce_red[part.device] = torch.empty(1024, dtype=f32, device=part.device)
+    assert chunk_w.numel() >= nchunks and chunk_w.dtype == f32
+    red = ce_red_ws(part.device, nchunks)
     check(lib.svae_ce_finalize(part.data_ptr(), ntile, label_logit.data_ptr(), labels.data_ptr(), rows, seq,
                                nchunks, chunk_len, lse.data_ptr(), row_loss.data_ptr(), chunk_w.data_ptr(),
                                nll.data_ptr(), red.data_ptr(), stream()), 'svae_ce_finalize')
+
+
+def ce_weighted_nll(row_loss, labels, tok_w, rows, seq, nchunks, chunk_len, out):
+    """Chunked mean of row_loss with per-target weights tok_w [V] (F.cross_entropy(weight=...)), into out[0]."""
+    _dev(row_loss, labels, tok_w, out)
+    assert tok_w.dtype == f32 and tok_w.is_contiguous()
+    red = ce_red_ws(row_loss.device, nchunks)
+    check(lib.svae_ce_weighted_nll(row_loss.data_ptr(), labels.data_ptr(), tok_w.data_ptr(), rows, seq, nchunks,
+                                   chunk_len, out.data_ptr(), red.data_ptr(), stream()), 'svae_ce_weighted_nll')
+
+
+def ce_chunking(B, L, V, chunk_numel=2 ** 30):
+    """robust_cross_entropy's split (language_model.py:163-170) of logits [B, L-1, V]: cdiv(numel, 2^30) chunks
+    requested along the sequence; torch.chunk makes ceil((L-1)/chunks)-long pieces, so fewer may result.
+    Returns (nchunks, chunk_len)."""
+    chunks = -(-(B * (L - 1) * V) // chunk_numel)
+    chunk_len = -(-(L - 1) // chunks)
+    return -(-(L - 1) // chunk_len), chunk_len
 
 
 def mutual_info(stats, kl, B, Z, seed, out, ws, eps=None, S=10):
@@ -234,6 +260,11 @@ def extract_rows(x, ld, rows, mod, D, out):
 
 def sumsq(g, n, part):
     check(lib.svae_sumsq(g.data_ptr(), n, part.data_ptr(), part.numel(), stream()), 'svae_sumsq')
+
+
+def clip_grad(g, n, part, max_norm, norm_out=None):
+    check(lib.svae_clip_grad(g.data_ptr(), n, part.data_ptr(), part.numel(), float(max_norm), ptr(norm_out), stream()),
+          'svae_clip_grad')
 
 
 def radam(p, pbf, g, m, v, n, part, scal, norm_out):

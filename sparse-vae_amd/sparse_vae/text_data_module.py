@@ -172,11 +172,24 @@ class TextDataModule:
         return batch
 
     # ------------------------------------------------------------------ loaders
-    def train_dataloader(self, split: str = 'train'):
+    @staticmethod
+    def _rank_world(rank=None, world=None):
+        if rank is None or world is None:
+            import torch.distributed as dist
+            if dist.is_available() and dist.is_initialized():
+                return dist.get_rank(), dist.get_world_size()
+            return 0, 1
+        return rank, world
+
+    def train_dataloader(self, split: str = 'train', rank: Optional[int] = None, world: Optional[int] = None):
         """text_data_module.py:176-184: token-budget batches of similar-length documents, collated in worker
-        processes into pinned memory."""
+        processes into pinned memory. Under data parallelism (an initialised process group, or rank/world given)
+        rank r gets batches r, r + world, ... of the first len - len % world: disjoint shards, equal counts."""
+        rank, world = self._rank_world(rank, world)
         if self.synthetic:
-            return (self.synthetic_batch(i) for i in range(self.hparams.num_batches))
+            n = self.hparams.num_batches if split == 'train' else 8
+            base = 0 if split == 'train' else 10 ** 9
+            return _SyntheticLoader(self, base, n - n % world if world > 1 else n, rank, world)
         from torch.utils.data import DataLoader
         if self.dataset is None:
             self.prepare_data()
@@ -184,14 +197,14 @@ class TextDataModule:
         data = self.dataset[split]
         docs = list(enumerate(np.asarray(data['length_bin']).tolist()))
         sampler = UniformSizeRandomSampler(documents=docs, max_size=self.hparams.tokens_per_batch)
+        if world > 1:
+            sampler = RankBatchSampler(sampler, rank, world)
         workers = min(self.hparams.num_workers, os.cpu_count() or 1)
         return DataLoader(data, batch_sampler=sampler, collate_fn=self.collate, num_workers=workers,
                           pin_memory=torch.cuda.is_available())
 
-    def val_dataloader(self):
-        if self.synthetic:
-            return (self.synthetic_batch(10 ** 9 + i) for i in range(8))
-        return self.train_dataloader(split='test')
+    def val_dataloader(self, rank: Optional[int] = None, world: Optional[int] = None):
+        return self.train_dataloader(split='test' if not self.synthetic else 'val', rank=rank, world=world)
 
     def test_dataloader(self, *args, **kwargs):
         return self.val_dataloader()
@@ -224,3 +237,36 @@ class TextDataModule:
         for i, seq in enumerate(batch):
             buffer[i, extras:len(seq) + extras] = seq
         return buffer
+
+
+class _SyntheticLoader:
+    """Synthetic batches base + k for k = rank, rank + world, ... < n (a sized iterable, one pass)."""
+
+    def __init__(self, dm, base, n, rank, world):
+        self.dm, self.base, self.n, self.rank, self.world = dm, base, n, rank, world
+
+    def __len__(self):
+        return len(range(self.rank, self.n, self.world))
+
+    def __iter__(self):
+        return (self.dm.synthetic_batch(self.base + k) for k in range(self.rank, self.n, self.world))
+
+
+class RankBatchSampler:
+    """Data-parallel shard of a batch sampler: rank r takes batches r, r + world, ... of each epoch's first
+    len - len % world batches, so every rank runs the same number of steps (and collectives). Every rank draws
+    the same batch order (seed_everything on all ranks), as Lightning's replaced samplers assume."""
+
+    def __init__(self, sampler, rank, world):
+        self.sampler, self.rank, self.world = sampler, rank, world
+
+    def __len__(self):
+        return len(self.sampler) // self.world
+
+    def __iter__(self):
+        n = len(self.sampler) // self.world * self.world
+        for i, b in enumerate(self.sampler):
+            if i >= n:
+                continue                      # drain the epoch (the sampler repacks when exhausted)
+            if i % self.world == self.rank:
+                yield b

@@ -1,9 +1,22 @@
 """A minimal Trainer for the reference's fit loop (pytorch_lightning is not installed here).
 
-Per step: training_step -> loss.backward() (engine backward; with data parallelism the bucketed RCCL
-all-reduces run during it) -> on_after_backward (grad norm + KL anneal) -> RAdam.step (fused clip + update)
--> LambdaLR.step. One process per GPU: launch with torch.distributed.run; RANK/LOCAL_RANK/WORLD_SIZE come
-from the environment and the backend is 'nccl' (RCCL on ROCm).
+Mirrors what Lightning does for the reference (train.py:12-95 builds `Trainer(**config.trainer)` and calls
+`fit(model, datamodule)`):
+
+* epochs over the train dataloader until `max_steps` optimiser steps (or `max_epochs`) -- the reference's
+  cosine schedule ends training by raising KeyboardInterrupt (language_model.py:135-141);
+* per micro-batch: training_step -> (loss / accumulate_grad_batches).backward() -> on_after_backward; every
+  `accumulate_grad_batches` micro-batches (and at the end of an epoch) RAdam.step (fused clip + update) ->
+  LambdaLR.step -> zero_grad. `model.require_backward_grad_sync` is False on the micro-steps no optimiser step
+  follows (DDP's no_sync): their backward all-reduces nothing;
+* validation (`validation_step` over the val loader, logged values averaged over its batches) every
+  `val_check_interval` training batches (int), or that fraction of an epoch (float; 1.0 = end of each epoch),
+  `limit_val_batches` batches at most.
+
+Data parallel: one process per GPU (torch.distributed.run); RANK/LOCAL_RANK/WORLD_SIZE come from the
+environment and the backend is 'nccl' (RCCL on ROCm). The datamodule hands each rank a disjoint shard of the
+batches with the same batch count on every rank (the tail that does not divide by the world size is dropped,
+as DistributedSampler(drop_last=True) does), so every rank runs the same number of collectives.
 """
 import os
 import time
@@ -31,18 +44,64 @@ def init_distributed():
     return world, (dist.get_rank() if world > 1 else 0), local
 
 
+def _scalar(v):
+    return v.item() if torch.is_tensor(v) else v
+
+
 class Trainer:
-    def __init__(self, max_steps: int = -1, accumulate_grad_batches: int = 1, log_every_n_steps: int = 50,
-                 val_check_interval=None, gpus=None, precision='bf16', **unused):
+    def __init__(self, max_steps: int = -1, max_epochs=None, accumulate_grad_batches: int = 1,
+                 log_every_n_steps: int = 50, val_check_interval=1.0, limit_val_batches=None, gpus=None,
+                 precision='bf16', **unused):
         self.max_steps = max_steps
-        self.accumulate_grad_batches = accumulate_grad_batches
+        self.max_epochs = max_epochs
+        self.accumulate_grad_batches = max(1, int(accumulate_grad_batches))
         self.log_every_n_steps = log_every_n_steps
+        self.val_check_interval = val_check_interval
+        self.limit_val_batches = limit_val_batches
         self.global_step = 0
+        self.current_epoch = 0
         self.datamodule = None
         self.history = []
+        self.val_history = []
+        self.rank = 0
+
+    # ------------------------------------------------------------------ loop pieces
+    def _val_every(self, loader):
+        """Training batches between validation runs (None: end of epoch only)."""
+        v = self.val_check_interval
+        if v is None:
+            return None
+        if isinstance(v, int) and not isinstance(v, bool) and v >= 1:
+            return v
+        n = len(loader) if hasattr(loader, '__len__') else None
+        if n is None or float(v) >= 1.0:
+            return None
+        return max(1, int(n * float(v)))
+
+    @torch.no_grad()
+    def validate(self, model):
+        dm = self.datamodule
+        sums, count = {}, 0
+        for j, batch in enumerate(dm.val_dataloader()):
+            if self.limit_val_batches is not None and j >= int(self.limit_val_batches):
+                break
+            model.logged.clear()
+            model.validation_step(batch, j)
+            for k, v in model.logged.items():
+                if k.startswith('val_'):
+                    sums[k] = sums.get(k, 0.0) + float(_scalar(v))
+            count += 1
+        logs = {k: v / max(count, 1) for k, v in sums.items()}
+        logs['step'] = self.global_step
+        logs['val_batches'] = count
+        self.val_history.append(logs)
+        if self.rank == 0:
+            print(logs, flush=True)
+        return logs
 
     def fit(self, model, datamodule=None):
         world, rank, local = init_distributed()
+        self.rank = rank
         self.datamodule = datamodule
         model._trainer = self
         if torch.cuda.is_available():
@@ -50,36 +109,60 @@ class Trainer:
         model.initialize_weights()                     # on_fit_start, transformer_language_model.py:74-75
         if world > 1:
             model.enable_data_parallel()
-        model.on_train_start()
         datamodule.prepare_data()
         datamodule.setup('fit')
+        model.setup('fit')
+        model.on_train_start()
         [opt], [sch] = model.configure_optimizers(datamodule.tokens_per_step(), self.accumulate_grad_batches)
         sched = sch['scheduler']
+        self.model, self.optimizer, self.lr_scheduler = model, opt, sched
         model.train()
         t0 = time.time()
-        micro = 0
+        accum = self.accumulate_grad_batches
+        done = False
         try:
-            for i, batch in enumerate(datamodule.train_dataloader()):
-                if world > 1 and i % world != rank:
-                    continue
-                out = model.training_step(batch, i)
-                loss = out['loss'] / self.accumulate_grad_batches
-                loss.backward()
-                model.on_after_backward()
-                micro += 1
-                if micro % self.accumulate_grad_batches == 0:
-                    opt.step()
-                    sched.step()
-                    opt.zero_grad()
-                    self.global_step += 1
-                    if rank == 0 and self.global_step % self.log_every_n_steps == 0:
-                        logs = {k: (v.item() if torch.is_tensor(v) else v) for k, v in model.logged.items()}
-                        logs['step'] = self.global_step
-                        logs['elapsed_s'] = round(time.time() - t0, 2)
-                        self.history.append(logs)
-                        print(logs, flush=True)
-                    if 0 < self.max_steps <= self.global_step:
+            while not done and (self.max_epochs is None or self.current_epoch < self.max_epochs):
+                loader = datamodule.train_dataloader()
+                every = self._val_every(loader)
+                it = iter(loader)
+                batch = next(it, None)
+                if batch is None:
+                    break
+                i, micro = 0, 0
+                while batch is not None:
+                    nxt = next(it, None)                 # one batch of lookahead: the epoch's last micro-step
+                    micro += 1
+                    step_now = micro == accum or nxt is None
+                    model.require_backward_grad_sync = step_now
+                    out = model.training_step(batch, i)
+                    (out['loss'] / accum).backward()
+                    model.on_after_backward()
+                    if step_now:
+                        opt.step()
+                        sched.step()
+                        opt.zero_grad()
+                        micro = 0
+                        self.global_step += 1
+                        if rank == 0 and self.global_step % self.log_every_n_steps == 0:
+                            logs = {k: _scalar(v) for k, v in model.logged.items()}
+                            logs['step'] = self.global_step
+                            logs['elapsed_s'] = round(time.time() - t0, 2)
+                            self.history.append(logs)
+                            print(logs, flush=True)
+                    i += 1
+                    if every is not None and i % every == 0:
+                        self.validate(model)
+                        model.train()
+                    if step_now and 0 < self.max_steps <= self.global_step:
+                        done = True
                         break
+                    batch = nxt
+                if not done and every is None:
+                    self.validate(model)
+                    model.train()
+                self.current_epoch += 1
         except KeyboardInterrupt:        # cosine_decay's end-of-schedule signal (language_model.py:139)
             pass
+        finally:
+            model.require_backward_grad_sync = True
         return self.history

@@ -8,6 +8,7 @@ Autograd compatibility: `training_step` returns a loss tensor whose `.backward()
 explicit backward and leaves every parameter's `.grad` as a view of the gradient arena, so the reference's
 Lightning loop (training_step -> backward -> on_after_backward -> optimizer.step) works unchanged.
 """
+import math
 from copy import deepcopy
 from dataclasses import dataclass
 from typing import Any, Dict, Optional
@@ -101,6 +102,11 @@ class TransformerVAE(ContinuousVAEHooks, LanguageModel):
         self._norm_valid = False
         self._dp = None
         self._step_seed = 7295
+        # DDP's flag (Lightning sets it through no_sync under accumulate_grad_batches): False marks a gradient-
+        # accumulation micro-step that no optimiser step follows -- its backward runs no all-reduce (the final
+        # micro-step's buckets carry the accumulated sum) and on_after_backward applies its clip in place
+        self.require_backward_grad_sync = True
+        self.token_weights = None
 
     # ------------------------------------------------------------------ flat arena plumbing
     def _bind_flat(self, device):
@@ -237,6 +243,12 @@ class TransformerVAE(ContinuousVAEHooks, LanguageModel):
             return {'loss': loss, 'posterior': Normal(loc=mu.detach(), scale=scale.detach())}
         if stage == 'val':
             self.log('val_loss', out['nll'] + out['kl'])
+            if self.token_weights is not None:
+                # language_model.py:106-110: robust_cross_entropy(weight=token_weights) * bytes_per_token / log 2;
+                # bytes_per_token is [B] there, logged here as its batch mean
+                bpt = batch['num_bytes'].to(self.device, torch.float32) / ntok.to(torch.float32)
+                tw = self.token_weights.to(self.device, torch.float32).contiguous()
+                self.log('val_bpb', (eng.weighted_nll(tw) * bpt).mean() / math.log(2))
         return None
 
     def validation_step(self, batch, batch_index: int = 0):
@@ -255,8 +267,13 @@ class TransformerVAE(ContinuousVAEHooks, LanguageModel):
         g = gloss.reshape(()).to(torch.float32)
         if self._dp is not None:
             g = g / self._dp['world']
-        eng.backward(g, self._kl_weight_used, ready=self._dp_ready if self._dp is not None else None)
-        self._dp_finish()
+        # all-reduce only on the micro-step an optimiser step follows (DDP no_sync semantics): the buckets then
+        # reduce the accumulated sum once; reducing every micro-step would add the already-averaged earlier
+        # micro-gradients world times over
+        sync = self._dp is not None and self.require_backward_grad_sync
+        eng.backward(g, self._kl_weight_used, ready=self._dp_ready if sync else None)
+        if sync:
+            self._dp_finish()
         self._norm_valid = False
 
     def _norm_partials(self, fresh=True):
@@ -272,6 +289,12 @@ class TransformerVAE(ContinuousVAEHooks, LanguageModel):
 
     def on_after_backward(self):
         super().on_after_backward()        # grad norm (+ clip inside the fused optimiser step)
+        if not self.require_backward_grad_sync:
+            # an accumulation micro-step: the reference clips after every backward (language_model.py:120-122),
+            # so this partial gradient is clipped now; the last micro-step's clip is fused into RAdam
+            K.clip_grad(self._flat.grad, self._flat.n_live, self._norm_partials(fresh=False),
+                        float(self.hparams.get('grad_clip_threshold', 5.0)))
+            self._norm_valid = False
         self.anneal_kl()                   # continuous_autoencoder.py:28-39
 
     # ------------------------------------------------------------------ inference-side helpers

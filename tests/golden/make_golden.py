@@ -31,6 +31,7 @@ CONFIGS = {
     'small6_pad': (256, 4, 6, 192, 3, True),     # hd 64, one middle (cross-attention) encoder layer
     'hd96': (384, 4, 6, 128, 2, True),           # decoder hd 96, encoder 6 heads x 64
     'c2shape': (512, 8, 6, 512, 2, False),       # the C2 model at B=2
+    'c4shape': (768, 8, 12, 1024, 2, True),      # the C4/C5 model (decoder hd 96, encoder 12 x 64) at L=1024, B=2
 }
 N_SAMPLE = 64   # gradient elements sampled per parameter
 
@@ -285,6 +286,53 @@ def iw_vectors(sv):
     np.savez_compressed(os.path.join(HERE, 'iw.npz'), **rec)
 
 
+# robust_cross_entropy's chunked branch (language_model.py:161-170): logits [33, 999, 32768] = 1.08e9 > 2^30
+# elements -> cdiv = 2 chunks of 500 / 499 sequence positions, mean of the per-chunk means. The logits are the
+# rank-2 product a (x) w + u (x) s with every factor bf16-representable, so a bf16-operand / f32-accumulate GEMM
+# with K = 2 reproduces them bit for bit (each product is exact in f32, one rounding at the sum); only the factors
+# and labels are stored. Padding lengths put most ignored positions into the second chunk, so the mean of means
+# differs clearly from the single mean.
+CE_SHAPE = (33, 999, 2 ** 15)
+
+
+def ce_logits(a, u, w, s):
+    logits = a[:, :, None] * w[None, None, :]
+    logits.addcmul_(u[:, :, None], s[None, None, :])
+    return logits
+
+
+def ce_vectors(sv):
+    lm = sys.modules['sparse_vae.core.language_model']
+    import torch.nn.functional as F
+    B, L1, V = CE_SHAPE
+
+    def bf(x):
+        return torch.from_numpy(np.asarray(x, dtype=np.float32)).bfloat16().float()
+
+    a = bf(portable_normal(B * L1, 'ce_a', 7)).reshape(B, L1)
+    u = bf(portable_normal(B * L1, 'ce_u', 7)).reshape(B, L1)
+    w = bf(2.0 * portable_normal(V, 'ce_w', 7))
+    s = bf(portable_normal(V, 'ce_s', 7))
+    ids = portable_ids((B, L1 + 1), 71)
+    lens = np.asarray([L1 + 1 - (37 * b) % 700 for b in range(B)], dtype=np.int64)
+    for b, n in enumerate(lens):
+        ids[b, n:] = 0
+    labels = torch.from_numpy(ids[:, 1:].astype(np.int64))
+    tok_w = torch.from_numpy(portable_ids((V,), 5, low=1, high=9).astype(np.float32))   # class weights 1..8
+    tok_w[0] = 1.0
+    logits = ce_logits(a, u, w, s)
+    assert -(-logits.numel() // 2 ** 30) == 2
+    with torch.no_grad():
+        nll = lm.robust_cross_entropy(logits, labels)
+        wnll = lm.robust_cross_entropy(logits, labels, weight=tok_w)
+        single = F.cross_entropy(logits.flatten(end_dim=1), labels.flatten(), ignore_index=0)
+    rec = {'a': a.numpy(), 'u': u.numpy(), 'w': w.numpy(), 's': s.numpy(), 'labels': labels.numpy().astype(np.int32),
+           'lens': lens, 'tok_w': tok_w.numpy(), 'nll': np.float64(nll.item()), 'wnll': np.float64(wnll.item()),
+           'single_mean': np.float64(single.item())}
+    np.savez_compressed(os.path.join(HERE, 'ce_chunked.npz'), **rec)
+    print(f'ce_chunked: nll={nll.item():.6f} weighted={wnll.item():.6f} single-chunk mean={single.item():.6f}')
+
+
 def main():
     torch.set_num_threads(min(8, os.cpu_count()))
     sv = ref_stubs.import_reference()
@@ -292,6 +340,9 @@ def main():
     only = sys.argv[1:]
     if only == ['sparse']:
         sparse_vectors(sv)
+        return
+    if only == ['ce']:
+        ce_vectors(sv)
         return
     if only == ['eval']:
         generation_vectors(sv)
@@ -302,9 +353,13 @@ def main():
             continue
         model = run_config(sv, name, cfg)
         keys[name] = {k: list(v.shape) for k, v in model.state_dict().items()}
+    kpath = os.path.join(HERE, 'reference_keys.json')
+    if only and os.path.exists(kpath):
+        with open(kpath) as f:
+            keys = {**json.load(f), **keys}
+    with open(kpath, 'w') as f:
+        json.dump(keys, f, indent=0)
     if not only:
-        with open(os.path.join(HERE, 'reference_keys.json'), 'w') as f:
-            json.dump(keys, f, indent=0)
         op_vectors(sv)
 
 

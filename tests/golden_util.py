@@ -7,7 +7,7 @@ import torch
 from oracle.params import HParams, init_params
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden')
-CONFIG_NAMES = ['tiny', 'tiny_pad', 'small6_pad', 'hd96', 'c2shape']
+CONFIG_NAMES = ['tiny', 'tiny_pad', 'small6_pad', 'hd96', 'c2shape', 'c4shape']
 
 
 def load(name):
@@ -45,3 +45,16 @@ def setup_iw():
     params = init_params(hp, seed)
     ids = torch.from_numpy(g['ids'].astype(np.int64))
     return g, hp, params, ids
+
+
+def ce_logits(a, u, w, s):
+    """The chunked-CE fixture's logits (make_golden.ce_vectors): a (x) w + u (x) s, [B, L-1, V] f32."""
+    logits = a[:, :, None] * w[None, None, :]
+    logits.addcmul_(u[:, :, None], s[None, None, :])
+    return logits
+
+
+def setup_ce():
+    g = load('ce_chunked')
+    t = {k: torch.from_numpy(g[k]) for k in ('a', 'u', 'w', 's', 'tok_w')}
+    return g, t, torch.from_numpy(g['labels'].astype(np.int64))

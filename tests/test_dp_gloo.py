@@ -71,3 +71,65 @@ def test_gradients_are_averaged_and_weights_broadcast(bucket_mb):
     assert torch.equal(g0, g1)
     # gradients of parameters that never receive one (pos_linear) are not communicated
     assert not torch.equal(d0, d1)
+
+
+class _FakeEngine:
+    """Stands in for the HIP engine's backward on CPU: micro-step k on rank r adds g * G_k,r to the arena and
+    emits the engine's ready() sequence when asked to."""
+
+    def __init__(self, flat, ends, rank):
+        self.flat, self.ends, self.rank, self.calls = flat, ends, rank, 0
+
+    def backward(self, g, kl_weight, ready=None):
+        self.calls += 1
+        k = self.calls
+        grad_k = torch.arange(self.flat.total, dtype=torch.float32) * 1e-6 * k + self.rank + 10 * k
+        self.flat.grad.add_(g * grad_k)
+        if ready is not None:
+            for e in self.ends:
+                ready(e)
+
+
+def _worker_accum(rank, world, port, q):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'sparse-vae_amd'))
+    from sparse_vae import TransformerVAE, TransformerVAEHparams
+    hp = TransformerVAEHparams(d_model=128, num_layers=4, num_heads=8, sparse_self_attention=False)
+    m = TransformerVAE(hp, device='cpu')
+    m.enable_data_parallel(bucket_mb=0.25)
+    flat = m._flat
+    m._engine = _FakeEngine(flat, _ready_sequence(flat, m._ehp), rank)
+    m._kl_weight_used = 1.0
+    # micro-step 1 (accumulation, no optimiser step after it) then micro-step 2 (optimiser step follows)
+    for sync in (False, True):
+        m.require_backward_grad_sync = sync
+        m._run_backward(torch.tensor(1.0))
+        if not sync:
+            assert not m._dp['works'] and m._dp['start'] == 0     # nothing was communicated
+    q.put((rank, flat.grad[:flat.n_live].numpy().copy()))
+    dist.destroy_process_group()
+
+
+def test_gradient_accumulation_reduces_once():
+    """DP + accumulate_grad_batches=2 (the train.py default, train.py:16-23): the result is the rank-mean of
+    each rank's summed micro-gradients -- the first micro-step's gradient is not reduced twice."""
+    world = 2
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker_accum, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda r: r[0])
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    g0, g1 = torch.from_numpy(res[0][1]), torch.from_numpy(res[1][1])
+    n = g0.numel()
+    ar = torch.arange(n, dtype=torch.float32) * 1e-6
+    # sum over k = 1, 2 of (ar * k + rank + 10 k), averaged over ranks 0, 1
+    expect = ar * 3 + 0.5 * 2 + 30
+    torch.testing.assert_close(g0, expect, rtol=1e-6, atol=1e-5)
+    assert torch.equal(g0, g1)

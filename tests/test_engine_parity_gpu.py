@@ -1,7 +1,9 @@
 """Full training-step parity: the HIP engine (bf16 MFMA path) against the CPU fp32 oracle on the same seeded
 weights, tokens and injected noise (dropout off). The oracle is pinned to the reference by
-tests/test_oracle_golden.py. Tolerances: loss/ELBO 1e-3 rel (BASELINE.json north_star), KL and mu/logvar
-(kept f32 on the device) 2e-3 rel, gradients by cosine similarity and norm ratio per parameter."""
+tests/test_oracle_golden.py. Tolerances: loss/ELBO 1e-3 rel (BASELINE.json north_star), KL 2e-2 and mu 2e-2
+rel (the posterior comes out of the bf16 encoder), every parameter gradient cosine >= 0.995 and norm ratio
+within 2 %. c4shape is the C4/C5 model (12 layers, d768, decoder hd 96 on the hd-128 kernels, encoder 12 x 64,
+L=1024)."""
 import os
 
 import numpy as np
@@ -24,7 +26,7 @@ def _build(hp, params):
     return flat, VAEEngine(hp, flat)
 
 
-@pytest.mark.parametrize('name', ['tiny_pad', 'small6_pad', 'hd96', 'c2shape'])
+@pytest.mark.parametrize('name', ['tiny_pad', 'small6_pad', 'hd96', 'c2shape', 'c4shape'])
 def test_step_matches_oracle(name):
     torch.set_num_threads(min(16, os.cpu_count()))
     g, hp, params, ids = setup(name)
@@ -46,6 +48,9 @@ def test_step_matches_oracle(name):
     assert abs(loss - ref['loss'].item()) / abs(ref['loss'].item()) < 1e-3
     assert abs(-(nll + kl) - elbo_ref) / abs(elbo_ref) < 1e-3
     assert abs(kl - ref['kl'].item()) / abs(ref['kl'].item()) < 2e-2
+    # the oracle itself is pinned to the reference's logged values (test_oracle_golden); check the engine
+    # against the reference's own numbers too
+    assert abs(loss - float(g['loss'])) / abs(float(g['loss'])) < 1e-3
     mu = out['mu'].cpu()
     assert ((mu - ref['mu'].detach().view_as(mu)).norm() / ref['mu'].detach().norm()).item() < 2e-2
 
@@ -61,8 +66,8 @@ def test_step_matches_oracle(name):
     worst.sort()
     msg = '\n'.join(f'{c:.5f} {r:.4f} {n}' for c, r, n in worst[:8])
     print(f'[{name}] loss {loss:.6f} ref {ref["loss"].item():.6f} kl {kl:.6f} ref {ref["kl"].item():.6f}\n' + msg)
-    assert worst[0][0] > 0.98, msg
-    assert all(0.95 < r < 1.05 for _, r, _ in worst), msg
+    assert worst[0][0] >= 0.995, msg
+    assert all(0.98 < r < 1.02 for _, r, _ in worst), msg
 
 
 @pytest.mark.parametrize('name,window', [('tiny_pad', 1), ('small6_pad', 2), ('c2shape', 4)])
@@ -100,8 +105,8 @@ def test_sparse_step_matches_oracle(name, window):
     worst.sort()
     msg = '\n'.join(f'{c:.5f} {r:.4f} {n}' for c, r, n in worst[:8])
     print(f'[{name} w{window}] loss {loss:.6f} ref {ref["loss"].item():.6f}\n' + msg)
-    assert worst[0][0] > 0.98, msg
-    assert all(0.95 < r < 1.05 for _, r, _ in worst), msg
+    assert worst[0][0] >= 0.995, msg
+    assert all(0.98 < r < 1.02 for _, r, _ in worst), msg
 
 
 @pytest.mark.parametrize('name', ['tiny_pad', 'small6_pad', 'c2shape'])

@@ -12,7 +12,7 @@ HEADER = os.path.join(ROOT, 'include', 'svae.h')
 def header_functions():
     src = open(HEADER).read()
     src = re.sub(r'/\*.*?\*/', '', src, flags=re.S)
-    return sorted(set(re.findall(r'^\s*(?:int|int64_t|const char\*)\s+(svae_\w+)\s*\(', src, flags=re.M)))
+    return sorted(set(re.findall(r'^\s*(?:int|int32_t|int64_t|const char\*)\s+(svae_\w+)\s*\(', src, flags=re.M)))
 
 
 def header_struct_fields(name):

@@ -122,3 +122,20 @@ def test_sparse_rotary_table_matches_reference():
     a, b = x[:, 0::2], x[:, 1::2]
     out = torch.stack([a * c + (-b) * s, b * c + a * s], -1).flatten(-2)
     np.testing.assert_allclose(out.numpy(), g['rot2_out'][0], rtol=0, atol=2e-6)
+
+
+def test_robust_cross_entropy_chunked_branch_pinned():
+    """The > 2^30-element branch (language_model.py:163-170): 2 sequence chunks, mean of per-chunk means, and the
+    class-weighted form (val_bpb), against the reference's own values on the same 4.3 GB of logits."""
+    from golden_util import ce_logits, setup_ce
+    torch.set_num_threads(min(8, os.cpu_count()))
+    g, t, labels = setup_ce()
+    logits = ce_logits(t['a'], t['u'], t['w'], t['s'])
+    assert -(-logits.numel() // 2 ** 30) == 2
+    with torch.no_grad():
+        nll = oracle.robust_cross_entropy(logits, labels).item()
+        wnll = oracle.robust_cross_entropy(logits, labels, weight=t['tok_w']).item()
+    del logits
+    assert abs(nll - float(g['nll'])) <= 1e-6 * abs(float(g['nll']))
+    assert abs(wnll - float(g['wnll'])) <= 1e-6 * abs(float(g['wnll']))
+    assert abs(float(g['nll']) - float(g['single_mean'])) > 1e-3   # the chunking matters at this bar

@@ -66,7 +66,8 @@ def main(args):
     model = TransformerVAE(hparams)
     data = TextDataModule(**config.get('data', {}))
     trainer = Trainer(**config['trainer'])
-    return trainer.fit(model, datamodule=data)
+    trainer.fit(model, datamodule=data)
+    return trainer
 
 
 if __name__ == '__main__':
