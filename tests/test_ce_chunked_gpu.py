@@ -65,10 +65,12 @@ def test_chunked_nll_matches_reference():
     wn = torch.empty(1, device=dev)
     K.ce_weighted_nll(rl, lab, t['tok_w'].to(dev), T, L, nchunks, chunk_len, wn)
     assert abs(wn.item() - float(g['wnll'])) / float(g['wnll']) < 1e-5, (wn.item(), float(g['wnll']))
-    # the stored logits are the fixture's exactly (bf16 of the exact f32 values)
+    # the stored (bf16) logits are the fixture's: within one bf16 rounding of the f32 values, identical to their
+    # bf16 rounding almost everywhere (the MFMA's f32 sum may differ in the last bit, flipping a bf16 tie)
     ref = ce_logits(t['a'][:2], t['u'][:2], t['w'], t['s'])
     got = logits.view(B, L, V)[:2, :L - 1].float().cpu()
-    assert torch.equal(got, ref.bfloat16().float())
+    assert ((got - ref).abs() <= ref.abs() * 2.0 ** -8 + 1e-30).all()
+    assert (got != ref.bfloat16().float()).float().mean().item() < 1e-3
 
 
 @pytest.mark.parametrize('nchunks', [2, 3])
