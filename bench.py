@@ -234,7 +234,9 @@ def main():
                        'seq_len': cfg['L'], 'parallelism': f'dp{world}'},
             'model_tflops_per_gpu': round(value / world * fpt / 1e12, 1),
             'step_mfu': round(value / world * fpt / (PEAK_BF16_TFLOPS * 1e12), 4),
-            'roofline': {'kernel': 'gemm256_kernel<false,false,SVAE_EPI_CE_STATS> (vocab head + CE stats)',
+            'roofline': {'kernel': ('gemm256_kernel<false,false,SVAE_EPI_CE_PROB> (vocab head, stores P = exp(logit - '
+                                    'label logit) + per-tile sums)' if eng.head_mode == 'prob' else
+                                    'gemm256_kernel<false,false,SVAE_EPI_CE_STATS> (vocab head + CE stats)'),
                          'bound': 'mfma', 'achieved': round(achieved, 1) if achieved else None,
                          'peak': PEAK_BF16_TFLOPS, 'unit': 'TFLOP/s',
                          'frac': round(achieved / PEAK_BF16_TFLOPS, 4) if achieved else None,

@@ -43,8 +43,13 @@ enum svae_epi {
   SVAE_EPI_GELU_BWD = 5,      /* C bf16 = acc * aux  (aux = the gelu' saved by SVAE_EPI_GELU)          */
   SVAE_EPI_DROPOUT_RESID = 6, /* C f32 = resid + keep(seed, m*N+n) * acc / (1 - p)                     */
   SVAE_EPI_ROTARY_BF16 = 7,   /* C bf16 = rotary(acc + bias) on cols < rot_cols (attention.py:194-208) */
-  SVAE_EPI_CE_STATS = 8       /* C bf16 = acc + bias; per (row, 128-col tile) online (max, sumexp) to
+  SVAE_EPI_CE_STATS = 8,      /* C bf16 = acc + bias; per (row, 128-col tile) online (max, sumexp) to
                                  aux f32 [M][ceil(N/128)][2]; label logit (f32) to resid-as-out [M]   */
+  SVAE_EPI_CE_PROB = 9,       /* vocab head, training: C bf16 = exp(acc + bias - row_a[m]) for rows with
+                                 labels[m] != 0, else 0 (exponent clamped at 2^127); aux f32
+                                 [M][ceil(N/128)] = per (row, 128-col tile) sums of those values       */
+  SVAE_EPI_ROWSCALE_GATHER = 10 /* C bf16 = alpha * row_a[m] * acc - row_b[m] * gather[labels[m]][n]
+                                 (the gather term is skipped where labels[m] == 0)                    */
 };
 
 typedef struct svae_gemm_desc {
@@ -70,6 +75,12 @@ typedef struct svae_gemm_desc {
   const int32_t* labels;    /* CE_STATS: [M] target column per row (0 = ignored) */
   float* label_logit;       /* CE_STATS: [M] f32 out */
   float* a_rowsum;          /* a_t only, optional: a_rowsum[m] += sum_k A[m][k] (bias grad of a dW GEMM) */
+  /* optional with a_rowsum (a_t && b_t, splits 1): a_rowsum[m] += sum_k A[m][k] * k_weight[k]            */
+  const float* k_weight;
+  const float* row_a;       /* CE_PROB / ROWSCALE_GATHER: [M] f32 (see svae_epi)                        */
+  const float* row_b;       /* ROWSCALE_GATHER: [M] f32                                                  */
+  const void* gather;       /* ROWSCALE_GATHER: bf16 rows [*][ldg], row labels[m] gathered; 16-B aligned */
+  int64_t ldg;
 } svae_gemm_desc;
 
 int svae_gemm(const svae_gemm_desc* d, svae_stream_t stream);
@@ -177,6 +188,33 @@ int32_t svae_ce_red_ws_elems(int32_t nchunks);
 int svae_ce_grad(void* logits, int64_t ld, const float* lse, const float* chunk_w, const int32_t* labels,
                  const float* gscale, float* dbias, int32_t rows, int32_t V, int32_t seq, int32_t nchunks,
                  int32_t chunk_len, svae_stream_t stream);
+
+/* ---- P-head cross entropy (training path of the tied vocabulary head + robust_cross_entropy) -----------
+ * The head GEMM (SVAE_EPI_CE_PROB, row_a = c) stores P = exp(logit - c), c = the row's label logit, instead of
+ * the logits; the backward then needs neither an exponential nor a dlogits pass:
+ *   dlogits = r (x) P - q (x) onehot(label),  q = gscale * chunk_w[chunk] (0 for ignored rows),
+ *   r = q * exp(c - lse);  dX = r . (P W) - q W[label] (SVAE_EPI_ROWSCALE_GATHER);
+ *   dW = P^T (r . hh) (+ the one-hot part, svae_embedding_bwd_ce); d bias = sum_t r_t P[t] (k_weight row sums
+ *   of the dW GEMM) - q scattered to the labels (bwd_prep).
+ * ce_label_logit: out[r] = hh[r] . W[labels[r]] + bias[labels[r]] (f32 dot of bf16 rows; 0 where labels[r] = 0).
+ * ce_prob_finalize: part f32 [rows][ntile] (the per-tile sums of P) -> lse = c + log sum, row_loss = lse - c,
+ *   chunk_w, nll_out: the chunked mean of means of svae_ce_finalize.
+ * ce_prob_bwd_prep: r_out, q_out [rows]; hh_out bf16 [rows][D] = r * hh; dbias[label] -= q (atomics; may be NULL).
+ * Exact while every labelled row's logits stay below its label logit + 88 (a token loss < 88 nats): beyond, the
+ * exponent saturates at 2^127. */
+int svae_ce_label_logit(const void* hh, int64_t ldh, const void* W, int64_t ldw, const float* bias,
+                        const int32_t* labels, int32_t rows, int32_t D, float* out, svae_stream_t stream);
+int svae_ce_prob_finalize(const float* part, int32_t ntile, const float* row_off, const int32_t* labels,
+                          int32_t rows, int32_t seq, int32_t nchunks, int32_t chunk_len, float* lse, float* row_loss,
+                          float* chunk_w, float* nll_out, float* red_ws, svae_stream_t stream);
+int svae_ce_prob_bwd_prep(const void* hh, int64_t ldh, const float* lse, const float* row_off, const float* chunk_w,
+                          const int32_t* labels, const float* gscale, int32_t rows, int32_t seq, int32_t nchunks,
+                          int32_t chunk_len, int32_t D, void* hh_out, float* r_out, float* q_out, float* dbias,
+                          svae_stream_t stream);
+/* Embedding backward fused with the one-hot part of the P-head's dW: dtable[ids[t]] += dout[t] - q[t-1] * hh[t-1]
+ * (the second term where t % seq != 0; valid because labels[t-1] = ids[t] inside a sequence). */
+int svae_embedding_bwd_ce(const int32_t* ids, const float* dout, float* dtable, int32_t rows, int32_t D, int32_t seq,
+                          const void* hh, const float* q, svae_stream_t stream);
 
 /* ---- elementwise helpers ------------------------------------------------------------------------ */
 /* dropout backward + cast: out bf16 = keep(seed, idx) * g / (1-p) (p = 0: plain cast). */

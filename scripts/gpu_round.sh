@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 OUT=gpurun_out/${1:-run}
 ST=${2:-tbpm}
 mkdir -p "$OUT"
-HEAD_RE='gemm256_kernel<false, false, 8>'
+HEAD_RE="gemm256_kernel<false, false, (8|9)>"
 PB="python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-parity"
 run() { echo "== $*" >&2; "$@"; }
 rc=0

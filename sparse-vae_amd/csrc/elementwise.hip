@@ -36,6 +36,26 @@ __global__ __launch_bounds__(256) void emb_bwd_kernel(const int* __restrict__ id
   for (int c = lane; c < D; c += 64) atomicAdd(dtable + dst + c, dout[(long long)row * D + c]);
 }
 
+// Embedding backward fused with the one-hot part of the vocabulary head's dW (P-head, see ce_prob_*): dlogits =
+// r (x) P - q (x) onehot(labels) puts -q[t] * hh[t] into table row labels[t]; labels[t] = ids[t + 1] inside a
+// sequence (the head predicts the next token), so row ids[t] also receives -q[t-1] hh[t-1] (t % seq != 0): one
+// atomic pass for both (q = 0 where the label is ignored).
+__global__ __launch_bounds__(256) void emb_bwd_ce_kernel(const int* __restrict__ ids, const float* __restrict__ dout,
+                                                         float* __restrict__ dtable, int rows, int D, int seq,
+                                                         const bf16* __restrict__ hh, const float* __restrict__ q) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const long long dst = (long long)ids[row] * D;
+  const float qp = (row % seq != 0) ? q[row - 1] : 0.f;
+  const bf16* hp = hh + (long long)(row - 1) * D;
+  for (int c = lane; c < D; c += 64) {
+    float g = dout[(long long)row * D + c];
+    if (qp != 0.f) g -= qp * (float)hp[c];
+    atomicAdd(dtable + dst + c, g);
+  }
+}
+
 // ------------------------------------------------------------------ reparameterise + KL
 // One wave per sample (latent index on the lane); one block of 4 waves walks all samples so the batch
 // means come out of the same launch.
@@ -119,6 +139,90 @@ __global__ __launch_bounds__(256) void ce_rows_kernel(const float* __restrict__ 
     const float l = mx + __logf(se);
     lse[row] = l;
     row_loss[row] = labels[row] != 0 ? l - label_logit[row] : 0.f;
+  }
+}
+
+// ---- P-head cross entropy (training): the vocabulary GEMM stores P = exp(logit - c) with c = the row's label
+// logit (SVAE_EPI_CE_PROB) instead of the logits, so the backward needs no exponential and no dlogits pass:
+//   dlogits = r (x) P - q (x) onehot,  q = g * w_chunk (0 for ignored rows),  r = q * exp(c - lse)
+//   dX = r . (P W) - q W[label]   (SVAE_EPI_ROWSCALE_GATHER)
+//   dW = P^T (r . hh) + [one-hot part, folded into the embedding backward], d bias = sum_t r_t P[t] - hist(q)
+// c from ce_label_logit: one wave per row, f32 dot of the bf16 operands + bias (0 for ignored rows).
+__global__ __launch_bounds__(256) void ce_label_logit_kernel(const bf16* __restrict__ hh, long long ldh,
+                                                             const bf16* __restrict__ W, long long ldw,
+                                                             const float* __restrict__ bias,
+                                                             const int* __restrict__ labels, int rows, int D,
+                                                             float* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int lab = labels[row];
+  if (lab == 0) {
+    if (lane == 0) out[row] = 0.f;
+    return;
+  }
+  float acc = 0.f;
+  for (int c = lane * 8; c < D; c += 512) {
+    const bf16x8 a = *(const bf16x8*)(hh + (long long)row * ldh + c);
+    const bf16x8 b = *(const bf16x8*)(W + (long long)lab * ldw + c);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc = fmaf((float)a[e], (float)b[e], acc);
+  }
+  acc = wave_sum(acc);
+  if (lane == 0) out[row] = acc + (bias ? bias[lab] : 0.f);
+}
+
+// lse = c + log(sum of the row's per-tile sums of P); row loss = lse - c (labelled rows; 0 and lse = 0 otherwise)
+__global__ __launch_bounds__(256) void ce_prob_rows_kernel(const float* __restrict__ part, int ntile,
+                                                           const float* __restrict__ off, const int* __restrict__ labels,
+                                                           int rows, float* __restrict__ lse, float* __restrict__ row_loss) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const float* pr = part + (long long)row * ntile;
+  float se = 0.f;
+  for (int t = lane; t < ntile; t += 64) se += pr[t];
+  se = wave_sum(se);
+  if (lane == 0) {
+    const bool live = labels[row] != 0;
+    const float l = live ? __logf(se) : 0.f;
+    lse[row] = live ? off[row] + l : 0.f;
+    row_loss[row] = l;
+  }
+}
+
+// Backward prologue of the P-head, one wave per row: q = g * w_chunk, r = q * exp(c - lse) (0 for ignored rows),
+// hh_out = r * hh (the B operand of dW = P^T (r . hh)), d bias[label] -= q (the one-hot column sums).
+__global__ __launch_bounds__(256) void ce_prob_bwd_prep_kernel(const bf16* __restrict__ hh, long long ldh,
+                                                               const float* __restrict__ lse,
+                                                               const float* __restrict__ off,
+                                                               const float* __restrict__ chunk_w,
+                                                               const int* __restrict__ labels,
+                                                               const float* __restrict__ gscale, int rows, int seq,
+                                                               int nchunks, int chunk_len, int D,
+                                                               bf16* __restrict__ hh_out, float* __restrict__ r_out,
+                                                               float* __restrict__ q_out, float* __restrict__ dbias) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int lab = labels[row];
+  float q = 0.f, r = 0.f;
+  if (lab != 0) {
+    const int ch = min((row % seq) / chunk_len, nchunks - 1);
+    q = gscale[0] * chunk_w[ch];
+    r = q * __expf(off[row] - lse[row]);
+  }
+  for (int c = lane * 8; c < D; c += 512) {
+    const bf16x8 a = *(const bf16x8*)(hh + (long long)row * ldh + c);
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = f2bf(r * (float)a[e]);
+    *(bf16x8*)(hh_out + (long long)row * D + c) = o;
+  }
+  if (lane == 0) {
+    r_out[row] = r;
+    q_out[row] = q;
+    if (lab != 0 && dbias) atomicAdd(dbias + lab, -q);
   }
 }
 
@@ -559,6 +663,57 @@ SVAE_EXPORT int svae_embedding_bwd(const int32_t* ids, const float* dout, float*
                                    svae_stream_t stream) {
   if (!ids || !dout || !dtable || rows <= 0 || D <= 0) return SVAE_EINVAL;
   hipLaunchKernelGGL(emb_bwd_kernel, dim3((rows + 3) / 4), dim3(256), 0, (hipStream_t)stream, ids, dout, dtable, rows, D);
+  SVAE_LAUNCH_CHECK();
+  return SVAE_OK;
+}
+
+SVAE_EXPORT int svae_embedding_bwd_ce(const int32_t* ids, const float* dout, float* dtable, int32_t rows, int32_t D,
+                                      int32_t seq, const void* hh, const float* q, svae_stream_t stream) {
+  if (!ids || !dout || !dtable || !hh || !q || rows <= 0 || D <= 0 || seq <= 0 || rows % seq) return SVAE_EINVAL;
+  hipLaunchKernelGGL(emb_bwd_ce_kernel, dim3((rows + 3) / 4), dim3(256), 0, (hipStream_t)stream, ids, dout, dtable, rows,
+                     D, seq, (const bf16*)hh, q);
+  SVAE_LAUNCH_CHECK();
+  return SVAE_OK;
+}
+
+SVAE_EXPORT int svae_ce_label_logit(const void* hh, int64_t ldh, const void* W, int64_t ldw, const float* bias,
+                                    const int32_t* labels, int32_t rows, int32_t D, float* out, svae_stream_t stream) {
+  if (!hh || !W || !labels || !out || rows <= 0 || D <= 0 || D % 8 || ldh % 8 || ldw % 8) return SVAE_EINVAL;
+  if (((uintptr_t)hh | (uintptr_t)W) & 15) return SVAE_EINVAL;
+  hipLaunchKernelGGL(ce_label_logit_kernel, dim3((rows + 3) / 4), dim3(256), 0, (hipStream_t)stream, (const bf16*)hh,
+                     (long long)ldh, (const bf16*)W, (long long)ldw, bias, labels, rows, D, out);
+  SVAE_LAUNCH_CHECK();
+  return SVAE_OK;
+}
+
+SVAE_EXPORT int svae_ce_prob_finalize(const float* part, int32_t ntile, const float* row_off, const int32_t* labels,
+                                      int32_t rows, int32_t seq, int32_t nchunks, int32_t chunk_len, float* lse,
+                                      float* row_loss, float* chunk_w, float* nll_out, float* red_ws,
+                                      svae_stream_t stream) {
+  if (!part || !row_off || !labels || !lse || !row_loss || !chunk_w || !nll_out || !red_ws) return SVAE_EINVAL;
+  if (rows <= 0 || ntile <= 0 || seq <= 0 || rows % seq || nchunks <= 0 || nchunks > CE_MAX_CHUNKS ||
+      chunk_len <= 0 || (long long)(nchunks - 1) * chunk_len >= seq)
+    return SVAE_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(ce_prob_rows_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, part, ntile, row_off, labels, rows, lse,
+                     row_loss);
+  hipLaunchKernelGGL(ce_reduce_part_kernel, dim3(CE_RED_BLOCKS, nchunks), dim3(256), 0, s, row_loss, labels,
+                     (const float*)nullptr, rows, seq, nchunks, chunk_len, red_ws);
+  hipLaunchKernelGGL(ce_reduce_final_kernel, dim3(1), dim3(256), 0, s, red_ws, nchunks, chunk_w, nll_out);
+  SVAE_LAUNCH_CHECK();
+  return SVAE_OK;
+}
+
+SVAE_EXPORT int svae_ce_prob_bwd_prep(const void* hh, int64_t ldh, const float* lse, const float* row_off,
+                                      const float* chunk_w, const int32_t* labels, const float* gscale, int32_t rows,
+                                      int32_t seq, int32_t nchunks, int32_t chunk_len, int32_t D, void* hh_out,
+                                      float* r_out, float* q_out, float* dbias, svae_stream_t stream) {
+  if (!hh || !lse || !row_off || !chunk_w || !labels || !gscale || !hh_out || !r_out || !q_out) return SVAE_EINVAL;
+  if (rows <= 0 || seq <= 0 || nchunks <= 0 || chunk_len <= 0 || D <= 0 || D % 8 || ldh % 8) return SVAE_EINVAL;
+  if (((uintptr_t)hh | (uintptr_t)hh_out) & 15) return SVAE_EINVAL;
+  hipLaunchKernelGGL(ce_prob_bwd_prep_kernel, dim3((rows + 3) / 4), dim3(256), 0, (hipStream_t)stream, (const bf16*)hh,
+                     (long long)ldh, lse, row_off, chunk_w, labels, gscale, rows, seq, nchunks, chunk_len, D,
+                     (bf16*)hh_out, r_out, q_out, dbias);
   SVAE_LAUNCH_CHECK();
   return SVAE_OK;
 }

@@ -33,6 +33,9 @@ struct GP {
   const float* rot_tab; int rot_cols, rot_d, rot_seq;
   const int* labels; float* label_logit;
   float* a_rowsum;   // optional: += sum_k A[m][k] (bias gradient fused into the dW GEMM); a_t layout only
+  const float* k_weight;   // optional with a_rowsum: a_rowsum[m] += sum_k A[m][k] * k_weight[k] (gemm256 only)
+  const float* row_a; const float* row_b;   // CE_PROB offset / ROWSCALE_GATHER scale and gather weight, per row
+  const bf16* gather; long long ldg;        // ROWSCALE_GATHER: bf16 rows, row labels[m] gathered
   int epi;
   int tn2, tm2;      // 256-tile counts (gemm256)
   int group;         // L2 grouping: consecutive tiles walk `group` tile rows (M) before the next tile column
@@ -777,11 +780,34 @@ __device__ __forceinline__ void g3_reg_epilogue(const GP& p, const f32x4 (&acc)[
           store_pair_bf16(crow, 32 * jp, row_ok ? nleft : 0, gg[2 * jp], gg[2 * jp + 1], g);
           store_pair_bf16(arow, 32 * jp, row_ok ? nleft : 0, dg[2 * jp], dg[2 * jp + 1], g);
         }
+      } else if constexpr (EPI == SVAE_EPI_CE_PROB) {
+        // p = exp(logit - c_row) for rows with a target (0 elsewhere); the f32 values feed the per-tile sums below
+        const float off = sstat[1024 + rl] * G3_LOG2E;
+        const bool live = slabel[rl] != 0;
+        const bool ragged = n0 + wc * 64 + 64 > p.N;   // wave-uniform
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float x = __builtin_amdgcn_exp2f(fminf(fmaf(v[j][e], G3_LOG2E, -off), 127.0f));
+            if (ragged && n0 + wc * 64 + j * 16 + 4 * g + e >= p.N) x = 0.f;
+            v[j][e] = live ? x : 0.f;
+          }
+#pragma unroll
+        for (int jp = 0; jp < 2; ++jp)   // P [T, V] bf16 (2 GiB at C2): nontemporal
+          store_pair_bf16<true>(crow, 32 * jp, row_ok ? nleft : 0, v[2 * jp], v[2 * jp + 1], g);
       } else if (EPI != SVAE_EPI_CE_STATS || p.C) {   // CE statistics with C == nullptr: no logits stored
 #pragma unroll
         for (int jp = 0; jp < 2; ++jp)   // vocab logits (2 GiB at C2): nontemporal, 1444 -> 1322 us
           store_pair_bf16<EPI == SVAE_EPI_CE_STATS>(crow, 32 * jp, row_ok ? nleft : 0, v[2 * jp], v[2 * jp + 1], g);
       }
+    }
+    if constexpr (EPI == SVAE_EPI_CE_PROB) {
+      float se = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) se += (v[j][0] + v[j][1]) + (v[j][2] + v[j][3]);
+      se = sum_x16_x32(se);
+      if (g == 0) sstat[rl * 4 + wc] = se;
     }
     if constexpr (EPI == SVAE_EPI_CE_STATS) {
       const bool ragged = n0 + wc * 64 + 64 > p.N;   // wave-uniform
@@ -830,6 +856,65 @@ __device__ __forceinline__ void g3_reg_epilogue(const GP& p, const f32x4 (&acc)[
       float* part = (float*)p.aux + ((long long)m * p.tiles_n + bn * 2 + hf) * 2;
       part[0] = mm;
       part[1] = s1 * e1 + s2 * e2;
+    }
+  }
+  if constexpr (EPI == SVAE_EPI_CE_PROB) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    const int row = tid >> 1, hf = tid & 1, m = m0 + row;   // 512 threads: (row, 128-column half)
+    if (m < p.M && n0 + 128 * hf < p.N)
+      ((float*)p.aux)[(long long)m * p.tiles_n + bn * 2 + hf] = sstat[row * 4 + 2 * hf] + sstat[row * 4 + 2 * hf + 1];
+  }
+}
+
+// ROWSCALE_GATHER (the vocabulary head's dX = dlogits . W with dlogits = r (x) P - q (x) onehot, never stored):
+// C bf16 [m][n] = row_a[m] * acc - row_b[m] * gather[labels[m]][n]. The permlane-swapped 8-column layout of
+// store_pair_bf16 with 16-B gather loads of the same 8 columns; row i + 1's gather rows are loaded before row i's
+// stores (vmcnt retires in issue order).
+__device__ __forceinline__ void g3_rowscale_gather_epilogue(const GP& p, const f32x4 (&acc)[8][4], const int* slabel,
+                                                            const float* sra, const float* srb, int m0, int n0, int wr,
+                                                            int wc, int lane) {
+  const int g = lane >> 4, li = lane & 15;
+  const int nb = n0 + wc * 64;
+  const int cs = ((g & 1) ? 16 : 0) + ((g & 2) ? 8 : 0);
+  auto ld_row = [&](int i, u32x4 (&r)[2]) {
+    const int rl = wr * 128 + i * 16 + li, m = m0 + rl, lab = slabel[rl];
+    const bool on = m < p.M && lab != 0 && srb[rl] != 0.f;
+#pragma unroll
+    for (int jp = 0; jp < 2; ++jp) {
+      const int n = nb + 32 * jp + cs;
+      r[jp] = (on && n + 8 <= p.N) ? *(const u32x4*)(p.gather + (long long)lab * p.ldg + n) : (u32x4){0u, 0u, 0u, 0u};
+    }
+  };
+  u32x4 cur[2], nxt[2];
+  ld_row(0, cur);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    if (i + 1 < 8) ld_row(i + 1, nxt);
+    const int rl = wr * 128 + i * 16 + li, m = m0 + rl;
+    const float ra = sra[rl] * p.alpha, rb = srb[rl];
+#pragma unroll
+    for (int jp = 0; jp < 2; ++jp) {
+      const f32x4 x = acc[i][2 * jp], y = acc[i][2 * jp + 1];
+      float w[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(x[e]), __float_as_uint(y[e]), false, false);
+        w[e] = __uint_as_float(sw[0]);
+        w[4 + e] = __uint_as_float(sw[1]);
+      }
+      const bf16x8 gv = __builtin_bit_cast(bf16x8, cur[jp]);
+      const u32x4 o = {pack_bf16x2(ra * w[0] - rb * (float)gv[0], ra * w[1] - rb * (float)gv[1]),
+                       pack_bf16x2(ra * w[2] - rb * (float)gv[2], ra * w[3] - rb * (float)gv[3]),
+                       pack_bf16x2(ra * w[4] - rb * (float)gv[4], ra * w[5] - rb * (float)gv[5]),
+                       pack_bf16x2(ra * w[6] - rb * (float)gv[6], ra * w[7] - rb * (float)gv[7])};
+      const int n = nb + 32 * jp + cs;
+      if (m < p.M && n + 8 <= p.N) *(u32x4*)((bf16*)p.C + (long long)m * p.ldc + n) = o;
+      else if (m < p.M && n < p.N) *(u32x2*)((bf16*)p.C + (long long)m * p.ldc + n) = (u32x2){o[0], o[1]};
+    }
+    if (i + 1 < 8) {
+      cur[0] = nxt[0];
+      cur[1] = nxt[1];
     }
   }
 }
@@ -964,6 +1049,9 @@ __device__ unsigned long long svae_stamps[8][96][3];
 #define G3_STAMP(k) ((void)0)
 #endif
 static_assert(G3_EPI_STORES == 16, "the first K-step's s_waitcnt literal below");
+// internal instantiation: SVAE_EPI_F32_ACC whose fused bias-gradient row sums are weighted by k_weight (the
+// vocabulary head's dW, where the per-token weight r folds the softmax normalisation into the row sums)
+constexpr int G3_EPI_ACC_KW = 64;
 
 template <bool AT, bool BT, int EPI>
 __global__ __launch_bounds__(512, 1) void gemm256_kernel(GP p) {
@@ -1093,14 +1181,17 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GP p) {
           for (int j = 0; j < 2; ++j) acc[4 + i][j] = mfma16(b0[j][ks], a1[i][ks], acc[4 + i][j]);
       G3_PRIO_LO();
       if constexpr (AT) {
-        if (p.a_rowsum && T.bn == 0) {   // sum_k A[k][m]: thread = 4 m (one 8-B unit) x 8 k-rows
-          const int u = tid & 63, kg = tid >> 6;
+        if (p.a_rowsum && T.bn == 0) {   // sum_k A[k][m] (* k_weight[k]): thread = 4 m (one 8-B unit) x 8 k-rows
+          const int u = tid & 63, kg = wave;   // (wave-uniform: the k_weight loads are scalar)
           const char* lh = la + (u >> 5) * (G3_T / 2);
+          const int kb = T.kbeg + kt * 64 + kg * 8;
 #pragma unroll
           for (int r = 0; r < 8; ++r) {
             const bf16x4 v = __builtin_bit_cast(bf16x4, *(const short4v*)(lh + mn_off(kg * 8 + r, u & 31)));
+            float kw = 1.f;
+            if constexpr (EPI == G3_EPI_ACC_KW) kw = kb + r < T.kend ? p.k_weight[kb + r] : 0.f;
 #pragma unroll
-            for (int e = 0; e < 4; ++e) rsum[e] += (float)v[e];
+            for (int e = 0; e < 4; ++e) rsum[e] += (float)v[e] * kw;
           }
         }
       }
@@ -1111,7 +1202,10 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GP p) {
     if (tid < 256) {
       const int n = T.n0 + tid, m = T.m0 + tid;
       sbias[tid] = (p.bias && n < p.N) ? p.bias[n] : 0.f;
-      if (EPI == SVAE_EPI_CE_STATS) slabel[tid] = m < p.M ? p.labels[m] : 0;
+      if (EPI == SVAE_EPI_CE_STATS || EPI == SVAE_EPI_CE_PROB || EPI == SVAE_EPI_ROWSCALE_GATHER)
+        slabel[tid] = m < p.M ? p.labels[m] : 0;
+      if (EPI == SVAE_EPI_CE_PROB || EPI == SVAE_EPI_ROWSCALE_GATHER) sstat[1024 + tid] = m < p.M ? p.row_a[m] : 0.f;
+      if (EPI == SVAE_EPI_ROWSCALE_GATHER) sstat[1280 + tid] = m < p.M ? p.row_b[m] : 0.f;
     }
     // every wave's reads of the last K-tile's stage are done: it becomes the epilogue's staging area
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1125,11 +1219,15 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GP p) {
       }
     }
     if constexpr (EPI == SVAE_EPI_BF16 || EPI == SVAE_EPI_GELU || EPI == SVAE_EPI_CE_STATS ||
-                  EPI == SVAE_EPI_ROTARY_BF16)
+                  EPI == SVAE_EPI_ROTARY_BF16 || EPI == SVAE_EPI_CE_PROB)
       g3_reg_epilogue<EPI>(p, acc, sbias, slabel, sstat, T.m0, T.n0, T.bn, T.batch, T.split, wr, wc, tid, lane);
+    else if constexpr (EPI == SVAE_EPI_ROWSCALE_GATHER)
+      g3_rowscale_gather_epilogue(p, acc, slabel, sstat + 1024, sstat + 1280, T.m0, T.n0, wr, wc, lane);
     else if constexpr (EPI == SVAE_EPI_F32 || EPI == SVAE_EPI_F32_ACC || EPI == SVAE_EPI_DROPOUT_RESID ||
                        EPI == SVAE_EPI_GELU_BWD)
       g3_reg_epilogue_ld<EPI>(p, acc, sbias, T.m0, T.n0, T.batch, T.split, wr, wc, lane);
+    else if constexpr (EPI == G3_EPI_ACC_KW)
+      g3_reg_epilogue_ld<SVAE_EPI_F32_ACC>(p, acc, sbias, T.m0, T.n0, T.batch, T.split, wr, wc, lane);
     else
       g3_epilogue<EPI>(p, smem + ((g + 1) & 1) * G3_STAGE, acc, sbias, slabel, T.m0, T.n0, T.bn, T.batch, T.split,
                        wr, wc, tid, lane);
@@ -1174,13 +1272,20 @@ static int launch_slab_reduce(const svae_gemm_desc* d, hipStream_t s) {
 
 SVAE_EXPORT int svae_gemm(const svae_gemm_desc* d, svae_stream_t stream) {
   if (!d || !d->A || !d->B || (!d->C && d->epi != SVAE_EPI_CE_STATS)) return SVAE_EINVAL;
+  const bool epi_new = d->epi == SVAE_EPI_CE_PROB || d->epi == SVAE_EPI_ROWSCALE_GATHER;
   if (d->M <= 0 || d->N <= 0 || d->K <= 0 || d->batch <= 0 || d->splits <= 0) return SVAE_EINVAL;
   if ((d->K % 8 && !(d->a_t && d->b_t)) || d->lda % 8 || d->ldb % 8) return SVAE_EINVAL;
   if (d->a_t && d->M % 8) return SVAE_EINVAL;
   if (d->b_t && d->N % 8) return SVAE_EINVAL;
   if (((uintptr_t)d->A | (uintptr_t)d->B) & 15) return SVAE_EINVAL;
   if (d->batch_stride_a % 8 || d->batch_stride_b % 8) return SVAE_EINVAL;
-  if (d->epi < 0 || d->epi > SVAE_EPI_CE_STATS) return SVAE_EINVAL;
+  if (d->epi < 0 || d->epi > SVAE_EPI_ROWSCALE_GATHER) return SVAE_EINVAL;
+  // the P-head epilogues (CE_PROB, ROWSCALE_GATHER) and weighted row sums exist in the 256x256 kernel only
+  if (epi_new && (d->a_t || d->splits != 1 || d->batch != 1 || !d->labels || !d->row_a)) return SVAE_EINVAL;
+  if (d->epi == SVAE_EPI_CE_PROB && !d->aux) return SVAE_EINVAL;
+  if (d->epi == SVAE_EPI_ROWSCALE_GATHER && (!d->row_b || !d->gather || d->ldg % 8 || ((uintptr_t)d->gather & 15)))
+    return SVAE_EINVAL;
+  if (d->k_weight && (!d->a_rowsum || !d->b_t || d->splits != 1)) return SVAE_EINVAL;
   if (d->epi == SVAE_EPI_ROTARY_BF16 && (!d->rot_tab || d->rot_d <= 0 || d->rot_seq <= 0)) return SVAE_EINVAL;
   if ((d->epi == SVAE_EPI_GELU || d->epi == SVAE_EPI_GELU_BWD || d->epi == SVAE_EPI_CE_STATS) && !d->aux)
     return SVAE_EINVAL;
@@ -1211,6 +1316,9 @@ SVAE_EXPORT int svae_gemm(const svae_gemm_desc* d, svae_stream_t stream) {
   p.rot_tab = d->rot_tab; p.rot_cols = d->rot_cols; p.rot_d = d->rot_d; p.rot_seq = d->rot_seq;
   p.labels = d->labels; p.label_logit = d->label_logit;
   p.a_rowsum = d->a_rowsum;
+  p.k_weight = d->k_weight;
+  p.row_a = d->row_a; p.row_b = d->row_b;
+  p.gather = (const bf16*)d->gather; p.ldg = d->ldg;
   p.epi = d->epi;
   p.slab = 0;
   // split-K slab mode (F32_ATOMIC with aux): every split stores its partial tile with plain stores into
@@ -1243,6 +1351,11 @@ SVAE_EXPORT int svae_gemm(const svae_gemm_desc* d, svae_stream_t stream) {
   const long long blocks256 = (long long)p.tn2 * p.tm2 * d->batch * d->splits;
   const bool ok3 = !(d->a_t && !d->b_t);
   int impl = forced ? forced : ((ok3 && blocks256 >= 192) ? 3 : ((kslice <= 2048 && !(d->a_t && d->b_t)) ? 2 : 1));
+  if (epi_new || d->k_weight) impl = 3;
+  if (d->k_weight) {
+    if (d->epi != SVAE_EPI_F32_ACC) return SVAE_EINVAL;
+    epi_run = G3_EPI_ACC_KW;
+  }
   if (impl == 3 && !ok3) impl = 1;
   if (impl == 3) {
     int kc3 = (d->K + d->splits - 1) / d->splits;
@@ -1280,6 +1393,16 @@ SVAE_EXPORT int svae_gemm(const svae_gemm_desc* d, svae_stream_t stream) {
       SVAE_GEMM3_CASE(SVAE_EPI_DROPOUT_RESID)
       SVAE_GEMM3_CASE(SVAE_EPI_ROTARY_BF16)
       SVAE_GEMM3_CASE(SVAE_EPI_CE_STATS)
+      case G3_EPI_ACC_KW:
+        hipLaunchKernelGGL((gemm256_kernel<true, true, G3_EPI_ACC_KW>), grid3, dim3(512), 0, s, p);
+        break;
+      case SVAE_EPI_CE_PROB:
+        hipLaunchKernelGGL((gemm256_kernel<false, false, SVAE_EPI_CE_PROB>), grid3, dim3(512), 0, s, p);
+        break;
+      case SVAE_EPI_ROWSCALE_GATHER:
+        if (d->b_t) hipLaunchKernelGGL((gemm256_kernel<false, true, SVAE_EPI_ROWSCALE_GATHER>), grid3, dim3(512), 0, s, p);
+        else hipLaunchKernelGGL((gemm256_kernel<false, false, SVAE_EPI_ROWSCALE_GATHER>), grid3, dim3(512), 0, s, p);
+        break;
       default: return SVAE_EINVAL;
     }
 #undef SVAE_GEMM3_CASE

@@ -17,7 +17,7 @@ c_void_p, c_int32, c_int64, c_float, c_uint64 = (ctypes.c_void_p, ctypes.c_int32
 c_fptr = ctypes.c_void_p
 
 EPI_BF16, EPI_F32, EPI_F32_ACC, EPI_F32_ATOMIC, EPI_GELU, EPI_GELU_BWD, EPI_DROPOUT_RESID, \
-    EPI_ROTARY_BF16, EPI_CE_STATS = range(9)
+    EPI_ROTARY_BF16, EPI_CE_STATS, EPI_CE_PROB, EPI_ROWSCALE_GATHER = range(11)
 
 
 class GemmDesc(ctypes.Structure):
@@ -36,6 +36,7 @@ class GemmDesc(ctypes.Structure):
         ('rot_tab', c_void_p), ('rot_cols', c_int32), ('rot_d', c_int32), ('rot_seq', c_int32),
         ('labels', c_void_p), ('label_logit', c_void_p),
         ('a_rowsum', c_void_p),
+        ('k_weight', c_void_p), ('row_a', c_void_p), ('row_b', c_void_p), ('gather', c_void_p), ('ldg', c_int64),
     ]
 
 
@@ -82,6 +83,13 @@ _SIGS = {
                              c_void_p],
     'svae_ce_red_ws_elems': [c_int32],
     'svae_clip_grad': [c_void_p, c_int64, c_void_p, c_int32, c_float, c_void_p, c_void_p],
+    'svae_ce_label_logit': [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_int32, c_int32, c_void_p,
+                            c_void_p],
+    'svae_ce_prob_finalize': [c_void_p, c_int32, c_void_p, c_void_p, c_int32, c_int32, c_int32, c_int32, c_void_p,
+                              c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+    'svae_ce_prob_bwd_prep': [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32,
+                              c_int32, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+    'svae_embedding_bwd_ce': [c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_int32, c_void_p, c_void_p, c_void_p],
     'svae_ce_grad': [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_int32,
                      c_int32, c_int32, c_void_p],
     'svae_dropout_bwd_cast': [c_void_p, c_void_p, c_float, c_uint64, c_int64, c_int32, c_int64, c_void_p],

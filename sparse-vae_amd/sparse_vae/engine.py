@@ -21,7 +21,7 @@ import torch
 
 from . import kernels as K
 from ._native import EPI_BF16, EPI_F32, EPI_F32_ACC, EPI_GELU, EPI_GELU_BWD, EPI_DROPOUT_RESID, \
-    EPI_ROTARY_BF16, EPI_CE_STATS, EPI_F32_ATOMIC
+    EPI_ROTARY_BF16, EPI_CE_STATS, EPI_F32_ATOMIC, EPI_CE_PROB, EPI_ROWSCALE_GATHER
 
 bf16, f32 = torch.bfloat16, torch.float32
 ALIGN = 64
@@ -230,6 +230,11 @@ class VAEEngine:
         # (they feed nothing else in it). Measured at C2: 15.33 vs 15.37 ms/step -- the overlap is eaten by
         # contention (LayerNorm backward 35 -> 85 us beside a GEMM, the head dW doubled beside the head dX), so
         # the default keeps one stream.
+        # vocabulary head + cross entropy of the training step: 'prob' stores P = exp(logit - label logit) and runs
+        # the backward on it without a dlogits pass (svae.h, P-head); 'logits' stores the bf16 logits and rewrites
+        # them into dlogits in place (ce_grad) -- the round-1 path, kept for A/B runs (SVAE_HEAD=logits)
+        self.head_mode = os.environ.get('SVAE_HEAD', 'prob')
+        assert self.head_mode in ('prob', 'logits'), self.head_mode
         self.side = None
         if flat.device.type == 'cuda' and os.environ.get('SVAE_DW_STREAM', '0') != '0':
             self.side = torch.cuda.Stream(device=flat.device)
@@ -512,29 +517,40 @@ class VAEEngine:
         K.gemm(xf, P.w('output_layer.0.weight'), h0, T, d, d, epi=EPI_GELU, bias=P.f('output_layer.0.bias'),
                aux=gp0, ldaux=d)
         hh, ln_h = self._ln_fwd('output_layer.2', h0, T, 'head.ln')
-        logits = ws.get('logits', (T, V))
-        ntile = -(-V // 128)
-        part = ws.get('ce.part', (T, ntile, 2), f32)
-        lab_logit = ws.get('ce.label_logit', (T,), f32)
-        probe = self.probe
-        if probe is not None:
-            e0 = torch.cuda.Event(enable_timing=True)
-            e0.record()
-        K.gemm(hh, P.w('input_layer.0.weight'), logits, T, V, d, epi=EPI_CE_STATS, bias=P.f('output_layer.3.bias'),
-               aux=part, labels=labels, label_logit=lab_logit)
-        if probe is not None:
-            e1 = torch.cuda.Event(enable_timing=True)
-            e1.record()
-            probe.append((e0, e1))
         nchunks, chunk_len = K.ce_chunking(B, L, V, CE_CHUNK_NUMEL)
         lse = ws.get('ce.lse', (T,), f32)
         row_loss = ws.get('ce.row_loss', (T,), f32)
         chunk_w = ws.get('ce.chunk_w', (max(8, nchunks),), f32)
         nll = ws.get('nll', (1,), f32)
-        K.ce_finalize(part, ntile, lab_logit, labels, T, L, nchunks, chunk_len, lse, row_loss, chunk_w, nll)
+        ntile = -(-V // 128)
+        head = 'logits' if need_logits else self.head_mode
+        W, bias = P.w('input_layer.0.weight'), P.f('output_layer.3.bias')
+        logits = ws.get('logits', (T, V))          # the bf16 logits, or P = exp(logit - label logit)
+        probe = self.probe
+        if probe is not None:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+        if head == 'prob':
+            coff = ws.get('ce.off', (T,), f32)
+            K.ce_label_logit(hh, W, bias, labels, T, d, coff)
+            part = ws.get('ce.psum', (T, ntile), f32)
+            K.gemm(hh, W, logits, T, V, d, epi=EPI_CE_PROB, bias=bias, aux=part, labels=labels, row_a=coff)
+        else:
+            coff = None
+            part = ws.get('ce.part', (T, ntile, 2), f32)
+            lab_logit = ws.get('ce.label_logit', (T,), f32)
+            K.gemm(hh, W, logits, T, V, d, epi=EPI_CE_STATS, bias=bias, aux=part, labels=labels, label_logit=lab_logit)
+        if probe is not None:
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record()
+            probe.append((e0, e1))
+        if head == 'prob':
+            K.ce_prob_finalize(part, ntile, coff, labels, T, L, nchunks, chunk_len, lse, row_loss, chunk_w, nll)
+        else:
+            K.ce_finalize(part, ntile, lab_logit, labels, T, L, nchunks, chunk_len, lse, row_loss, chunk_w, nll)
         sv.update(xf=xf, gp0=gp0, h0=h0, hh=hh, ln_h=ln_h, logits=logits, lse=lse, chunk_w=chunk_w,
                   nchunks=nchunks, chunk_len=chunk_len, labels=labels, ids32=ids32, ntok=ntok64, x_emb=x_emb,
-                  row_loss=row_loss)
+                  row_loss=row_loss, head=head, coff=coff)
         loss = nll[0] + kl_weight * kl[0]                                          # transformer_vae.py:55
         self.saved = sv
         return {'loss': loss, 'nll': nll[0], 'kl': kl[0], 'train_kl': kl[1], 'raw_kl': raw_kl,
@@ -777,11 +793,30 @@ class VAEEngine:
 
         # ---- head
         logits = sv['logits']
-        K.ce_grad(logits, V, sv['lse'], sv['chunk_w'], sv['labels'], gs[0:1], T, V, L, sv['nchunks'], sv['chunk_len'])
-        # (the vocabulary-head dW stays in order: next to the equally large head dX it only contends)
-        self._dw(logits, sv['hh'], 'input_layer.0.weight', T, V, d, bias='output_layer.3.bias', on_side=False)
         dhh = ws.get('b.dhh', (T, d))
-        K.gemm(logits, P.wT('input_layer.0.weight', V, d), dhh, T, d, V, epi=EPI_BF16)
+        nch, clen = sv['nchunks'], sv['chunk_len']
+        if sv['head'] == 'prob':
+            # dlogits = r (x) P - q (x) onehot, never formed: dW = P^T (r . hh) (+ one-hot part in the embedding
+            # backward), d bias = sum_t r_t P[t] (weighted row sums of the dW GEMM) - q at the labels (prep),
+            # dX = r . (P W) - q W[label]
+            hh = sv['hh']
+            hh_r = ws.get('b.hh_r', (T, d))
+            r_t = ws.get('b.ce_r', (T,), f32)
+            q_t = ws.get('b.ce_q', (T,), f32)
+            dbias = P.g('output_layer.3.bias')
+            K.ce_prob_bwd_prep(hh, sv['lse'], sv['coff'], sv['chunk_w'], sv['labels'], gs[0:1], T, L, nch, clen, d, hh_r,
+                               r_t, q_t, dbias)
+            K.gemm(logits, hh_r, P.g('input_layer.0.weight'), V, d, T, a_t=True, b_t=True, lda=V, ldb=d, ldc=d,
+                   epi=EPI_F32_ACC, a_rowsum=dbias, k_weight=r_t)
+            W = P.w('input_layer.0.weight')
+            K.gemm(logits, P.wT('input_layer.0.weight', V, d), dhh, T, d, V, epi=EPI_ROWSCALE_GATHER,
+                   labels=sv['labels'], row_a=r_t, row_b=q_t, gather=W, ldg=d)
+            sv['ce_q'] = q_t
+        else:
+            K.ce_grad(logits, V, sv['lse'], sv['chunk_w'], sv['labels'], gs[0:1], T, V, L, nch, clen)
+            # (the vocabulary-head dW stays in order: next to the equally large head dX it only contends)
+            self._dw(logits, sv['hh'], 'input_layer.0.weight', T, V, d, bias='output_layer.3.bias', on_side=False)
+            K.gemm(logits, P.wT('input_layer.0.weight', V, d), dhh, T, d, V, epi=EPI_BF16)
         dh0 = ws.get('b.dh0', (T, d), f32)
         self._ln_bwd('output_layer.2', dhh, sv['ln_h'], T, None, dh0)
         dpre0 = ws.get('b.dpre0', (T, d))
@@ -836,13 +871,20 @@ class VAEEngine:
             tmp = ws.get('b.dfirst', (T, d), f32)
             self.layer_bwd(st0, dcur, tmp)
             self.join_side()        # the tied weight's head gradient (side stream) before the scatter-add
-            K.embedding_bwd(sv['ids32'], tmp, P.g('input_layer.0.weight'), T, d)
+            K.embedding_bwd(sv['ids32'], tmp, P.g('input_layer.0.weight'), T, d)   # (the head's part: below)
         else:
             self.layer_bwd(st0, dcur, dx_emb, dx_accumulate=True)
 
         ready(P.end('encoder.first_layer.ffn_layer_norm.bias'))
         # ---- embedding (tied with the head weight)
         self.join_side()            # the tied weight's head gradient (side stream) before the scatter-add
-        K.embedding_bwd(sv['ids32'], dx_emb, P.g('input_layer.0.weight'), T, d)
+        self._embedding_bwd(sv, dx_emb, T, d)
         ready(P.n_live)
         self.join_side()
+
+    def _embedding_bwd(self, sv, dx, T, d):
+        """Scatter-add of d x_emb into the tied table; with the P-head, fused with the head's one-hot dW part."""
+        if sv['head'] == 'prob':
+            K.embedding_bwd_ce(sv['ids32'], dx, self.P.g('input_layer.0.weight'), T, d, sv['L'], sv['hh'], sv['ce_q'])
+        else:
+            K.embedding_bwd(sv['ids32'], dx, self.P.g('input_layer.0.weight'), T, d)

@@ -21,7 +21,8 @@ def _dev(*ts):
 
 def gemm(A, B, C, M, N_, K, *, a_t=False, b_t=False, lda=None, ldb=None, ldc=None, epi=N.EPI_BF16, bias=None,
          resid=None, ldr=0, aux=None, ldaux=0, alpha=1.0, splits=1, drop_p=0.0, seed=0, rot=None, rot_cols=0,
-         rot_d=0, rot_seq=0, labels=None, label_logit=None, batch=1, sA=0, sB=0, sC=0, a_rowsum=None):
+         rot_d=0, rot_seq=0, labels=None, label_logit=None, batch=1, sA=0, sB=0, sC=0, a_rowsum=None, k_weight=None,
+         row_a=None, row_b=None, gather=None, ldg=0):
     """C = epi(alpha * A . B) with A [M,K] (a_t: stored [K,M]) and B [K,N] (b_t: stored [K,N], else [N,K])."""
     _dev(A, B, C)
     assert A.dtype == bf16 and B.dtype == bf16
@@ -50,6 +51,9 @@ def gemm(A, B, C, M, N_, K, *, a_t=False, b_t=False, lda=None, ldb=None, ldc=Non
     d.labels = ptr(labels)
     d.label_logit = ptr(label_logit)
     d.a_rowsum = ptr(a_rowsum)
+    d.k_weight = ptr(k_weight)
+    d.row_a, d.row_b = ptr(row_a), ptr(row_b)
+    d.gather, d.ldg = ptr(gather), ldg
     check(lib.svae_gemm(ctypes.byref(d), stream()), 'svae_gemm')
 
 
@@ -213,6 +217,34 @@ def ce_chunking(B, L, V, chunk_numel=2 ** 30):
     chunks = -(-(B * (L - 1) * V) // chunk_numel)
     chunk_len = -(-(L - 1) // chunks)
     return -(-(L - 1) // chunk_len), chunk_len
+
+
+def ce_label_logit(hh, W, bias, labels, rows, D, out):
+    _dev(hh, W, labels, out)
+    check(lib.svae_ce_label_logit(hh.data_ptr(), hh.stride(0), W.data_ptr(), W.stride(0), ptr(bias), labels.data_ptr(),
+                                  rows, D, out.data_ptr(), stream()), 'svae_ce_label_logit')
+
+
+def ce_prob_finalize(part, ntile, row_off, labels, rows, seq, nchunks, chunk_len, lse, row_loss, chunk_w, nll):
+    assert chunk_w.numel() >= nchunks and chunk_w.dtype == f32
+    red = ce_red_ws(part.device, nchunks)
+    check(lib.svae_ce_prob_finalize(part.data_ptr(), ntile, row_off.data_ptr(), labels.data_ptr(), rows, seq, nchunks,
+                                    chunk_len, lse.data_ptr(), row_loss.data_ptr(), chunk_w.data_ptr(),
+                                    nll.data_ptr(), red.data_ptr(), stream()), 'svae_ce_prob_finalize')
+
+
+def ce_prob_bwd_prep(hh, lse, row_off, chunk_w, labels, gscale, rows, seq, nchunks, chunk_len, D, hh_out, r_out,
+                     q_out, dbias=None):
+    _dev(hh, lse, row_off, chunk_w, labels, gscale, hh_out, r_out, q_out)
+    check(lib.svae_ce_prob_bwd_prep(hh.data_ptr(), hh.stride(0), lse.data_ptr(), row_off.data_ptr(),
+                                    chunk_w.data_ptr(), labels.data_ptr(), gscale.data_ptr(), rows, seq, nchunks,
+                                    chunk_len, D, hh_out.data_ptr(), r_out.data_ptr(), q_out.data_ptr(), ptr(dbias),
+                                    stream()), 'svae_ce_prob_bwd_prep')
+
+
+def embedding_bwd_ce(ids, dout, dtable, rows, D, seq, hh, q):
+    check(lib.svae_embedding_bwd_ce(ids.data_ptr(), dout.data_ptr(), dtable.data_ptr(), rows, D, seq, hh.data_ptr(),
+                                    q.data_ptr(), stream()), 'svae_embedding_bwd_ce')
 
 
 def mutual_info(stats, kl, B, Z, seed, out, ws, eps=None, S=10):

@@ -95,3 +95,100 @@ def test_chunked_grad_matches_autograd(nchunks):
     assert dl[:, L - 1].abs().max().item() == 0.0               # the label-0 row carries no gradient
     assert _rel(dl[:, :L - 1], ref.grad) < 1e-2
     assert _rel(db, ref.grad.sum((0, 1))) < 1e-2
+
+
+def _prob_head(hh, W, bias, lab, T, L, V, d, nchunks, chunk_len, g=0.75):
+    """The engine's P-head (svae.h): forward (label logits, CE_PROB GEMM, finalize) and backward (prep, dW GEMM
+    with weighted row sums, ROWSCALE_GATHER dX GEMM, one-hot part through the fused embedding backward with
+    zero upstream gradient). Returns nll, row_loss and the gradients (dhh bf16, dW f32, dbias f32)."""
+    ntile = V // 128
+    coff = torch.empty(T, device=dev)
+    K.ce_label_logit(hh, W, bias, lab, T, d, coff)
+    Pm = torch.empty(T, V, dtype=torch.bfloat16, device=dev)
+    part = torch.empty(T, ntile, device=dev)
+    K.gemm(hh, W, Pm, T, V, d, epi=N.EPI_CE_PROB, bias=bias, aux=part, labels=lab, row_a=coff)
+    lse, rl, cw, nll = (torch.empty(T, device=dev), torch.empty(T, device=dev), torch.empty(nchunks, device=dev),
+                        torch.empty(1, device=dev))
+    K.ce_prob_finalize(part, ntile, coff, lab, T, L, nchunks, chunk_len, lse, rl, cw, nll)
+    gs = torch.full((1,), g, device=dev)
+    hh_r = torch.empty(T, d, dtype=torch.bfloat16, device=dev)
+    r, q = torch.empty(T, device=dev), torch.empty(T, device=dev)
+    dbias, dW = torch.zeros(V, device=dev), torch.zeros(V, d, device=dev)
+    K.ce_prob_bwd_prep(hh, lse, coff, cw, lab, gs, T, L, nchunks, chunk_len, d, hh_r, r, q, dbias)
+    K.gemm(Pm, hh_r, dW, V, d, T, a_t=True, b_t=True, lda=V, ldb=d, ldc=d, epi=N.EPI_F32_ACC, a_rowsum=dbias,
+           k_weight=r)
+    dhh = torch.empty(T, d, dtype=torch.bfloat16, device=dev)
+    K.gemm(Pm, W.t().contiguous(), dhh, T, d, V, epi=N.EPI_ROWSCALE_GATHER, labels=lab, row_a=r, row_b=q, gather=W,
+           ldg=d)
+    B = T // L
+    ids = torch.zeros(B, L, dtype=torch.int32, device=dev)
+    ids[:, 0] = 1
+    ids[:, 1:] = lab.view(B, L)[:, :L - 1]
+    K.embedding_bwd_ce(ids.view(T), torch.zeros(T, d, device=dev), dW, T, d, L, hh, q)
+    return nll, rl, dhh, dW, dbias
+
+
+def _torch_ref(hh, W, bias, lab, B, L, V, chunk_len, g=0.75):
+    hr = hh.float().requires_grad_()
+    Wr = W.float().requires_grad_()
+    br = bias.clone().requires_grad_()
+    logits = (hr @ Wr.t() + br).view(B, L, V)[:, :L - 1]
+    y = lab.view(B, L)[:, :L - 1].long()
+    loss = torch.stack([F.cross_entropy(lc.flatten(end_dim=1), yc.flatten(), ignore_index=0)
+                        for lc, yc in zip(logits.split(chunk_len, dim=1), y.split(chunk_len, dim=1))]).mean()
+    (loss * g).backward()
+    return loss, hr.grad, Wr.grad, br.grad
+
+
+def test_prob_head_chunked_matches_reference():
+    """The P-head training path on the reference's chunked fixture: nll and val_bpb's weighted nll against the
+    reference's values (1e-5), gradients against torch fp32 autograd (1e-2 rel)."""
+    g, t, labels = setup_ce()
+    B, L1 = t['a'].shape
+    L, V, d = L1 + 1, t['w'].numel(), 512
+    T = B * L
+    hh = torch.zeros(B, L, d, device=dev)
+    hh[:, :L1, 0], hh[:, :L1, 1] = t['a'].to(dev), t['u'].to(dev)
+    hh = hh.view(T, d).bfloat16()
+    W = torch.zeros(V, d, device=dev)
+    W[:, 0], W[:, 1] = t['w'].to(dev), t['s'].to(dev)
+    W = W.bfloat16()
+    lab = torch.zeros(B, L, dtype=torch.int32, device=dev)
+    lab[:, :L1] = labels.to(dev)
+    lab = lab.view(T)
+    bias = torch.zeros(V, device=dev)
+    nchunks, chunk_len = K.ce_chunking(B, L, V)
+    nll, rl, dhh, dW, dbias = _prob_head(hh, W, bias, lab, T, L, V, d, nchunks, chunk_len)
+    assert abs(nll.item() - float(g['nll'])) / float(g['nll']) < 1e-5, (nll.item(), float(g['nll']))
+    wn = torch.empty(1, device=dev)
+    K.ce_weighted_nll(rl, lab, t['tok_w'].to(dev), T, L, nchunks, chunk_len, wn)
+    assert abs(wn.item() - float(g['wnll'])) / float(g['wnll']) < 1e-5, (wn.item(), float(g['wnll']))
+    loss, gh, gW, gb = _torch_ref(hh, W, bias, lab, B, L, V, chunk_len)
+    assert abs(loss.item() - float(g['nll'])) / float(g['nll']) < 1e-5
+    assert _rel(dhh[:, :2], gh[:, :2]) < 1e-2 and dhh[:, 2:].abs().max().item() == 0.0
+    assert _rel(dW[:, :2], gW[:, :2]) < 1e-2
+    assert _rel(dbias, gb) < 1e-2
+
+
+@pytest.mark.parametrize('nchunks', [1, 3])
+def test_prob_head_random_matches_autograd(nchunks):
+    """P-head on unstructured operands (random hh, W, bias; padded rows; d = 256): nll 1e-5, dhh / dW / dbias
+    1e-2 rel against torch fp32 autograd, with 1 and 3 sequence chunks."""
+    torch.manual_seed(11 + nchunks)
+    B, L, V, d = 8, 512, 32768, 256
+    T = B * L
+    hh = torch.randn(T, d, device=dev).bfloat16()
+    W = (0.1 * torch.randn(V, d, device=dev)).bfloat16()
+    bias = 0.5 * torch.randn(V, device=dev)
+    lab = torch.randint(3, V, (B, L), dtype=torch.int32, device=dev)
+    lab[:, -1] = 0
+    lab[2, 300:] = 0                          # padded sequences
+    lab[5, 100:] = 0
+    lab = lab.view(T)
+    chunk_len = -(-(L - 1) // nchunks)
+    nll, rl, dhh, dW, dbias = _prob_head(hh, W, bias, lab, T, L, V, d, nchunks, chunk_len)
+    loss, gh, gW, gb = _torch_ref(hh, W, bias, lab, B, L, V, chunk_len)
+    assert abs(nll.item() - loss.item()) / loss.item() < 1e-5, (nll.item(), loss.item())
+    assert _rel(dhh, gh) < 1e-2
+    assert _rel(dW, gW) < 1e-2
+    assert _rel(dbias, gb) < 1e-2
