@@ -785,29 +785,30 @@ __device__ __forceinline__ void g3_reg_epilogue(const GP& p, const f32x4 (&acc)[
         const float off = sstat[1024 + rl] * G3_LOG2E;
         const bool live = slabel[rl] != 0;
         const bool ragged = n0 + wc * 64 + 64 > p.N;   // wave-uniform
+        float se = 0.f;
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int jp = 0; jp < 2; ++jp) {   // P [T, V] bf16 (2 GiB at C2): nontemporal stores
+          f32x4 x2[2];
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            float x = __builtin_amdgcn_exp2f(fminf(fmaf(v[j][e], G3_LOG2E, -off), 127.0f));
-            if (ragged && n0 + wc * 64 + j * 16 + 4 * g + e >= p.N) x = 0.f;
-            v[j][e] = live ? x : 0.f;
-          }
+          for (int h = 0; h < 2; ++h)
 #pragma unroll
-        for (int jp = 0; jp < 2; ++jp)   // P [T, V] bf16 (2 GiB at C2): nontemporal
-          store_pair_bf16<true>(crow, 32 * jp, row_ok ? nleft : 0, v[2 * jp], v[2 * jp + 1], g);
+            for (int e = 0; e < 4; ++e) {
+              const int j = 2 * jp + h;
+              float x = __builtin_amdgcn_exp2f(fminf(fmaf(v[j][e], G3_LOG2E, -off), 127.0f));
+              if (ragged && n0 + wc * 64 + j * 16 + 4 * g + e >= p.N) x = 0.f;
+              x = live ? x : 0.f;
+              x2[h][e] = x;
+              se += x;
+            }
+          store_pair_bf16<true>(crow, 32 * jp, row_ok ? nleft : 0, x2[0], x2[1], g);
+        }
+        se = sum_x16_x32(se);
+        if (g == 0) sstat[rl * 4 + wc] = se;
       } else if (EPI != SVAE_EPI_CE_STATS || p.C) {   // CE statistics with C == nullptr: no logits stored
 #pragma unroll
         for (int jp = 0; jp < 2; ++jp)   // vocab logits (2 GiB at C2): nontemporal, 1444 -> 1322 us
           store_pair_bf16<EPI == SVAE_EPI_CE_STATS>(crow, 32 * jp, row_ok ? nleft : 0, v[2 * jp], v[2 * jp + 1], g);
       }
-    }
-    if constexpr (EPI == SVAE_EPI_CE_PROB) {
-      float se = 0.f;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) se += (v[j][0] + v[j][1]) + (v[j][2] + v[j][3]);
-      se = sum_x16_x32(se);
-      if (g == 0) sstat[rl * 4 + wc] = se;
     }
     if constexpr (EPI == SVAE_EPI_CE_STATS) {
       const bool ragged = n0 + wc * 64 + 64 > p.N;   // wave-uniform
@@ -1083,8 +1084,21 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GP p) {
     else xb = g3_src_k(p.ldb, X.n0, p.N, wave, lane);
   };
   srcs(T, sa, sb);
+  // ACC_KW: wave 0 also DMAs the K-tile's 64 k_weight floats into the side ring (sstat, [2][64]) with the tile, so
+  // the weighted row sums read them from LDS behind the same counted wait + barrier (no scalar loads in the loop)
+  auto issue_kw = [&](const G3Tile& X, int k0, int parity) {
+    if constexpr (EPI == G3_EPI_ACC_KW) {
+      if (wave == 0 && p.a_rowsum && X.bn < 2) {
+        const u32x4 rs = buffer_rsrc(p.k_weight + k0, 0x7FFFFFF0u);
+        dma4_lds(rs, sstat + parity * 64, k0 + lane < X.kend ? lane * 4 : 0x7FFFFFF0);
+      }
+    }
+  };
   int g = 0;   // K-tiles consumed so far by this block: the stage of K-tile g is g & 1
-  if (T.nk > 0) g3_issue<AT, BT>(p, T.A, T.B, sa, sb, T.m0, T.n0, T.kbeg, T.kend, smem, wave);
+  if (T.nk > 0) {
+    g3_issue<AT, BT>(p, T.A, T.B, sa, sb, T.m0, T.n0, T.kbeg, T.kend, smem, wave);
+    issue_kw(T, T.kbeg, 0);
+  }
   if (p.desync > 0 && (bid & 1)) {   // stagger the epilogues of neighbouring blocks (HBM write bursts)
     for (int i = 0; i < p.desync; ++i) __builtin_amdgcn_s_sleep(127);
   }
@@ -1112,20 +1126,48 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GP p) {
       const char* la = smem + (g & 1) * G3_STAGE;
       const char* lb = la + G3_T;
       char* nxt = smem + ((g + 1) & 1) * G3_STAGE;
-      if (kt + 1 < T.nk)
+      if (kt + 1 < T.nk) {
         g3_issue<AT, BT>(p, T.A, T.B, sa, sb, T.m0, T.n0, T.kbeg + (kt + 1) * 64, T.kend, nxt, wave);
-      else if (has_next) {   // the next tile's first K-tile, in flight during this tile's epilogue
+        issue_kw(T, T.kbeg + (kt + 1) * 64, (g + 1) & 1);
+      } else if (has_next) {   // the next tile's first K-tile, in flight during this tile's epilogue
         const G3Tile TN = g3_tile(p, t3n);
         if (TN.nk > 0) {
           G3Src xa, xb;
           srcs(TN, xa, xb);
           g3_issue<AT, BT>(p, TN.A, TN.B, xa, xb, TN.m0, TN.n0, TN.kbeg, TN.kend, nxt, wave);
+          issue_kw(TN, TN.kbeg, (g + 1) & 1);
         }
       }
       // Quadrant walk (mh, nh) = (0,0) (0,1) (1,1) (1,0): A fragments of a half reused by two quadrants, B
       // fragments of a half by the turn. The next quadrant's fragment reads are issued ahead of the current
       // quadrant's MFMAs.
       bf16x8 a0[4][2], a1[4][2], b0[2][2], b1[2][2];
+      // AT: sum_k A[m][k] (* k_weight[k]) from the A fragments already in registers (no extra LDS reads): lane l of
+      // a fragment holds row 16i + (l & 15), k = 32 ks + 8 (l >> 4) + (0..7); column wave wc takes row groups
+      // 2 wc, 2 wc + 1 of its wave row's eight (balanced over the SIMDs; a0's right after their last MFMA use),
+      // summed over the lane groups at the end of the tile. ACC_KW: the K-tile's 64 weights arrived with its DMA
+      // into the side ring, stage g & 1. The first two column tiles (blocks bn = 0, 1 hold the same A rows) split
+      // the work by k-step, so neither runs much longer than the blocks without row sums.
+      const bool do_rs = AT && p.a_rowsum && T.bn < 2;
+      const int ks0 = p.tn2 >= 2 ? T.bn : 0, ks1 = p.tn2 >= 2 ? T.bn + 1 : 2;
+      auto rowsum2 = [&](const bf16x8 (&x)[2], const bf16x8 (&y)[2]) {
+        const float* kws = sstat + (g & 1) * 64 + 8 * (lane >> 4);
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          if (ks < ks0 || ks >= ks1) continue;   // (block-uniform)
+          f32x4 k0 = {1.f, 1.f, 1.f, 1.f}, k1 = k0;
+          if constexpr (EPI == G3_EPI_ACC_KW) {
+            k0 = *(const f32x4*)(kws + 32 * ks);
+            k1 = *(const f32x4*)(kws + 32 * ks + 4);
+          }
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float kwe = e < 4 ? k0[e] : k1[e - 4];
+            rsum[0] = fmaf((float)x[ks][e], kwe, rsum[0]);
+            rsum[1] = fmaf((float)y[ks][e], kwe, rsum[1]);
+          }
+        }
+      };
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -1161,6 +1203,10 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GP p) {
           for (int j = 0; j < 2; ++j) acc[i][2 + j] = mfma16(b1[j][ks], a0[i][ks], acc[i][2 + j]);
       if constexpr (AT) {
         G3_PRIO_LO();
+        if (do_rs) {
+          if (wc == 0) rowsum2(a0[0], a0[1]);
+          else if (wc == 1) rowsum2(a0[2], a0[3]);
+        }
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -1181,18 +1227,9 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GP p) {
           for (int j = 0; j < 2; ++j) acc[4 + i][j] = mfma16(b0[j][ks], a1[i][ks], acc[4 + i][j]);
       G3_PRIO_LO();
       if constexpr (AT) {
-        if (p.a_rowsum && T.bn == 0) {   // sum_k A[k][m] (* k_weight[k]): thread = 4 m (one 8-B unit) x 8 k-rows
-          const int u = tid & 63, kg = wave;   // (wave-uniform: the k_weight loads are scalar)
-          const char* lh = la + (u >> 5) * (G3_T / 2);
-          const int kb = T.kbeg + kt * 64 + kg * 8;
-#pragma unroll
-          for (int r = 0; r < 8; ++r) {
-            const bf16x4 v = __builtin_bit_cast(bf16x4, *(const short4v*)(lh + mn_off(kg * 8 + r, u & 31)));
-            float kw = 1.f;
-            if constexpr (EPI == G3_EPI_ACC_KW) kw = kb + r < T.kend ? p.k_weight[kb + r] : 0.f;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) rsum[e] += (float)v[e] * kw;
-          }
+        if (do_rs) {
+          if (wc == 2) rowsum2(a1[0], a1[1]);
+          else if (wc == 3) rowsum2(a1[2], a1[3]);
         }
       }
     }
@@ -1211,11 +1248,13 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GP p) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if constexpr (AT) {
-      if (p.a_rowsum && T.bn == 0) {
-        const int m = T.m0 + (tid & 63) * 4;
+      if (p.a_rowsum && T.bn < 2) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
-          if (m + e < p.M) atomicAdd(p.a_rowsum + m + e, rsum[e]);
+        for (int h = 0; h < 2; ++h) {
+          const float t = sum_x16_x32(rsum[h]);
+          const int m = T.m0 + wr * 128 + (2 * wc + h) * 16 + (lane & 15);
+          if ((lane >> 4) == 0 && m < p.M) atomicAdd(p.a_rowsum + m, t);
+        }
       }
     }
     if constexpr (EPI == SVAE_EPI_BF16 || EPI == SVAE_EPI_GELU || EPI == SVAE_EPI_CE_STATS ||
@@ -1239,8 +1278,10 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GP p) {
     t3 = t3n;
     T = g3_tile(p, t3);
     srcs(T, sa, sb);
-    if (!prefetched && T.nk > 0)   // (an empty split-K slice prefetched nothing)
+    if (!prefetched && T.nk > 0) {   // (an empty split-K slice prefetched nothing)
       g3_issue<AT, BT>(p, T.A, T.B, sa, sb, T.m0, T.n0, T.kbeg, T.kend, smem + (g & 1) * G3_STAGE, wave);
+      issue_kw(T, T.kbeg, g & 1);
+    }
   }
 }
 
