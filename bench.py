@@ -115,7 +115,9 @@ def cpu_baseline(cfg):
         return time.time() - t0
 
     run(2)
-    B = cfg['B']
+    # the config's own batch at seq 512 (C2: 64 x 512); longer sequences (C4/C5, ~10x the CPU work per sequence)
+    # a batch of B/8 sequences, so the sample stays at 10-30 s of CPU time
+    B = cfg['B'] if cfg['L'] <= 512 else max(1, cfg['B'] // 8)
     dt = run(B)
     return {'value': round(B * L / dt, 1), 'unit': 'tokens/s', 'cores': threads, 'kind': 'port',
             'sample': f'oracle/ (torch fp32 CPU restatement, golden-pinned) fwd+bwd of the {cfg["layers"]}L '
@@ -123,14 +125,18 @@ def cpu_baseline(cfg):
                       f'{threads} threads (affinity mask capped by the cgroup CPU quota)'}
 
 
-def parity_check(device):
-    """GPU engine vs CPU oracle on the C2 model at batch 2 (same portable weights and noise)."""
+def parity_check(cfg, device):
+    """GPU engine vs CPU oracle on the bench config's own model (layers, d_model, heads, seq) at batch 2 (batch 1
+    from seq 2048 on, to bound the CPU time), same portable weights and injected noise, dropout off; plus the
+    fp32-kernel-mode argmax reconstructions at z = mu against the oracle's."""
     import oracle
     from oracle.params import portable_ids, portable_normal
     from sparse_vae.engine import FlatParams, VAEEngine
-    hp = oracle.HParams(d_model=512, num_heads=8, num_layers=6, kl_weight=0.7)
+    d, L = cfg['d'], cfg['L']
+    hp = oracle.HParams(d_model=d, num_heads=cfg['heads'], num_layers=cfg['layers'], kl_weight=0.7,
+                        attn_window=cfg.get('window', 0))
     params = oracle.init_params(hp, 3)
-    B, L = 2, 512
+    B = 2 if L < 2048 else 1
     ids = torch.from_numpy(portable_ids((B, L), 5))
     ntok = torch.full((B,), L, dtype=torch.int64)
     eps = torch.from_numpy(portable_normal(B * 64, 'eps', 3).reshape(B, 1, 64).astype('float32'))
@@ -145,14 +151,14 @@ def parity_check(device):
     elbo, elbo_ref = -(nll + kl), -(ref['nll'].item() + ref['kl'].item())
     # argmax reconstructions at z = mu: fp32 kernel mode vs the CPU fp32 path
     from sparse_vae import kernels as K
-    x = torch.empty(B * L, 512, device=device)
-    K.embedding_fwd(ids.to(torch.int32).to(device), flat.f('input_layer.0.weight'), x, B * L, 512)
+    x = torch.empty(B * L, d, device=device)
+    K.embedding_fwd(ids.to(torch.int32).to(device), flat.f('input_layer.0.weight'), x, B * L, d)
     mu = out['mu'].clone()
-    am_gpu = eng.reconstruct_f32(x.view(B, L, 512), mu)[:, :-1].argmax(-1).cpu()
+    am_gpu = eng.reconstruct_f32(x.view(B, L, d), mu)[:, :-1].argmax(-1).cpu()
     with torch.no_grad():
         xr = torch.nn.functional.embedding(ids, params['input_layer.0.weight'])
         am_ref = oracle.reconstruct(params, xr, mu.cpu().view(B, 1, 64), ids.eq(0), hp)[:, :-1].argmax(-1)
-    return {'config': 'C2 model (6L d512 L512) batch 2, dropout off, injected eps',
+    return {'config': f'{cfg["layers"]}L d{d} heads {cfg["heads"]} seq {L} at batch {B}, dropout off, injected eps',
             'loss_gpu': loss, 'loss_cpu_ref': ref['loss'].item(),
             'loss_rel_err': abs(loss - ref['loss'].item()) / abs(ref['loss'].item()),
             'elbo_rel_err': abs(elbo - elbo_ref) / abs(elbo_ref), 'tolerance': 1e-3,
@@ -245,7 +251,7 @@ def main():
         }
         if world == 1 and not args.no_parity:
             try:
-                res['parity'] = parity_check(device)
+                res['parity'] = parity_check(cfg, device)
             except Exception as e:  # parity is reported, never allowed to kill the throughput line
                 res['parity'] = {'error': repr(e)}
         if world == 1 and not args.no_cpu_baseline:

@@ -1,0 +1,61 @@
+"""Per-GEMM census of the C2 training step: every libsvae GEMM launch of a few bench steps timed with HIP events
+on its stream, grouped by (M, N, K, layout, epilogue, splits).
+
+    python scripts/gemm_census.py [steps] > profiles/<round>_c2_gemm_census.txt
+"""
+import os
+import sys
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, 'sparse-vae_amd'))
+import torch  # noqa: E402
+import bench  # noqa: E402
+from sparse_vae import kernels as K  # noqa: E402
+
+EPI = ['bf16', 'f32', 'f32_acc', 'f32_atomic', 'gelu', 'gelu_bwd', 'drop_resid', 'rotary', 'ce_stats', 'ce_prob',
+       'rowscale_gather']
+
+
+def main():
+    steps = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+    dev = torch.device('cuda', 0)
+    torch.cuda.set_device(0)
+    model, opt, sched, batch = bench.build(bench.CONFIGS['c2'], dev)
+    for _ in range(3):
+        bench.step(model, opt, sched, batch)
+    torch.cuda.synchronize()
+    rec = []
+    orig = K.gemm
+
+    def timed(A, B, C, M, N_, K_, **kw):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        orig(A, B, C, M, N_, K_, **kw)
+        e1.record()
+        key = (M, N_, K_, int(kw.get('a_t', False)), int(kw.get('b_t', False)), kw.get('epi', 0), kw.get('splits', 1),
+               int(kw.get('a_rowsum') is not None), int(kw.get('k_weight') is not None))
+        rec.append((key, e0, e1))
+
+    K.gemm = timed
+    for _ in range(steps):
+        bench.step(model, opt, sched, batch)
+    torch.cuda.synchronize()
+    K.gemm = orig
+    agg = defaultdict(lambda: [0, 0.0])
+    for key, e0, e1 in rec:
+        agg[key][0] += 1
+        agg[key][1] += e0.elapsed_time(e1) * 1e3
+    total = sum(v[1] for v in agg.values()) / steps
+    print(f'GEMM time {total / 1e3:.3f} ms/step (HIP events around each launch, {steps} steps, C2 bench step)')
+    for key, (n, us) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
+        M, N_, K_, at, bt, epi, sp, rs, kwt = key
+        per = us / n
+        print(f'{us / steps / 1e3:7.3f} ms  x{n // steps:2d} {per:9.1f} us {2.0 * M * N_ * K_ / per / 1e6:8.1f} TF/s  '
+              f'M={M} N={N_} K={K_} a_t={at} b_t={bt} epi={EPI[epi] if epi < len(EPI) else epi} splits={sp} '
+              f'rowsum={rs} k_weight={kwt}')
+
+
+if __name__ == '__main__':
+    main()

@@ -5,14 +5,16 @@
 // Layout: q/k/v/o are token-major rows of H*hd bf16 (the nn.Linear output layout, heads interleaved),
 // so no head-split copies exist. Head dim is padded to HDP = 64 or 128 inside the kernel.
 //
-// Forward: one block = 64 queries of one (batch, head), 4 waves x 16 queries. "Swapped" products keep the
-// query on the MFMA lane: S^T = K . Q^T (K tile ds_read_b128, Q fragment in registers), then
+// Forward: one block = 128 queries of one (batch, head), 4 waves x 32 queries. "Swapped" products keep the
+// query on the MFMA lane: S^T = K . Q^T (K tile ds_read_b128, Q fragments in registers), then
 // O^T += V^T . P^T where P^T is the S^T accumulator converted in place (key order permuted to match the
-// ds_read_b64_tr_b16 reads of V). Online softmax per lane, no P round trip through LDS.
+// ds_read_b64_tr_b16 reads of V). Online softmax per lane, no P round trip through LDS. K/V tiles of 64 keys by
+// LDS-DMA one tile ahead.
 //
-// Backward: one block = 64 keys, 4 waves x 16 keys, sweeping query tiles (key on the lane: S = Q K^T and
+// Backward: one block = 128 keys, 4 waves x 32 keys, sweeping 64-query tiles (key on the lane: S = Q K^T and
 // dP = dO V^T accumulators are already the B operands of dV^T += dO^T P and dK^T += Q^T dS). dS^T goes
-// through LDS once for dQ = dS K, which is summed across key blocks with f32 atomics.
+// through LDS once for dQ = dS K: each key block stores its f32 partial dQ into its own slice of dq_part (no
+// atomics) and attn_dq_reduce_kernel sums the slices in a fixed order (deterministic).
 #include "common.h"
 #include "../../include/svae.h"
 
