@@ -172,8 +172,10 @@ __device__ unsigned long long svae_attn_stamps[1024][6];
 #define ATTN_NS 2   // (3 stages with the XCD order: 70.7 vs 67.5 us)
 #endif
 
+
+// One 128-query tile of one (batch, head). smem: the K/V ring + key-padding ring of the kernel.
 template <int HDP>
-__global__ __launch_bounds__(256, HDP == 64 ? 3 : 2) void attn_fwd_kernel(AP p) {
+__device__ __forceinline__ void attn_fwd_tile(const AP& p, char* smem, int bx, int h, int b) {
   using T = Tile<HDP>;
   constexpr int NKK = HDP / 32, NT = HDP / 16;
   // K/V ring: NS stages of (K, V) tiles filled NS - 1 key tiles ahead; the key-padding bytes ride along in an
@@ -181,10 +183,7 @@ __global__ __launch_bounds__(256, HDP == 64 ? 3 : 2) void attn_fwd_kernel(AP p) 
   // 3 or 4 stages at 2 blocks / CU (73.5 vs 78.4 / 92 us): blocks in flight, not prefetch depth, set the time.
   constexpr int NS = ATTN_NS;
   constexpr int DMA_OPS = 2 * (64 * T::PITCH / 1024) / 4;   // buffer_load_lds per wave per (K, V) tile
-  __shared__ __attribute__((aligned(16))) char smem[NS * 2 * T::BYTES + NS * 64 * 4];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, li = lane & 15;
-  int bx, h, b;
-  xcd_block(bx, h, b);
   const int q0 = bx * 128;
 #ifdef SVAE_STAMPS
   const int lin_id = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
@@ -367,6 +366,17 @@ __global__ __launch_bounds__(256, HDP == 64 ? 3 : 2) void attn_fwd_kernel(AP p) 
 #endif
 }
 
+// One query tile per workgroup. (Running query tiles x and nqt - 1 - x in one workgroup, to even out the causal
+// work, measured 68 -> 73 us at the C2 shape on two boxes out of three, scripts/attn_probe.py: half the workgroups
+// in flight cost more than the imbalance.)
+template <int HDP>
+__global__ __launch_bounds__(256, HDP == 64 ? 3 : 2) void attn_fwd_kernel(AP p) {
+  __shared__ __attribute__((aligned(16))) char smem[ATTN_NS * 2 * Tile<HDP>::BYTES + ATTN_NS * 64 * 4];
+  int bx, h, b;
+  xcd_block(bx, h, b);
+  attn_fwd_tile<HDP>(p, smem, bx, h, b);
+}
+
 // ===================================================================================== backward
 // delta[b][h][q] = sum_d dO . O   (LPR = hd / 8 lanes per (q, h) row: 8 for hd <= 64, 16 for hd <= 128, so no
 // lane idles)
@@ -410,19 +420,16 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(AP p) {
 constexpr int BWD_KEYS = 128;
 
 template <int HDP>
-__global__ __launch_bounds__(256, HDP == 64 ? 2 : 1) void attn_bwd_kernel(AP p) {
+__device__ __forceinline__ void attn_bwd_tile(const AP& p, char* smem, int kb, int h, int b) {
   using T = Tile<HDP>;          // [rows][HDP] bf16
   using TS = Tile<64>;          // dS^T [128 keys][64 queries]
   constexpr int NKK = HDP / 32, NT = HDP / 16;
-  __shared__ __attribute__((aligned(16))) char smem[6 * T::BYTES + 2 * TS::BYTES + 4 * 64 * 4];
   char* QO = smem;                                  // [buf][Q, dO] tiles
   char* Ks = smem + 4 * T::BYTES;                   // 128 key rows
   char* dSs = smem + 6 * T::BYTES;                  // 128 key rows x 64 queries
   float* cst = (float*)(smem + 6 * T::BYTES + 2 * TS::BYTES);   // [buf][lse, delta][64] (DMA'd with the tile)
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, li = lane & 15;
-  int kb, h, b;
-  xcd_block(kb, h, b);
   const int k0 = kb * BWD_KEYS;
   const bf16* Q = p.q + b * p.bq + (long long)h * p.hd;
   const bf16* K = p.k + b * p.bk + (long long)h * p.hd;
@@ -629,6 +636,17 @@ __global__ __launch_bounds__(256, HDP == 64 ? 2 : 1) void attn_bwd_kernel(AP p) 
       *(bf16x4*)(DV + d) = (bf16x4){f2bf(dv[j][u][0]), f2bf(dv[j][u][1]), f2bf(dv[j][u][2]), f2bf(dv[j][u][3])};
     }
   }
+}
+
+// One key block per workgroup. (Pairing key blocks x and nkb - 1 - x per workgroup, to even out the causal
+// sweeps, measured slower: 219 -> 247 us at the C2 shape, 629 -> 771 us at L = 1024 -- half the workgroups and
+// two serial prologues per workgroup cost more than the imbalance.)
+template <int HDP>
+__global__ __launch_bounds__(256, HDP == 64 ? 2 : 1) void attn_bwd_kernel(AP p) {
+  __shared__ __attribute__((aligned(16))) char smem[6 * Tile<HDP>::BYTES + 2 * Tile<64>::BYTES + 4 * 64 * 4];
+  int kb, h, b;
+  xcd_block(kb, h, b);
+  attn_bwd_tile<HDP>(p, smem, kb, h, b);
 }
 
 // dQ = scale * sum over the key blocks that can see the query (causal: kb <= q / 128) of the partials;
