@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 OUT=gpurun_out/${1:-run}
 ST=${2:-tbpm}
 mkdir -p "$OUT"
-HEAD_RE="gemm256_kernel<false, false, (8|9)>"
+HEAD_RE="gemm256_kernel<false, false, 9>"
 PB="python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-parity"
 run() { echo "== $*" >&2; "$@"; }
 rc=0
@@ -30,6 +30,7 @@ fi
 if [[ $ST == *m* && $rc == 0 ]]; then
   timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$HEAD_RE" -f csv -d "$OUT/pmc_write" -o run -- $PB > "$OUT/pmc_write.log" 2>&1; rc=$?
 fi
+timeout -k 10 120 python3 -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1; tail -1 "$OUT/smoke.log"
 find "$OUT" -type f -size +8M -print -delete
 echo "gpu_round rc=$rc"
 exit $rc
