@@ -47,7 +47,7 @@ enum svae_epi {
                                  aux f32 [M][ceil(N/128)][2]; label logit (f32) to resid-as-out [M]   */
   SVAE_EPI_CE_PROB = 9,       /* vocab head, training: C bf16 = exp(acc + bias - row_a[m]) for rows with
                                  labels[m] != 0, else 0 (exponent clamped at 2^127); aux f32
-                                 [M][ceil(N/128)] = per (row, 128-col tile) sums of those values       */
+                                 [ceil(N/128)][M] (tile-major) = per (128-col tile, row) sums of them  */
   SVAE_EPI_ROWSCALE_GATHER = 10 /* C bf16 = alpha * row_a[m] * acc - row_b[m] * gather[labels[m]][n]
                                  (the gather term is skipped where labels[m] == 0)                    */
 };
@@ -197,7 +197,7 @@ int svae_ce_grad(void* logits, int64_t ld, const float* lse, const float* chunk_
  *   dW = P^T (r . hh) (+ the one-hot part, svae_embedding_bwd_ce); d bias = sum_t r_t P[t] (k_weight row sums
  *   of the dW GEMM) - q scattered to the labels (bwd_prep).
  * ce_label_logit: out[r] = hh[r] . W[labels[r]] + bias[labels[r]] (f32 dot of bf16 rows; 0 where labels[r] = 0).
- * ce_prob_finalize: part f32 [rows][ntile] (the per-tile sums of P) -> lse = c + log sum, row_loss = lse - c,
+ * ce_prob_finalize: part f32 [ntile][rows] (the per-tile sums of P) -> lse = c + log sum, row_loss = lse - c,
  *   chunk_w, nll_out: the chunked mean of means of svae_ce_finalize.
  * ce_prob_bwd_prep: r_out, q_out [rows]; hh_out bf16 [rows][D] = r * hh; dbias[label] -= q (atomics; may be NULL).
  * Exact while every labelled row's logits stay below its label logit + 88 (a token loss < 88 nats): beyond, the

@@ -39,7 +39,7 @@ def main():
     labels = torch.randint(3, V, (T,), dtype=torch.int32, device=dev)
     out = torch.empty(T, V, dtype=bf16, device=dev)
     part2 = torch.empty(T, V // 128, 2, device=dev)
-    part1 = torch.empty(T, V // 128, device=dev)
+    part1 = torch.empty(V // 128, T, device=dev)
     ll = torch.empty(T, device=dev)
     coff = torch.empty(T, device=dev)
     K.ce_label_logit(hh, W, bias, labels, T, d, coff)

@@ -172,23 +172,27 @@ __global__ __launch_bounds__(256) void ce_label_logit_kernel(const bf16* __restr
   if (lane == 0) out[row] = acc + (bias ? bias[lab] : 0.f);
 }
 
-// lse = c + log(sum of the row's per-tile sums of P); row loss = lse - c (labelled rows; 0 and lse = 0 otherwise)
+// lse = c + log(sum of the row's per-tile sums of P); row loss = lse - c (labelled rows; 0 and lse = 0 otherwise).
+// part is tile-major [ntile][rows]: one thread per row, coalesced across the threads for every tile.
 __global__ __launch_bounds__(256) void ce_prob_rows_kernel(const float* __restrict__ part, int ntile,
                                                            const float* __restrict__ off, const int* __restrict__ labels,
                                                            int rows, float* __restrict__ lse, float* __restrict__ row_loss) {
-  const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int row = blockIdx.x * 256 + threadIdx.x;
   if (row >= rows) return;
-  const float* pr = part + (long long)row * ntile;
-  float se = 0.f;
-  for (int t = lane; t < ntile; t += 64) se += pr[t];
-  se = wave_sum(se);
-  if (lane == 0) {
-    const bool live = labels[row] != 0;
-    const float l = live ? __logf(se) : 0.f;
-    lse[row] = live ? off[row] + l : 0.f;
-    row_loss[row] = l;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  int t = 0;
+  for (; t + 4 <= ntile; t += 4) {
+    s0 += part[(long long)t * rows + row];
+    s1 += part[(long long)(t + 1) * rows + row];
+    s2 += part[(long long)(t + 2) * rows + row];
+    s3 += part[(long long)(t + 3) * rows + row];
   }
+  for (; t < ntile; ++t) s0 += part[(long long)t * rows + row];
+  const float se = (s0 + s1) + (s2 + s3);
+  const bool live = labels[row] != 0;
+  const float l = live ? __logf(se) : 0.f;
+  lse[row] = live ? off[row] + l : 0.f;
+  row_loss[row] = l;
 }
 
 // Backward prologue of the P-head, one wave per row: q = g * w_chunk, r = q * exp(c - lse) (0 for ignored rows),
@@ -695,8 +699,8 @@ SVAE_EXPORT int svae_ce_prob_finalize(const float* part, int32_t ntile, const fl
       chunk_len <= 0 || (long long)(nchunks - 1) * chunk_len >= seq)
     return SVAE_EINVAL;
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(ce_prob_rows_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, part, ntile, row_off, labels, rows, lse,
-                     row_loss);
+  hipLaunchKernelGGL(ce_prob_rows_kernel, dim3((rows + 255) / 256), dim3(256), 0, s, part, ntile, row_off, labels, rows,
+                     lse, row_loss);
   hipLaunchKernelGGL(ce_reduce_part_kernel, dim3(CE_RED_BLOCKS, nchunks), dim3(256), 0, s, row_loss, labels,
                      (const float*)nullptr, rows, seq, nchunks, chunk_len, red_ws);
   hipLaunchKernelGGL(ce_reduce_final_kernel, dim3(1), dim3(256), 0, s, red_ws, nchunks, chunk_w, nll_out);

@@ -713,6 +713,9 @@ __device__ __forceinline__ void g3_epilogue(const GP& p, char* smem, const f32x4
 // waves through the side area into the 128-column partials ce_rows_kernel expects; the label logit is written
 // by the lane holding it.
 constexpr float G3_LOG2E = 1.4426950408889634f;
+#ifndef SVAE_P_NT
+#define SVAE_P_NT 0   // P-head stores: cached (A/B: -DSVAE_P_NT=1 nontemporal)
+#endif
 
 __device__ __forceinline__ unsigned pack_bf16x2(float a, float b) {
   typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
@@ -800,7 +803,7 @@ __device__ __forceinline__ void g3_reg_epilogue(const GP& p, const f32x4 (&acc)[
               x2[h][e] = x;
               se += x;
             }
-          store_pair_bf16<true>(crow, 32 * jp, row_ok ? nleft : 0, x2[0], x2[1], g);
+          store_pair_bf16<SVAE_P_NT != 0>(crow, 32 * jp, row_ok ? nleft : 0, x2[0], x2[1], g);
         }
         se = sum_x16_x32(se);
         if (g == 0) sstat[rl * 4 + wc] = se;
@@ -860,11 +863,13 @@ __device__ __forceinline__ void g3_reg_epilogue(const GP& p, const f32x4 (&acc)[
     }
   }
   if constexpr (EPI == SVAE_EPI_CE_PROB) {
+    // tile-major partial sums aux[128-column tile][M]: a wave writes 64 consecutive rows of one tile (256 B runs;
+    // a row-major [M][tiles] layout scatters 4-B writes 1 KiB apart, each a partial-line write)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    const int row = tid >> 1, hf = tid & 1, m = m0 + row;   // 512 threads: (row, 128-column half)
+    const int row = tid & 255, hf = tid >> 8, m = m0 + row;   // 512 threads: (128-column half, row)
     if (m < p.M && n0 + 128 * hf < p.N)
-      ((float*)p.aux)[(long long)m * p.tiles_n + bn * 2 + hf] = sstat[row * 4 + 2 * hf] + sstat[row * 4 + 2 * hf + 1];
+      ((float*)p.aux)[(long long)(bn * 2 + hf) * p.M + m] = sstat[row * 4 + 2 * hf] + sstat[row * 4 + 2 * hf + 1];
   }
 }
 

@@ -533,7 +533,7 @@ class VAEEngine:
         if head == 'prob':
             coff = ws.get('ce.off', (T,), f32)
             K.ce_label_logit(hh, W, bias, labels, T, d, coff)
-            part = ws.get('ce.psum', (T, ntile), f32)
+            part = ws.get('ce.psum', (ntile, T), f32)          # tile-major per-tile sums of P
             K.gemm(hh, W, logits, T, V, d, epi=EPI_CE_PROB, bias=bias, aux=part, labels=labels, row_a=coff)
         else:
             coff = None

@@ -105,7 +105,7 @@ def _prob_head(hh, W, bias, lab, T, L, V, d, nchunks, chunk_len, g=0.75):
     coff = torch.empty(T, device=dev)
     K.ce_label_logit(hh, W, bias, lab, T, d, coff)
     Pm = torch.empty(T, V, dtype=torch.bfloat16, device=dev)
-    part = torch.empty(T, ntile, device=dev)
+    part = torch.empty(ntile, T, device=dev)
     K.gemm(hh, W, Pm, T, V, d, epi=N.EPI_CE_PROB, bias=bias, aux=part, labels=lab, row_a=coff)
     lse, rl, cw, nll = (torch.empty(T, device=dev), torch.empty(T, device=dev), torch.empty(nchunks, device=dev),
                         torch.empty(1, device=dev))
