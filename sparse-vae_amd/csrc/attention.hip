@@ -274,25 +274,31 @@ __device__ __forceinline__ void attn_fwd_tile(const AP& p, char* smem, int bx, i
       }
       const bool pad_any = pad && __builtin_amdgcn_ballot_w64((pms[lane] & 0xFFu) != 0) != 0;
       if (pad_any || kbase + 64 > p.Lk || (p.causal && kbase + 63 > qw) || (kbase + 63 >= SBLK && kbase < lo_w)) {
-        // this lane's key-padding bits for its 16 keys (keys 16sx + 4g + r) gathered once
+        // Edge tile (wave-uniform branch). The per-key tests are branch-free: bitwise ORs of compares feeding one
+        // select per score (short-circuit || compiled to an exec-mask branch per score, ~5 scalar instructions each).
+        // This lane's keys are kl = 16 sx + 4 g + r; its key-padding bits come from 4 16-B LDS reads.
         unsigned pbits = 0;
         if (pad_any) {
 #pragma unroll
-          for (int sx = 0; sx < 4; ++sx)
+          for (int sx = 0; sx < 4; ++sx) {
+            const u32x4 pw = *(const u32x4*)(pms + 16 * sx + 4 * g);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) pbits |= ((pms[16 * sx + 4 * g + r] & 0xFFu) ? 1u : 0u) << (4 * sx + r);
+            for (int r = 0; r < 4; ++r) pbits |= (unsigned)((pw[r] & 0xFFu) != 0u) << (4 * sx + r);
+          }
         }
+        // visible iff kl < lim_j (ragged end; causal: key <= query) and not (hlo <= kl < hhi) (outside the window band)
+        const int lim0 = (p.causal ? min(p.Lk, qw + li + 1) : p.Lk) - kbase;
+        const int lim1 = (p.causal ? min(p.Lk, qw + 16 + li + 1) : p.Lk) - kbase;
+        const int hlo = SBLK - kbase, hhi = lo_w - kbase;
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int sx = 0; sx < 4; ++sx)
 #pragma unroll
-          for (int sx = 0; sx < 4; ++sx)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int kl = 16 * sx + 4 * g + r, key = kbase + kl;
-              if (key >= p.Lk || ((pbits >> (4 * sx + r)) & 1u) || (p.causal && key > qw + 16 * j + li) ||
-                  (key >= SBLK && key < lo_w))
-                s[j][sx][r] = -INFINITY;
-            }
+          for (int r = 0; r < 4; ++r) {
+            const int kl = 16 * sx + 4 * g + r;
+            const unsigned hid = ((pbits >> (4 * sx + r)) & 1u) | ((unsigned)(kl >= hlo) & (unsigned)(kl < hhi));
+            s[0][sx][r] = (hid | (unsigned)(kl >= lim0)) ? -INFINITY : s[0][sx][r];
+            s[1][sx][r] = (hid | (unsigned)(kl >= lim1)) ? -INFINITY : s[1][sx][r];
+          }
       }
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
