@@ -1,4 +1,5 @@
-"""Time the flash attention kernels alone at the C2 decoder shape (B=64, H=8, L=512, hd=64, q|k|v interleaved).
+"""Time the flash attention kernels alone at the C2 decoder shape (B=64, H=8, L=512, hd=64, q|k|v interleaved),
+some neighbours, and the C4 decoder shape (L=1024, hd=96).
 
     python scripts/attn_probe.py
 """
@@ -27,10 +28,15 @@ def timeit(fn, reps=20):
 
 
 def main():
-    for B, L, causal in [(64, 512, True), (64, 512, False), (16, 512, True), (256, 512, True), (64, 1024, True)]:
+    only = os.environ.get('ATTN_PROBE_ONLY')   # e.g. 'hd96': only the C4 decoder shape
+    cases = [(64, 512, True, 64), (64, 512, False, 64), (16, 512, True, 64), (256, 512, True, 64), (64, 1024, True, 64),
+             (64, 1024, True, 96)]
+    for B, L, causal, hd in cases:
+      if only == 'hd96' and hd != 96:
+          continue
       for with_o32 in (True, False):
-        H, hd = 8, 64
-        if not with_o32 and (B, L) != (64, 512):
+        H = 8
+        if not with_o32 and (B, L, hd) != (64, 512, 64):
             continue
         d = H * hd
         qkv = torch.randn(B * L, 3 * d, device=dev).bfloat16()
@@ -50,10 +56,10 @@ def main():
                                   delta=delta, dq_bf=dqkv, ldq_bf=3 * d, dk=dqkv[:, d:], dv=dqkv[:, 2 * d:], sdk=3 * d,
                                   sdv=3 * d, bdk=L * 3 * d, bdv=L * 3 * d, dq_part=part, **kw)
         if not with_o32:
-            print(f'B={B:4d} L={L:5d} causal={int(causal)} no-o32 fwd {t:8.1f} us', flush=True)
+            print(f'B={B:4d} L={L:5d} hd={hd:3d} causal={int(causal)} no-o32 fwd {t:8.1f} us', flush=True)
             continue
         tb = timeit(bwd)
-        print(f'B={B:4d} L={L:5d} causal={int(causal)}  fwd {t:8.1f} us {fl / t / 1e6:7.1f} TF/s   '
+        print(f'B={B:4d} L={L:5d} hd={hd:3d} causal={int(causal)}  fwd {t:8.1f} us {fl / t / 1e6:7.1f} TF/s   '
               f'bwd(+delta+dq) {tb:8.1f} us {2.5 * fl / tb / 1e6:7.1f} TF/s', flush=True)
 
 

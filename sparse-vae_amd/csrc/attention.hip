@@ -183,7 +183,8 @@ __device__ __forceinline__ void attn_fwd_tile(const AP& p, char* smem, int bx, i
   // 3 or 4 stages at 2 blocks / CU (73.5 vs 78.4 / 92 us): blocks in flight, not prefetch depth, set the time.
   constexpr int NS = ATTN_NS;
   constexpr int DMA_OPS = 2 * (64 * T::PITCH / 1024) / 4;   // buffer_load_lds per wave per (K, V) tile
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, li = lane & 15;
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, li = lane & 15;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: scalar branches, not exec masks
   const int q0 = bx * 128;
 #ifdef SVAE_STAMPS
   const int lin_id = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
@@ -435,6 +436,251 @@ __device__ __forceinline__ void attn_bwd_tile(const AP& p, char* smem, int kb, i
   char* dSs = smem + 6 * T::BYTES;                  // 128 key rows x 64 queries
   float* cst = (float*)(smem + 6 * T::BYTES + 2 * TS::BYTES);   // [buf][lse, delta][64] (DMA'd with the tile)
 
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, li = lane & 15;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: scalar branches, not exec masks
+  const int k0 = kb * BWD_KEYS;
+  const bf16* Q = p.q + b * p.bq + (long long)h * p.hd;
+  const bf16* K = p.k + b * p.bk + (long long)h * p.hd;
+  const bf16* V = p.v + b * p.bv + (long long)h * p.hd;
+  const bf16* dO = p.dout + b * p.bdo + (long long)h * p.hd;
+  const float* lse = p.lse + ((long long)b * p.H + h) * p.Lq;
+  const float* delta = p.delta + ((long long)b * p.H + h) * p.Lq;
+  const int kw = k0 + 32 * w;                       // this wave's first key
+  // V fragments of this wave's 32 keys stay in registers (B operands of dP = dO V^T); K fragments are read
+  // from the block's K tile in LDS each query tile (it is there anyway for dQ = dS K).
+  bool key_ok[2];
+  bf16x8 vf[2][NKK];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int key = kw + 16 * j + li;
+    key_ok[j] = key < p.Lk && !(p.pad && p.pad[(long long)b * p.Lk + key]);
+#pragma unroll
+    for (int kk = 0; kk < NKK; ++kk) {
+      const int d = 32 * kk + 8 * g;
+      u32x4 c = {0u, 0u, 0u, 0u};
+      if (key < p.Lk && d < p.hd) c = *(const u32x4*)(V + (long long)key * p.sv + d);
+      vf[j][kk] = __builtin_bit_cast(bf16x8, c);
+    }
+  }
+  const bool keys_all_ok = __builtin_amdgcn_ballot_w64(!(key_ok[0] && key_ok[1])) == 0;
+  {  // K tile (128 rows) for dQ = dS . K
+    dma_rows<HDP>(K, p.sk, k0, p.Lk, p.hd, Ks, w, lane);
+    dma_rows<HDP>(K, p.sk, k0 + 64, p.Lk, p.hd, Ks + T::BYTES, w, lane);
+  }
+  f32x4 dk[2][NT], dv[2][NT];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int t = 0; t < NT; ++t) { dk[j][t] = (f32x4){0.f, 0.f, 0.f, 0.f}; dv[j][t] = dk[j][t]; }
+
+  const float inv_scale = 1.0f / p.scale, c = p.scale * LOG2E;
+  const int qt0 = p.causal ? k0 / 64 : 0;
+  // sliding window: queries past the last in-band query of the block's last key block see none of its keys
+  // (block 0 holds the [CLS] keys, which every later query sees)
+  const int q_end = (p.window > 0 && k0 > 0) ? min(p.Lq, k0 + BWD_KEYS - SBLK + SBLK * p.window) : p.Lq;
+  const int nqt = (q_end + 63) / 64;
+  const int band_end = p.window > 0 && kw >= SBLK ? kw + SBLK * p.window : 0x7FFFFFFF;   // first query past kw's band
+  float* part = p.dq_part + ((long long)kb * p.B + b) * p.Lq * p.H * p.hd + (long long)h * p.hd;
+  const long long ldp = (long long)p.H * p.hd;
+  const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc((void*)part, 0, 0x7FFFFFF0, 0x00020000);
+  // Every wave issues exactly DQ_STORES dQ-partial stores per query tile after the next tile's DMA, so the
+  // end-of-tile wait can leave exactly those in flight (vmcnt retires in issue order).
+  constexpr int DQ_STORES = NT * 4;
+
+  // the row constants (lse, delta) of a query tile ride along with its Q / dO DMA into cst[buf][lse | delta]
+  const u32x4 lser = buffer_rsrc(lse, (unsigned)p.Lq * 4u), der = buffer_rsrc(delta, (unsigned)p.Lq * 4u);
+  auto fetch = [&](int qb, int buf) {
+    dma_rows<HDP>(Q, p.sq, qb, p.Lq, p.hd, QO + buf * 2 * T::BYTES, w, lane);
+    dma_rows<HDP>(dO, p.sdo, qb, p.Lq, p.hd, QO + buf * 2 * T::BYTES + T::BYTES, w, lane);
+    const int qo = qb + lane < p.Lq ? (qb + lane) * 4 : 0x7FFFFFF0;
+    if (w == 0) dma4_lds(lser, cst + buf * 128, qo);
+    else if (w == 1) dma4_lds(der, cst + buf * 128 + 64, qo);
+  };
+  if (qt0 < nqt) fetch(qt0 * 64, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  for (int qt = qt0; qt < nqt; ++qt) {
+    const int buf = (qt - qt0) & 1;
+    const int qb = qt * 64;
+    const char* Qs = QO + buf * 2 * T::BYTES;
+    const char* dOs = Qs + T::BYTES;
+    const float* nl = cst + buf * 128;
+    const bool more = qt + 1 < nqt;
+    if (more) fetch(qb + 64, buf ^ 1);
+    const bool live = (!p.causal || kw <= qb + 63) && qb < band_end;   // some key of this wave visible to some query
+    if (live) {
+      bf16x8 kf[2][NKK];
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int kk = 0; kk < NKK; ++kk) kf[j][kk] = *(const bf16x8*)(Ks + T::off(32 * w + 16 * j + li, g + 4 * kk));
+      // Masks only on edge tiles (wave-uniform): a masked score's accumulator starts at -inf, so the MFMA sum stays
+      // -inf and exp2 gives exactly 0; the tests are branch-free compares + one select per score (short-circuit ||
+      // compiled to an exec-mask branch per score, ~5 scalar instructions each).
+      const bool edge = !keys_all_ok || qb + 64 > p.Lq || (p.causal && kw + 31 > qb) || qb + 63 >= band_end;
+      const int qlim = min(p.Lq, band_end) - qb;   // queries ql >= qlim see nothing (ragged end, window)
+      // Two passes of TPP = 2 16-query row tiles: S and dP of a pass, its softmax, its dV / dK MFMAs (one k-step of
+      // 32 queries) and its dS^T stores, then the next pass (half the S / dP accumulators live at a time: 256 VGPRs
+      // without spills at 2 blocks / CU).
+      constexpr int TPP = 2;
+#pragma unroll
+      for (int pass = 0; pass < 4 / TPP; ++pass) {
+        f32x4 s[2][TPP], dp[2][TPP];
+#pragma unroll
+        for (int th = 0; th < TPP; ++th) {
+          const int t = pass * TPP + th;
+          const f32x4 sl = *(const f32x4*)(nl + 16 * t + 4 * g) * -inv_scale;   // -lse / scale
+          const f32x4 dl = -*(const f32x4*)(nl + 64 + 16 * t + 4 * g);          // -delta
+          s[0][th] = sl; s[1][th] = sl;
+          dp[0][th] = dl; dp[1][th] = dl;
+          if (edge) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+              const int kmin = p.causal ? kw + 16 * j + li - qb : -0x40000000;   // causal: query ql >= kmin sees it
+              const unsigned kbad = key_ok[j] ? 0u : 1u;
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const int ql = 16 * t + 4 * g + r;
+                s[j][th][r] = (kbad | (unsigned)(ql >= qlim) | (unsigned)(ql < kmin)) ? -INFINITY : s[j][th][r];
+              }
+            }
+          }
+#pragma unroll
+          for (int k2 = 0; k2 < NKK; ++k2) {
+            const bf16x8 qa = *(const bf16x8*)(Qs + T::off(16 * t + li, g + 4 * k2));
+            const bf16x8 oa = *(const bf16x8*)(dOs + T::off(16 * t + li, g + 4 * k2));
+            s[0][th] = mfma16(qa, kf[0][k2], s[0][th]);
+            s[1][th] = mfma16(qa, kf[1][k2], s[1][th]);
+            dp[0][th] = mfma16(oa, vf[0][k2], dp[0][th]);
+            dp[1][th] = mfma16(oa, vf[1][k2], dp[1][th]);
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int th = 0; th < TPP; ++th)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float pr = __builtin_amdgcn_exp2f(s[j][th][r] * c);
+              s[j][th][r] = pr;
+              dp[j][th][r] = pr * dp[j][th][r];
+            }
+        // dV^T += dO^T P ; dK^T += Q^T dS   (query order of k-step kk: 32kk + 16(jj>>2) + 4g + (jj&3))
+#pragma unroll
+        for (int k2 = 0; k2 < TPP / 2; ++k2) {
+          const int kk = pass * (TPP / 2) + k2;
+          const bf16x8 pf0 = pack8(s[0][2 * k2], s[0][2 * k2 + 1]), pf1 = pack8(s[1][2 * k2], s[1][2 * k2 + 1]);
+          const bf16x8 df0 = pack8(dp[0][2 * k2], dp[0][2 * k2 + 1]), df1 = pack8(dp[1][2 * k2], dp[1][2 * k2 + 1]);
+          const int r0 = 32 * kk + 4 * g + (li >> 2);
+#pragma unroll
+          for (int u = 0; u < NT; ++u) {
+            const int uu = 4 * u + (li & 3);
+            const bf16x8 ao = cat44(lds_read_tr(dOs + T::uoff(r0, uu)), lds_read_tr(dOs + T::uoff(r0 + 16, uu)));
+            dv[0][u] = mfma16(ao, pf0, dv[0][u]);
+            dv[1][u] = mfma16(ao, pf1, dv[1][u]);
+            const bf16x8 aq = cat44(lds_read_tr(Qs + T::uoff(r0, uu)), lds_read_tr(Qs + T::uoff(r0 + 16, uu)));
+            dk[0][u] = mfma16(aq, df0, dk[0][u]);
+            dk[1][u] = mfma16(aq, df1, dk[1][u]);
+          }
+        }
+        // dS^T -> LDS [key][q]: lane holds q = 16t + 4g + (0..3) at key row 32w + 16j + li
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int th = 0; th < TPP; ++th)
+            *(bf16x4*)(dSs + TS::uoff(32 * w + 16 * j + li, 4 * (pass * TPP + th) + g)) =
+                (bf16x4){f2bf(dp[j][th][0]), f2bf(dp[j][th][1]), f2bf(dp[j][th][2]), f2bf(dp[j][th][3])};
+      }
+    } else {
+      const bf16x4 z = {f2bf(0.f), f2bf(0.f), f2bf(0.f), f2bf(0.f)};
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) *(bf16x4*)(dSs + TS::uoff(32 * w + 16 * j + li, 4 * t + g)) = z;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();   // dS^T complete (a raw barrier: __syncthreads' vmcnt(0) would drain the DMA)
+    // partial dQ[q = qb + 16w + 4g + r][d = 16u + li] = sum over the block's 128 keys of dS[q][key] K[key][d]
+    f32x4 dq[NT];
+#pragma unroll
+    for (int u = 0; u < NT; ++u) dq[u] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    const int kvis = p.causal ? min(BWD_KEYS, qb + 64 - k0) : BWD_KEYS;   // keys past the tile's last query: dS = 0
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      if (32 * kk >= kvis) break;
+      const int kr = 32 * kk + 8 * g + (li >> 2);
+      const int uq = 4 * w + (li & 3);
+      const bf16x8 a = cat44(lds_read_tr(dSs + TS::uoff(kr, uq)), lds_read_tr(dSs + TS::uoff(kr + 4, uq)));
+#pragma unroll
+      for (int u = 0; u < NT; ++u) {
+        const int uk = 4 * u + (li & 3);
+        const bf16x8 bk = cat44(lds_read_tr(Ks + T::uoff(kr, uk)), lds_read_tr(Ks + T::uoff(kr + 4, uk)));
+        dq[u] = mfma16(a, bk, dq[u]);
+      }
+    }
+    // buffer stores, always DQ_STORES per wave: rows past Lq / dims past hd get an out-of-range offset and are dropped
+    // by the range check (no branches, and a fixed count for the wait below)
+    {
+      const int qrow = (qb + 16 * w + 4 * g) * (int)ldp + li;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const bool qok = qb + 16 * w + 4 * g + r < p.Lq;
+#pragma unroll
+        for (int u = 0; u < NT; ++u) {
+          const int off = (qok && 16 * u + li < p.hd) ? (qrow + r * (int)ldp + 16 * u) * 4 : 0x7FFFFFF0;
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(dq[u][r]), prs, off, 0, 0);
+        }
+      }
+    }
+    // the next tile's DMA (issued before this tile's stores) has landed; the stores stay in flight
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DQ_STORES) : "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+
+  // epilogue: dK (scaled, inverse rotary) and dV for key = kw + 16j + li, dims 16u + 4g + (0..3)
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int key = kw + 16 * j + li;
+    if (key >= p.Lk) continue;
+    bf16* DK = p.dk + b * p.bdk + (long long)key * p.sdk + (long long)h * p.hd;
+    bf16* DV = p.dv + b * p.bdv + (long long)key * p.sdv + (long long)h * p.hd;
+#pragma unroll
+    for (int u = 0; u < NT; ++u) {
+      const int d = 16 * u + 4 * g;
+      if (d >= p.hd) continue;
+      float x[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) x[r] = dk[j][u][r] * p.scale;
+      if (p.rot) {
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const int pair = (h * p.hd + d) / 2 + e;
+          const float2 cs = ((const float2*)p.rot)[(long long)key * (p.rot_d / 2) + pair];
+          const float a = x[2 * e], cc = x[2 * e + 1];
+          x[2 * e] = a * cs.x + cc * cs.y;
+          x[2 * e + 1] = -a * cs.y + cc * cs.x;
+        }
+      }
+      *(bf16x4*)(DK + d) = (bf16x4){f2bf(x[0]), f2bf(x[1]), f2bf(x[2]), f2bf(x[3])};
+      *(bf16x4*)(DV + d) = (bf16x4){f2bf(dv[j][u][0]), f2bf(dv[j][u][1]), f2bf(dv[j][u][2]), f2bf(dv[j][u][3])};
+    }
+  }
+}
+
+// hd 128 (hd 96 padded): the same algorithm in one pass of 64 queries with the original mask / store code, one wave
+// per SIMD (512 registers); the restructured attn_bwd_tile spills there (46 spills against 7).
+template <int HDP>
+__device__ __forceinline__ void attn_bwd_tile_wide(const AP& p, char* smem, int kb, int h, int b) {
+  using T = Tile<HDP>;          // [rows][HDP] bf16
+  using TS = Tile<64>;          // dS^T [128 keys][64 queries]
+  constexpr int NKK = HDP / 32, NT = HDP / 16;
+  char* QO = smem;                                  // [buf][Q, dO] tiles
+  char* Ks = smem + 4 * T::BYTES;                   // 128 key rows
+  char* dSs = smem + 6 * T::BYTES;                  // 128 key rows x 64 queries
+  float* cst = (float*)(smem + 6 * T::BYTES + 2 * TS::BYTES);   // [buf][lse, delta][64] (DMA'd with the tile)
+
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, li = lane & 15;
   const int k0 = kb * BWD_KEYS;
   const bf16* Q = p.q + b * p.bq + (long long)h * p.hd;
@@ -652,7 +898,8 @@ __global__ __launch_bounds__(256, HDP == 64 ? 2 : 1) void attn_bwd_kernel(AP p) 
   __shared__ __attribute__((aligned(16))) char smem[6 * Tile<HDP>::BYTES + 2 * Tile<64>::BYTES + 4 * 64 * 4];
   int kb, h, b;
   xcd_block(kb, h, b);
-  attn_bwd_tile<HDP>(p, smem, kb, h, b);
+  if constexpr (HDP == 64) attn_bwd_tile<HDP>(p, smem, kb, h, b);
+  else attn_bwd_tile_wide<HDP>(p, smem, kb, h, b);
 }
 
 // dQ = scale * sum over the key blocks that can see the query (causal: kb <= q / 128) of the partials;
