@@ -59,7 +59,9 @@ def shape_cases():
               (32768, 1536, 512, 0, 0, N.EPI_BF16, 1),        # QKV fwd
               (32768, 512, 512, 0, 0, N.EPI_F32, 1),          # out-proj fwd
               (32768, 2048, 512, 0, 0, N.EPI_BF16, 1),        # FFN2 dX (K = d)
-              (32768, 512, 2048, 0, 0, N.EPI_BF16, 1)]        # FFN1 dX
+              (32768, 512, 2048, 0, 0, N.EPI_BF16, 1),        # FFN1 dX
+              (8192, 8192, 8192, 0, 0, N.EPI_BF16, 1),        # square reference point
+              (4096, 4096, 4096, 0, 0, N.EPI_BF16, 1)]
     for (M, N_, K_, at, bt, epi, sp) in shapes:
         A = torch.randn((K_, M) if at else (M, K_), device=dev).to(bf16)
         B = torch.randn((K_, N_) if bt else (N_, K_), device=dev).to(bf16)
