@@ -173,11 +173,13 @@ __device__ unsigned long long svae_attn_stamps[1024][6];
 #endif
 
 
-// One 128-query tile of one (batch, head). smem: the K/V ring + key-padding ring of the kernel.
-template <int HDP>
+// One 128-query tile of one (batch, head). smem: the K/V ring + key-padding ring of the kernel. HDP: the LDS row
+// width (64 or 128 dims); HDC <= HDP: the dims the MFMAs cover (hd 96 runs HDC = 96 on 128-wide rows: no work on the
+// zero padding).
+template <int HDP, int HDC = HDP>
 __device__ __forceinline__ void attn_fwd_tile(const AP& p, char* smem, int bx, int h, int b) {
   using T = Tile<HDP>;
-  constexpr int NKK = HDP / 32, NT = HDP / 16;
+  constexpr int NKK = HDC / 32, NT = HDC / 16;
   // K/V ring: NS stages of (K, V) tiles filled NS - 1 key tiles ahead; the key-padding bytes ride along in an
   // [NS][64] ring. Measured at the C2 shape (hd 64): 2 stages at 3 blocks / CU (33 KB LDS, <= 170 VGPRs) beat
   // 3 or 4 stages at 2 blocks / CU (73.5 vs 78.4 / 92 us): blocks in flight, not prefetch depth, set the time.
@@ -376,12 +378,12 @@ __device__ __forceinline__ void attn_fwd_tile(const AP& p, char* smem, int bx, i
 // One query tile per workgroup. (Running query tiles x and nqt - 1 - x in one workgroup, to even out the causal
 // work, measured 68 -> 73 us at the C2 shape on two boxes out of three, scripts/attn_probe.py: half the workgroups
 // in flight cost more than the imbalance.)
-template <int HDP>
+template <int HDP, int HDC = HDP>
 __global__ __launch_bounds__(256, HDP == 64 ? 3 : 2) void attn_fwd_kernel(AP p) {
   __shared__ __attribute__((aligned(16))) char smem[ATTN_NS * 2 * Tile<HDP>::BYTES + ATTN_NS * 64 * 4];
   int bx, h, b;
   xcd_block(bx, h, b);
-  attn_fwd_tile<HDP>(p, smem, bx, h, b);
+  attn_fwd_tile<HDP, HDC>(p, smem, bx, h, b);
 }
 
 // ===================================================================================== backward
@@ -671,11 +673,11 @@ __device__ __forceinline__ void attn_bwd_tile(const AP& p, char* smem, int kb, i
 
 // hd 128 (hd 96 padded): the same algorithm in one pass of 64 queries with the original mask / store code, one wave
 // per SIMD (512 registers); the restructured attn_bwd_tile spills there (46 spills against 7).
-template <int HDP>
+template <int HDP, int HDC = HDP>
 __device__ __forceinline__ void attn_bwd_tile_wide(const AP& p, char* smem, int kb, int h, int b) {
   using T = Tile<HDP>;          // [rows][HDP] bf16
   using TS = Tile<64>;          // dS^T [128 keys][64 queries]
-  constexpr int NKK = HDP / 32, NT = HDP / 16;
+  constexpr int NKK = HDC / 32, NT = HDC / 16;   // the MFMAs cover HDC <= HDP dims (hd 96: HDC = 96)
   char* QO = smem;                                  // [buf][Q, dO] tiles
   char* Ks = smem + 4 * T::BYTES;                   // 128 key rows
   char* dSs = smem + 6 * T::BYTES;                  // 128 key rows x 64 queries
@@ -726,7 +728,7 @@ __device__ __forceinline__ void attn_bwd_tile_wide(const AP& p, char* smem, int 
   const int band_end = p.window > 0 && kw >= SBLK ? kw + SBLK * p.window : 0x7FFFFFFF;   // first query past kw's band
   float* part = p.dq_part + ((long long)kb * p.B + b) * p.Lq * p.H * p.hd + (long long)h * p.hd;
   const long long ldp = (long long)p.H * p.hd;
-  // On a full query tile (all 64 queries < Lq, hd == HDP) every wave issues exactly DQ_STORES dQ-partial stores
+  // On a full query tile (all 64 queries < Lq, hd == HDC) every wave issues exactly DQ_STORES dQ-partial stores
   // after the next tile's DMA, so the end-of-tile wait can leave exactly those in flight (vmcnt retires in
   // issue order); edge tiles wait for everything.
   constexpr int DQ_STORES = NT * 4;
@@ -854,7 +856,7 @@ __device__ __forceinline__ void attn_bwd_tile_wide(const AP& p, char* smem, int 
       }
     }
     // the next tile's DMA (issued before this tile's stores) has landed; on full tiles the stores stay in flight
-    if (qb + 64 <= p.Lq && p.hd == HDP) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DQ_STORES) : "memory");
+    if (qb + 64 <= p.Lq && p.hd == HDC) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DQ_STORES) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -893,13 +895,13 @@ __device__ __forceinline__ void attn_bwd_tile_wide(const AP& p, char* smem, int 
 // One key block per workgroup. (Pairing key blocks x and nkb - 1 - x per workgroup, to even out the causal
 // sweeps, measured slower: 219 -> 247 us at the C2 shape, 629 -> 771 us at L = 1024 -- half the workgroups and
 // two serial prologues per workgroup cost more than the imbalance.)
-template <int HDP>
+template <int HDP, int HDC = HDP>
 __global__ __launch_bounds__(256, HDP == 64 ? 2 : 1) void attn_bwd_kernel(AP p) {
   __shared__ __attribute__((aligned(16))) char smem[6 * Tile<HDP>::BYTES + 2 * Tile<64>::BYTES + 4 * 64 * 4];
   int kb, h, b;
   xcd_block(kb, h, b);
   if constexpr (HDP == 64) attn_bwd_tile<HDP>(p, smem, kb, h, b);
-  else attn_bwd_tile_wide<HDP>(p, smem, kb, h, b);
+  else attn_bwd_tile_wide<HDP, HDC>(p, smem, kb, h, b);
 }
 
 // dQ = scale * sum over the key blocks that can see the query (causal: kb <= q / 128) of the partials;
@@ -969,6 +971,7 @@ SVAE_EXPORT int svae_attn_fwd(const svae_attn_desc* d, svae_stream_t stream) {
   dim3 grid((d->Lq + 127) / 128, d->H, d->B);
   hipStream_t s = (hipStream_t)stream;
   if (d->hd <= 64) hipLaunchKernelGGL(attn_fwd_kernel<64>, grid, dim3(256), 0, s, p);
+  else if (d->hd <= 96) hipLaunchKernelGGL((attn_fwd_kernel<128, 96>), grid, dim3(256), 0, s, p);
   else hipLaunchKernelGGL(attn_fwd_kernel<128>, grid, dim3(256), 0, s, p);
   SVAE_LAUNCH_CHECK();
   return SVAE_OK;
@@ -989,6 +992,7 @@ SVAE_EXPORT int svae_attn_bwd(const svae_attn_desc* d, svae_stream_t stream) {
   else hipLaunchKernelGGL(attn_delta_kernel<16>, dim3((rows + 15) / 16), dim3(256), 0, s, p);
   dim3 grid((d->Lk + BWD_KEYS - 1) / BWD_KEYS, d->H, d->B);
   if (d->hd <= 64) hipLaunchKernelGGL(attn_bwd_kernel<64>, grid, dim3(256), 0, s, p);
+  else if (d->hd <= 96) hipLaunchKernelGGL((attn_bwd_kernel<128, 96>), grid, dim3(256), 0, s, p);
   else hipLaunchKernelGGL(attn_bwd_kernel<128>, grid, dim3(256), 0, s, p);
   const long long work = (long long)d->B * d->Lq * (d->H * d->hd / 4);
   hipLaunchKernelGGL(attn_dq_reduce_kernel, dim3((unsigned)min(8192LL, (work + 255) / 256)), dim3(256), 0, s, p);
