@@ -215,6 +215,9 @@ __device__ __forceinline__ void attn_fwd_tile(const AP& p, char* smem, int bx, i
   for (int j = 0; j < 2; ++j)
 #pragma unroll
     for (int t = 0; t < NT; ++t) o[j][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  // (Row sums of P by MFMA against a ones column of V^T -- 4 MFMAs per tile instead of 32 VALU adds -- sum the
+  // bf16-rounded P; measured: that moves a gradient norm ratio of the windowed small6_pad parity case from < 2 %
+  // to 2.03 %, so the row sums stay f32 VALU adds.)
   float m[2] = {-1e30f, -1e30f}, ls[2] = {0.f, 0.f};
   const int kv_end = p.causal ? min(p.Lk, q0 + 128) : p.Lk;
   const int ntiles = (kv_end + 63) / 64;
@@ -307,7 +310,10 @@ __device__ __forceinline__ void attn_fwd_tile(const AP& p, char* smem, int bx, i
       for (int j = 0; j < 2; ++j) {
         float mx = -INFINITY;
 #pragma unroll
-        for (int sx = 0; sx < 4; ++sx) mx = fmaxf(fmaxf(mx, fmaxf(s[j][sx][0], s[j][sx][1])), fmaxf(s[j][sx][2], s[j][sx][3]));
+        for (int sx = 0; sx < 4; ++sx) {   // (v_max3_f32 chains: 8 per 16 scores)
+          mx = fmaxf(fmaxf(mx, s[j][sx][0]), s[j][sx][1]);
+          mx = fmaxf(fmaxf(mx, s[j][sx][2]), s[j][sx][3]);
+        }
         mx = max_x16_x32(mx);
         // rescale O and the row sum only when some row's max grew (wave-uniform branch; alpha would be exactly 1
         // for every other row, so the result is bit-identical to rescaling every tile)

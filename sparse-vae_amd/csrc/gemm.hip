@@ -785,8 +785,7 @@ __device__ __forceinline__ void g3_reg_epilogue(const GP& p, const f32x4 (&acc)[
         }
       } else if constexpr (EPI == SVAE_EPI_CE_PROB) {
         // p = exp(logit - c_row) for rows with a target (0 elsewhere); the f32 values feed the per-tile sums below
-        const float off = sstat[1024 + rl] * G3_LOG2E;
-        const bool live = slabel[rl] != 0;
+        const float off = sstat[1024 + rl] * G3_LOG2E;   // +inf for rows without a target: P = 0
         const bool ragged = n0 + wc * 64 + 64 > p.N;   // wave-uniform
         float se = 0.f;
 #pragma unroll
@@ -799,7 +798,6 @@ __device__ __forceinline__ void g3_reg_epilogue(const GP& p, const f32x4 (&acc)[
               const int j = 2 * jp + h;
               float x = __builtin_amdgcn_exp2f(fminf(fmaf(v[j][e], G3_LOG2E, -off), 127.0f));
               if (ragged && n0 + wc * 64 + j * 16 + 4 * g + e >= p.N) x = 0.f;
-              x = live ? x : 0.f;
               x2[h][e] = x;
               se += x;
             }
@@ -1246,7 +1244,10 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GP p) {
       sbias[tid] = (p.bias && n < p.N) ? p.bias[n] : 0.f;
       if (EPI == SVAE_EPI_CE_STATS || EPI == SVAE_EPI_CE_PROB || EPI == SVAE_EPI_ROWSCALE_GATHER)
         slabel[tid] = m < p.M ? p.labels[m] : 0;
-      if (EPI == SVAE_EPI_CE_PROB || EPI == SVAE_EPI_ROWSCALE_GATHER) sstat[1024 + tid] = m < p.M ? p.row_a[m] : 0.f;
+      // CE_PROB: a row without a target gets offset +inf, so its P comes out exactly 0 from the exp2 (no select per
+      // element)
+      if (EPI == SVAE_EPI_CE_PROB) sstat[1024 + tid] = (m < p.M && p.labels[m] != 0) ? p.row_a[m] : INFINITY;
+      if (EPI == SVAE_EPI_ROWSCALE_GATHER) sstat[1024 + tid] = m < p.M ? p.row_a[m] : 0.f;
       if (EPI == SVAE_EPI_ROWSCALE_GATHER) sstat[1280 + tid] = m < p.M ? p.row_b[m] : 0.f;
     }
     // every wave's reads of the last K-tile's stage are done: it becomes the epilogue's staging area
