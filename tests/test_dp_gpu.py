@@ -2,8 +2,9 @@
 runs the real bucketed async all-reduce overlapped with the engine backward (ready() callbacks, the broadcast at
 enable_data_parallel, the final wait). Gradients and the optimizer step must equal the non-DP run (a SUM
 all-reduce over one rank; the backward runs on loss / world = loss) up to the backward's own run-to-run noise:
-f32 atomics (embedding scatter-add, bias row sums) add in a nondeterministic order, so the bar is 1e-5 of the
-norm, not bitwise. The 2..8-rank runs are the driver's
+f32 atomics (embedding scatter-add, bias row sums) add in a nondeterministic order, so the bar is 1e-4 of the
+norm, not bitwise (measured run-to-run: up to 1.4e-5 of the norm; a DP bug -- a missing 1/world, a bucket reduced
+twice or skipped -- is an O(1) relative error). The 2..8-rank runs are the driver's
 (bench.py under torch.distributed.run); the multi-rank averaging itself is covered on CPU by test_dp_gloo.py."""
 import os
 import socket
@@ -54,6 +55,6 @@ def test_rccl_data_parallel_one_rank_matches_single_gpu():
             outs.append((o['loss'].item(), g, m._flat.master[:m._flat.n_live].clone()))
         assert outs[0][0] == outs[1][0]
         for a, b in ((outs[0][1], outs[1][1]), (outs[0][2], outs[1][2])):
-            assert ((a - b).norm() / b.norm()).item() < 1e-5
+            assert ((a - b).norm() / b.norm()).item() < 1e-4
     finally:
         dist.destroy_process_group()
