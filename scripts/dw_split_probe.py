@@ -26,10 +26,12 @@ def timeit(fn, reps=20):
 
 
 T = 32768
-for n_out, n_in in [(512, 512), (1536, 512), (2048, 512), (512, 2048)]:
+RS = os.environ.get('DW_RS') == '1'   # with the fused bias-gradient row sums (as in the step)
+for n_out, n_in in [(512, 512), (1024, 512), (1536, 512), (2048, 512), (512, 2048)]:
     dY = torch.randn(T, n_out, device=dev).bfloat16()
     X = torch.randn(T, n_in, device=dev).bfloat16()
     Wg = torch.zeros(n_out, n_in, device=dev)
+    bg = torch.zeros(n_out, device=dev) if RS else None
     auto = K.auto_splits(n_out, n_in, T)
     for s in sorted({auto, 16, 32, 64, 128}):
         if T // s < 256:
@@ -38,7 +40,7 @@ for n_out, n_in in [(512, 512), (1536, 512), (2048, 512), (512, 2048)]:
 
         def fn():
             K.gemm(dY, X, Wg, n_out, n_in, T, a_t=True, b_t=True, lda=n_out, ldb=n_in, ldc=n_in,
-                   epi=N.EPI_F32_ATOMIC if s > 1 else N.EPI_F32_ACC, splits=s, aux=slab)
+                   epi=N.EPI_F32_ATOMIC if s > 1 else N.EPI_F32_ACC, splits=s, aux=slab, a_rowsum=bg)
         us = timeit(fn)
-        print(f'dW {n_out}x{n_in} K={T} splits={s:4d}{" (auto)" if s == auto else "       "} {us:8.1f} us '
+        print(f'dW{" rs" if RS else ""} impl={os.environ.get("SVAE_GEMM_IMPL", "0")} {n_out}x{n_in} K={T} splits={s:4d}{" (auto)" if s == auto else "       "} {us:8.1f} us '
               f'{2.0 * n_out * n_in * T / us / 1e6:7.1f} TF/s', flush=True)

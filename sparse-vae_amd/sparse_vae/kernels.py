@@ -63,8 +63,10 @@ def auto_splits(M, N_, K, target=512):
     t256 = -(-M // 256) * -(-N_ // 256)
     if t256 >= 192:
         return 1
-    if t256 >= 8:   # fill the 256 CUs with one round of 256x256 blocks (1 per CU), K-slices >= 1024
-        s3 = min(256 // t256, max(1, K // 1024))
+    if t256 >= 4:   # fill the 256 CUs with one round of 256x256 blocks (1 per CU), K-slices >= 512
+        # (the 512 x 512 dW over 32768 rows with bias row sums: 64 x 256^2 slices 50.7 us against 62.3 us for
+        # 32 x 128^2 -- scripts/dw_split_probe.py with DW_RS=1, profiles/r02_dw_split_impl.log)
+        s3 = min(256 // t256, max(1, K // 512))
         if t256 * s3 >= 192:
             return s3
     tiles = -(-M // 128) * -(-N_ // 128)
