@@ -913,36 +913,47 @@ __global__ __launch_bounds__(256, HDP == 64 ? 2 : 1) void attn_bwd_kernel(AP p) 
 // dQ = scale * sum over the key blocks that can see the query (causal: kb <= q / 128) of the partials;
 // bf16 out with inverse rotary (pos = query) or f32 out. One thread per 4 columns of one (batch, query).
 __global__ __launch_bounds__(256) void attn_dq_reduce_kernel(AP p) {
+  // one thread per 4 columns of one (batch, query) row: 32-bit index math only (the former 64-bit div / mod per
+  // element of a grid-stride loop cost more than the memory traffic), all partial-plane loads of a thread issued
+  // before the adds
   const int D = p.H * p.hd, D4 = D / 4;
-  const long long total = (long long)p.B * p.Lq * D4;
+  const int rows = p.B * p.Lq;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= rows * D4) return;
+  const int row = i / D4, c4 = i - row * D4;      // row = b * Lq + q
+  const int b = row / p.Lq, q = row - b * p.Lq;
   const int nkb = (p.Lk + BWD_KEYS - 1) / BWD_KEYS;
-  const long long plane = (long long)p.B * p.Lq * D;
-  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
-    const int c4 = (int)(i % D4);
-    const long long row = i / D4;                 // b * Lq + q
-    const int q = (int)(row % p.Lq), b = (int)(row / p.Lq);
-    const int nk = p.causal ? min(nkb, q / BWD_KEYS + 1) : nkb;
-    // sliding window: key block k >= 1 wrote partials only for the query tiles it swept (see attn_bwd_kernel)
-    int k1 = 1;
-    if (p.window > 0)
-      while (k1 < nk && q >= (min(p.Lq, k1 * BWD_KEYS + BWD_KEYS - SBLK + SBLK * p.window) + 63) / 64 * 64) ++k1;
-    const float* src = p.dq_part + row * D + 4 * c4;
-    f32x4 acc = *(const f32x4*)src;
-    for (int k = k1; k < nk; ++k) acc += *(const f32x4*)(src + k * plane);
-    acc *= p.scale;
-    if (p.dq_bf) {
-      if (p.rot) {   // inverse of (a c - b s, b c + a s) on the pairs (4c4, 4c4+1), (4c4+2, 4c4+3)
-        const f32x4 cs = *(const f32x4*)(p.rot + ((long long)q * (p.rot_d / 2) + 2 * c4) * 2);
-        const float a0 = acc[0], b0 = acc[1], a1 = acc[2], b1 = acc[3];
-        acc[0] = a0 * cs[0] + b0 * cs[1];
-        acc[1] = -a0 * cs[1] + b0 * cs[0];
-        acc[2] = a1 * cs[2] + b1 * cs[3];
-        acc[3] = -a1 * cs[3] + b1 * cs[2];
-      }
-      *(bf16x4*)((bf16*)p.dq_bf + row * p.ldq_bf + 4 * c4) = (bf16x4){f2bf(acc[0]), f2bf(acc[1]), f2bf(acc[2]), f2bf(acc[3])};
-    } else {
-      *(f32x4*)(p.dq + b * p.bdq + (long long)q * D + 4 * c4) = acc;
+  const long long plane = (long long)rows * D;
+  const int nk = p.causal ? min(nkb, q / BWD_KEYS + 1) : nkb;
+  // sliding window: key block k >= 1 wrote partials only for the query tiles it swept (see attn_bwd_kernel)
+  int k1 = 1;
+  if (p.window > 0)
+    while (k1 < nk && q >= (min(p.Lq, k1 * BWD_KEYS + BWD_KEYS - SBLK + SBLK * p.window) + 63) / 64 * 64) ++k1;
+  const float* src = p.dq_part + (long long)row * D + 4 * c4;
+  f32x4 acc = *(const f32x4*)src;
+  int k = k1;
+  for (; k + 4 <= nk; k += 4) {
+    const f32x4 v0 = *(const f32x4*)(src + k * plane), v1 = *(const f32x4*)(src + (k + 1) * plane);
+    const f32x4 v2 = *(const f32x4*)(src + (k + 2) * plane), v3 = *(const f32x4*)(src + (k + 3) * plane);
+    acc += v0;
+    acc += v1;
+    acc += v2;
+    acc += v3;
+  }
+  for (; k < nk; ++k) acc += *(const f32x4*)(src + k * plane);
+  acc *= p.scale;
+  if (p.dq_bf) {
+    if (p.rot) {   // inverse of (a c - b s, b c + a s) on the pairs (4c4, 4c4+1), (4c4+2, 4c4+3)
+      const f32x4 cs = *(const f32x4*)(p.rot + ((long long)q * (p.rot_d / 2) + 2 * c4) * 2);
+      const float a0 = acc[0], b0 = acc[1], a1 = acc[2], b1 = acc[3];
+      acc[0] = a0 * cs[0] + b0 * cs[1];
+      acc[1] = -a0 * cs[1] + b0 * cs[0];
+      acc[2] = a1 * cs[2] + b1 * cs[3];
+      acc[3] = -a1 * cs[3] + b1 * cs[2];
     }
+    *(bf16x4*)((bf16*)p.dq_bf + (long long)row * p.ldq_bf + 4 * c4) = (bf16x4){f2bf(acc[0]), f2bf(acc[1]), f2bf(acc[2]), f2bf(acc[3])};
+  } else {
+    *(f32x4*)(p.dq + b * p.bdq + (long long)q * D + 4 * c4) = acc;
   }
 }
 
@@ -992,6 +1003,7 @@ SVAE_EXPORT int svae_attn_bwd(const svae_attn_desc* d, svae_stream_t stream) {
   if (d->rot_tab && d->rot_d <= 0) return SVAE_EINVAL;
   if (d->hd % 4 || (d->dq_bf && d->ldq_bf % 4) || (!d->dq_bf && d->bdq % 4)) return SVAE_EINVAL;
   if (d->dq_bf && d->rot_tab && d->rot_d != d->H * d->hd) return SVAE_EINVAL;
+  if ((long long)d->B * d->Lq * (d->H * d->hd / 4) > 0x7FFFFF00LL) return SVAE_EINVAL;   // (32-bit dQ-reduce index)
   hipStream_t s = (hipStream_t)stream;
   const int rows = d->B * d->Lq * d->H;
   if (d->hd <= 64) hipLaunchKernelGGL(attn_delta_kernel<8>, dim3((rows + 31) / 32), dim3(256), 0, s, p);
@@ -1001,7 +1013,7 @@ SVAE_EXPORT int svae_attn_bwd(const svae_attn_desc* d, svae_stream_t stream) {
   else if (d->hd <= 96) hipLaunchKernelGGL((attn_bwd_kernel<128, 96>), grid, dim3(256), 0, s, p);
   else hipLaunchKernelGGL(attn_bwd_kernel<128>, grid, dim3(256), 0, s, p);
   const long long work = (long long)d->B * d->Lq * (d->H * d->hd / 4);
-  hipLaunchKernelGGL(attn_dq_reduce_kernel, dim3((unsigned)min(8192LL, (work + 255) / 256)), dim3(256), 0, s, p);
+  hipLaunchKernelGGL(attn_dq_reduce_kernel, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, s, p);
   SVAE_LAUNCH_CHECK();
   return SVAE_OK;
 }
