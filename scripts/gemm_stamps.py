@@ -55,8 +55,14 @@ lab = torch.empty(T, device=dev)
 report('head bf16', lambda: K.gemm(h, W, logits, T, V, d, epi=N.EPI_BF16, bias=bias))
 report('head ce_stats', lambda: K.gemm(h, W, logits, T, V, d, epi=N.EPI_CE_STATS, bias=bias, aux=part,
                                        labels=labels, label_logit=lab))
+row_a = torch.randn(T, device=dev)
+report('head ce_prob', lambda: K.gemm(h, W, logits, T, V, d, epi=N.EPI_CE_PROB, bias=bias, aux=part, labels=labels,
+                                      row_a=row_a))
 W1 = (0.02 * torch.randn(2048, d, device=dev)).to(bf16)
 f = torch.empty(T, 2048, dtype=bf16, device=dev)
 gp = torch.empty(T, 2048, dtype=bf16, device=dev)
 report('ffn1 bf16', lambda: K.gemm(h, W1, f, T, 2048, d, epi=N.EPI_BF16))
 report('ffn1 gelu', lambda: K.gemm(h, W1, f, T, 2048, d, epi=N.EPI_GELU, bias=bias[:2048], aux=gp, ldaux=2048))
+A8 = torch.randn(8192, 8192, device=dev).to(bf16)
+C8 = torch.empty(8192, 8192, device=dev, dtype=bf16)
+report('8K^3 bf16', lambda: K.gemm(A8, A8, C8, 8192, 8192, 8192, epi=N.EPI_BF16))
