@@ -40,6 +40,8 @@ def report(name, fn):
     loop = s[:, 1:ntiles, 1] - s[:, 1:ntiles, 0]
     epi = s[:, 1:ntiles, 2] - s[:, 1:ntiles, 1]
     gap = s[:, 2:ntiles, 0] - s[:, 1:ntiles - 1, 2]
+    if ntiles == 1:   # one tile per block: the first (cold) tile is all there is
+        loop, epi = s[:, :1, 1] - s[:, :1, 0], s[:, :1, 2] - s[:, :1, 1]
     print(f'{name:28s} tiles/block {ntiles:3d}  K-loop {np.median(loop):8.0f} cyc  epilogue {np.median(epi):7.0f} cyc  '
           f'between {np.median(gap) if gap.size else 0:6.0f} cyc', flush=True)
 
@@ -63,6 +65,19 @@ f = torch.empty(T, 2048, dtype=bf16, device=dev)
 gp = torch.empty(T, 2048, dtype=bf16, device=dev)
 report('ffn1 bf16', lambda: K.gemm(h, W1, f, T, 2048, d, epi=N.EPI_BF16))
 report('ffn1 gelu', lambda: K.gemm(h, W1, f, T, 2048, d, epi=N.EPI_GELU, bias=bias[:2048], aux=gp, ldaux=2048))
+x32 = torch.randn(T, d, device=dev)
+o32 = torch.empty(T, d, device=dev)
+hb = torch.randn(T, 2048, device=dev).to(bf16)
+W2 = (0.02 * torch.randn(d, 2048, device=dev)).to(bf16)
+Wo = (0.02 * torch.randn(d, d, device=dev)).to(bf16)
+report('outproj f32+resid', lambda: K.gemm(h, Wo, o32, T, d, d, epi=N.EPI_F32, bias=bias[:d], resid=x32, ldr=d))
+report('outproj bf16', lambda: K.gemm(h, Wo, f[:, :d], T, d, d, epi=N.EPI_BF16, ldc=2048))
+report('ffn2 bf16', lambda: K.gemm(hb, W2, f[:, :d], T, d, 2048, epi=N.EPI_BF16, ldc=2048))
+report('ffn2 drop+resid', lambda: K.gemm(hb, W2, o32, T, d, 2048, epi=N.EPI_DROPOUT_RESID, resid=x32, ldr=d,
+                                         drop_p=0.1, seed=3))
+report('ffn2 resid (p=0)', lambda: K.gemm(hb, W2, o32, T, d, 2048, epi=N.EPI_DROPOUT_RESID, resid=x32, ldr=d,
+                                          drop_p=0.0, seed=3))
+report('ffn1-dX gelu_bwd', lambda: K.gemm(h, W1, f, T, 2048, d, epi=N.EPI_GELU_BWD, aux=gp, ldaux=2048))
 A8 = torch.randn(8192, 8192, device=dev).to(bf16)
 C8 = torch.empty(8192, 8192, device=dev, dtype=bf16)
 report('8K^3 bf16', lambda: K.gemm(A8, A8, C8, 8192, 8192, 8192, epi=N.EPI_BF16))
