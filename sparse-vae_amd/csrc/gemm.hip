@@ -740,6 +740,11 @@ __device__ __forceinline__ void store_pair_bf16(bf16* row_base, int colbase, int
   } else if (c < ncols_left) *(u32x2*)(row_base + c) = (u32x2){w[0], w[1]};
 }
 
+template <bool B>
+struct BoolC {
+  static constexpr bool value = B;
+};
+
 template <int EPI>
 __device__ __forceinline__ void g3_reg_epilogue(const GP& p, const f32x4 (&acc)[8][4], const float* sbias,
                                                 const int* slabel, float* sstat, int m0, int n0, int bn, int batch,
@@ -786,23 +791,30 @@ __device__ __forceinline__ void g3_reg_epilogue(const GP& p, const f32x4 (&acc)[
       } else if constexpr (EPI == SVAE_EPI_CE_PROB) {
         // p = exp(logit - c_row) for rows with a target (0 elsewhere); the f32 values feed the per-tile sums below
         const float off = sstat[1024 + rl] * G3_LOG2E;   // +inf for rows without a target: P = 0
-        const bool ragged = n0 + wc * 64 + 64 > p.N;   // wave-uniform
         float se = 0.f;
+        // the column bound is checked per element only on a wave whose 64 columns cross N (a scalar branch between
+        // two copies: if-converted into the one loop it cost 4 VALU per element, as much as the exp's arithmetic)
+        auto body = [&](auto rag) {
 #pragma unroll
-        for (int jp = 0; jp < 2; ++jp) {   // P [T, V] bf16 (2 GiB at C2): nontemporal stores
-          f32x4 x2[2];
+          for (int jp = 0; jp < 2; ++jp) {   // P [T, V] bf16 (2 GiB at C2)
+            f32x4 x2[2];
 #pragma unroll
-          for (int h = 0; h < 2; ++h)
+            for (int h = 0; h < 2; ++h)
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const int j = 2 * jp + h;
-              float x = __builtin_amdgcn_exp2f(fminf(fmaf(v[j][e], G3_LOG2E, -off), 127.0f));
-              if (ragged && n0 + wc * 64 + j * 16 + 4 * g + e >= p.N) x = 0.f;
-              x2[h][e] = x;
-              se += x;
-            }
-          store_pair_bf16<SVAE_P_NT != 0>(crow, 32 * jp, row_ok ? nleft : 0, x2[0], x2[1], g);
-        }
+              for (int e = 0; e < 4; ++e) {
+                const int j = 2 * jp + h;
+                float x = __builtin_amdgcn_exp2f(fminf(fmaf(v[j][e], G3_LOG2E, -off), 127.0f));
+                if constexpr (decltype(rag)::value) {
+                  if (n0 + wc * 64 + j * 16 + 4 * g + e >= p.N) x = 0.f;
+                }
+                x2[h][e] = x;
+                se += x;
+              }
+            store_pair_bf16<SVAE_P_NT != 0>(crow, 32 * jp, row_ok ? nleft : 0, x2[0], x2[1], g);
+          }
+        };
+        if (__builtin_amdgcn_readfirstlane((int)(n0 + wc * 64 + 64 > p.N))) body(BoolC<true>{});
+        else body(BoolC<false>{});
         se = sum_x16_x32(se);
         if (g == 0) sstat[rl * 4 + wc] = se;
       } else if (EPI != SVAE_EPI_CE_STATS || p.C) {   // CE statistics with C == nullptr: no logits stored
