@@ -9,6 +9,7 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef short short4v __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
@@ -124,6 +125,25 @@ __device__ __forceinline__ void gelu_pair(float x, float& g, float& gp) {
   const float cdf = x >= 0.f ? 1.0f - half_erfc : half_erfc;
   g = x * cdf;
   gp = fmaf(x * 0.3989422804014327f, e, cdf);
+}
+
+// gelu_pair on two elements with the packed f32 VALU ops (v_pk_fma/mul_f32: two lanes' worth per instruction):
+// the same A-S 7.1.26 formula with 0.5 folded into the coefficients; cdf = step(x) - sign(x) * Phi(-|x|) (one
+// rounding, no cancellation for x << 0). ~9 VALU + 2 transcendental per element instead of ~17 + 2.
+__device__ __forceinline__ void gelu_pair2(f32x2 x, f32x2& g, f32x2& gp) {
+  const f32x2 z = {fabsf(x[0]) * 0.70710678118654752f, fabsf(x[1]) * 0.70710678118654752f};
+  const f32x2 d = z * 0.3275911f + 1.0f;
+  const f32x2 t = {__builtin_amdgcn_rcpf(d[0]), __builtin_amdgcn_rcpf(d[1])};
+  const f32x2 poly = t * (((((t * 0.5307027145f) + -0.7265760135f) * t + 0.7107068705f) * t + -0.142248368f) * t +
+                          0.127414796f);                                   // 0.5 * A-S polynomial
+  const f32x2 w = (x * x) * -0.72134752044448170f;                        // -x^2/2 * log2(e)
+  const f32x2 e = {__builtin_amdgcn_exp2f(w[0]), __builtin_amdgcn_exp2f(w[1])};   // exp(-x^2 / 2)
+  const f32x2 h = poly * e;                                                 // Phi(-|x|)
+  const f32x2 sg = __builtin_elementwise_copysign((f32x2){1.0f, 1.0f}, x);
+  const f32x2 step = sg * 0.5f + 0.5f;
+  const f32x2 cdf = (-sg) * h + step;
+  g = x * cdf;
+  gp = (x * 0.3989422804014327f) * e + cdf;
 }
 
 // Counter-based RNG (splitmix64 finaliser over (seed, counter)): stateless, so the backward pass

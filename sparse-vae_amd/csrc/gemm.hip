@@ -776,11 +776,13 @@ __device__ __forceinline__ void g3_reg_epilogue(const GP& p, const f32x4 (&acc)[
 #pragma unroll
         for (int j = 0; j < 4; ++j)
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            float ge, de;
-            gelu_pair(v[j][e], ge, de);
-            gg[j][e] = ge;
-            dg[j][e] = de;
+          for (int e = 0; e < 4; e += 2) {
+            f32x2 ge, de;
+            gelu_pair2((f32x2){v[j][e], v[j][e + 1]}, ge, de);
+            gg[j][e] = ge[0];
+            gg[j][e + 1] = ge[1];
+            dg[j][e] = de[0];
+            dg[j][e + 1] = de[1];
           }
         bf16* arow = (bf16*)p.aux + (long long)(row_ok ? m : 0) * p.ldaux + n0 + wc * 64;
 #pragma unroll
