@@ -754,6 +754,29 @@ __device__ __forceinline__ void g3_reg_epilogue(const GP& p, const f32x4 (&acc)[
   f32x4 b4[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) b4[j] = *(const f32x4*)(sbias + wc * 64 + j * 16 + 4 * g);
+  // ROTARY: a lane's 4 consecutive columns are two whole (2i, 2i+1) rotary pairs, rotated in registers. The table
+  // offsets of its 4 column groups are per tile, the table row (position m mod rot_seq) steps by 16 per fragment
+  // row, and row i + 1's (cos, sin) are loaded before row i is rotated (columns >= rot_cols get the identity).
+  int rofs[4] = {0, 0, 0, 0};
+  bool rot_on[4] = {false, false, false, false};
+  int pos = 0, pstep = 0;
+  f32x4 cs_cur[4], cs_nxt[4];
+  auto rot_load = [&](int ps, f32x4 (&cs)[4]) {
+    const float* t = p.rot_tab + (long long)ps * p.rot_d;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) cs[j] = rot_on[j] ? *(const f32x4*)(t + rofs[j]) : (f32x4){1.f, 0.f, 1.f, 0.f};
+  };
+  if constexpr (EPI == SVAE_EPI_ROTARY_BF16) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = n0 + wc * 64 + j * 16 + 4 * g;
+      rot_on[j] = n < p.rot_cols;
+      rofs[j] = ((n % p.rot_d) >> 1) * 2;
+    }
+    pos = (m0 + wr * 128 + li) % p.rot_seq;
+    pstep = 16 % p.rot_seq;
+    rot_load(pos, cs_cur);
+  }
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int rl = wr * 128 + i * 16 + li, m = m0 + rl;
@@ -761,10 +784,23 @@ __device__ __forceinline__ void g3_reg_epilogue(const GP& p, const f32x4 (&acc)[
 #pragma unroll
     for (int j = 0; j < 4; ++j) v[j] = p.alpha * acc[i][j] + b4[j];
     if constexpr (EPI == SVAE_EPI_ROTARY_BF16) {
-      // a lane's 4 consecutive columns are two whole (2i, 2i+1) rotary pairs: rotate in registers
-      const int mr = m < p.M ? m : 0;
+      int pn = pos + pstep;
+      if (pn >= p.rot_seq) pn -= p.rot_seq;
+      if (i + 1 < 8) rot_load(pn, cs_nxt);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) rotary4(p, v[j], mr, n0 + wc * 64 + j * 16 + 4 * g);
+      for (int j = 0; j < 4; ++j) {
+        const f32x4 cs2 = cs_cur[j];
+        const float a0 = v[j][0], b0 = v[j][1], a1 = v[j][2], b1 = v[j][3];
+        v[j][0] = a0 * cs2[0] + (-b0) * cs2[1];
+        v[j][1] = b0 * cs2[0] + a0 * cs2[1];
+        v[j][2] = a1 * cs2[2] + (-b1) * cs2[3];
+        v[j][3] = b1 * cs2[2] + a1 * cs2[3];
+      }
+      pos = pn;
+      if (i + 1 < 8) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) cs_cur[j] = cs_nxt[j];
+      }
     }
     {
       // (the permlane swaps need every lane: the bounds are applied to the stores only)
