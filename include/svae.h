@@ -85,6 +85,13 @@ typedef struct svae_gemm_desc {
 
 int svae_gemm(const svae_gemm_desc* d, svae_stream_t stream);
 
+/* Two weight-gradient GEMMs in one launch (engine.layer_bwd pairs the two dW GEMMs of the FFN, and the output
+ * projection's with the QKV / K-V projection's: the nn.Linear weight gradients of transformer_layer.py:56-61 and
+ * attention.py:51-105 under loss.backward()). Each desc as for svae_gemm with a_t = b_t = 1, epi
+ * SVAE_EPI_F32_ATOMIC, splits >= 2 and a slab workspace in aux (aux[split][M][N] f32, then C += the sum of the
+ * splits); the results equal two svae_gemm calls with the same descs. */
+int svae_gemm_pair(const svae_gemm_desc* d0, const svae_gemm_desc* d1, svae_stream_t stream);
+
 /* ---- LayerNorm ---------------------------------------------------------------------------------
  * nn.LayerNorm(d, eps=1e-5) forward/backward: transformer_layer.py:23-24,39-40,47,52,56;
  * transformer_language_model.py:59. x_dtype: 0 = f32 input, 1 = bf16 input. y is bf16.

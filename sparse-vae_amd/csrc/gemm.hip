@@ -1107,8 +1107,10 @@ static_assert(G3_EPI_STORES == 16, "the first K-step's s_waitcnt literal below")
 // vocabulary head's dW, where the per-token weight r folds the softmax normalisation into the row sums)
 constexpr int G3_EPI_ACC_KW = 64;
 
+// The gemm256 block program over the tiles of one GEMM: block `blk` of `nwg` blocks working on p (the plain kernel
+// passes blockIdx.x / gridDim.x; the paired kernel gives each GEMM its own range of blocks).
 template <bool AT, bool BT, int EPI>
-__global__ __launch_bounds__(512, 1) void gemm256_kernel(GP p) {
+__device__ __forceinline__ void gemm256_run(const GP& p, int blk, int nwg) {
   // 2 ring stages + a side area: the epilogue's per-tile bias (256 f32), CE labels (256 i32) and CE row statistics
   // ([256 rows][4 column waves][max, sum]); one array
   __shared__ __attribute__((aligned(16))) char smem[2 * G3_STAGE + 2048 + 8192];
@@ -1118,10 +1120,10 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GP p) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3;
-  // XCD-aware bijective remap of the block id; block b then walks tiles b, b + G, b + 2G, ... (G = gridDim.x):
-  // with G = 256 every XCD runs one contiguous N-fastest range of tiles at a time.
-  const int nwg = gridDim.x;
-  int bid = blockIdx.x;
+  // XCD-aware bijective remap of the block id; block b then walks tiles b, b + G, b + 2G, ... (G = nwg):
+  // with G = 256 every XCD runs one contiguous N-fastest range of tiles at a time. (blk % 8 is the XCD: the paired
+  // kernel's block ranges start at multiples of 8.)
+  int bid = blk;
   if (nwg >= 16) {
     const int q = nwg / 8, r = nwg % 8, xcd = bid % 8, idx = bid / 8;
     bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
@@ -1341,6 +1343,27 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GP p) {
   }
 }
 
+template <bool AT, bool BT, int EPI>
+__global__ __launch_bounds__(512, 1) void gemm256_kernel(GP p) {
+  gemm256_run<AT, BT, EPI>(p, blockIdx.x, gridDim.x);
+}
+
+// Two independent GEMMs in one launch (the weight gradients of two layers of one transformer block, split-K slab
+// mode): blocks [0, nb0) run p[0], the rest p[1]. Each GEMM then needs only half the split-K slices to fill the
+// chip, which halves its slab bytes (written by the epilogue, read by slab_reduce) and shares one launch's
+// ramp-up and tail between the two.
+struct GP2 {
+  GP p[2];
+  int nb0;   // a multiple of 8
+};
+
+template <bool AT, bool BT, int EPI>
+__global__ __launch_bounds__(512, 1) void gemm256_pair_kernel(GP2 q) {
+  const int b = blockIdx.x;
+  if (b < q.nb0) gemm256_run<AT, BT, EPI>(q.p[0], b, q.nb0);
+  else gemm256_run<AT, BT, EPI>(q.p[1], b - q.nb0, (int)gridDim.x - q.nb0);
+}
+
 // C[m][n] += sum over splits of slab[s][m][n] (slab rows of N floats); 4 columns per thread
 __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restrict__ slab, float* __restrict__ C,
                                                           int M, int N, long long ldc, int splits) {
@@ -1367,7 +1390,7 @@ static int launch_slab_reduce(const svae_gemm_desc* d, hipStream_t s) {
   return SVAE_OK;
 }
 
-SVAE_EXPORT int svae_gemm(const svae_gemm_desc* d, svae_stream_t stream) {
+static int validate_desc(const svae_gemm_desc* d) {
   if (!d || !d->A || !d->B || (!d->C && d->epi != SVAE_EPI_CE_STATS)) return SVAE_EINVAL;
   const bool epi_new = d->epi == SVAE_EPI_CE_PROB || d->epi == SVAE_EPI_ROWSCALE_GATHER;
   if (d->M <= 0 || d->N <= 0 || d->K <= 0 || d->batch <= 0 || d->splits <= 0) return SVAE_EINVAL;
@@ -1397,7 +1420,10 @@ SVAE_EXPORT int svae_gemm(const svae_gemm_desc* d, svae_stream_t stream) {
     return SVAE_EINVAL;
   if (d->epi == SVAE_EPI_ROTARY_BF16 && (d->rot_d % 4 || d->rot_cols % 4)) return SVAE_EINVAL;
 
-  GP p;
+  return SVAE_OK;
+}
+
+static void fill_gp(const svae_gemm_desc* d, GP& p) {
   p.A = (const bf16*)d->A; p.B = (const bf16*)d->B;
   p.lda = d->lda; p.ldb = d->ldb; p.sA = d->batch_stride_a; p.sB = d->batch_stride_b;
   p.M = d->M; p.N = d->N; p.K = d->K; p.splits = d->splits;
@@ -1418,6 +1444,13 @@ SVAE_EXPORT int svae_gemm(const svae_gemm_desc* d, svae_stream_t stream) {
   p.gather = (const bf16*)d->gather; p.ldg = d->ldg;
   p.epi = d->epi;
   p.slab = 0;
+}
+
+SVAE_EXPORT int svae_gemm(const svae_gemm_desc* d, svae_stream_t stream) {
+  if (const int rc = validate_desc(d)) return rc;
+  const bool epi_new = d->epi == SVAE_EPI_CE_PROB || d->epi == SVAE_EPI_ROWSCALE_GATHER;
+  GP p;
+  fill_gp(d, p);
   // split-K slab mode (F32_ATOMIC with aux): every split stores its partial tile with plain stores into
   // aux[split][M][N], then slab_reduce adds the splits into C (no float atomics on C).
   const bool slab = d->epi == SVAE_EPI_F32_ATOMIC && d->splits > 1 && d->aux;
@@ -1554,6 +1587,40 @@ SVAE_EXPORT int svae_gemm(const svae_gemm_desc* d, svae_stream_t stream) {
 #undef SVAE_GEMM_CASE
   SVAE_LAUNCH_CHECK();
   return slab ? launch_slab_reduce(d, s) : SVAE_OK;
+}
+
+SVAE_EXPORT int svae_gemm_pair(const svae_gemm_desc* d0, const svae_gemm_desc* d1, svae_stream_t stream) {
+  const svae_gemm_desc* d[2] = {d0, d1};
+  GP2 q;
+  long long nb[2];
+  for (int i = 0; i < 2; ++i) {
+    if (const int rc = validate_desc(d[i])) return rc;
+    // the weight-gradient shape only: A and B transposed (row-major [K][M] and [K][N]), split-K slab mode
+    if (!d[i]->a_t || !d[i]->b_t || d[i]->epi != SVAE_EPI_F32_ATOMIC || d[i]->splits < 2 || !d[i]->aux ||
+        d[i]->batch != 1 || d[i]->k_weight || ((uintptr_t)d[i]->aux & 15))
+      return SVAE_EINVAL;
+    GP& p = q.p[i];
+    fill_gp(d[i], p);
+    p.C = d[i]->aux; p.ldc = d[i]->N; p.sC = 0; p.slab = (long long)d[i]->M * d[i]->N;
+    p.bias = nullptr; p.resid = nullptr;
+    const int kc3 = (d[i]->K + d[i]->splits - 1) / d[i]->splits;
+    p.kchunk = (kc3 + 63) / 64 * 64;
+    p.tn2 = (d[i]->N + 255) / 256;
+    p.tm2 = (d[i]->M + 255) / 256;
+    p.group = 0;
+    nb[i] = (long long)p.tn2 * p.tm2 * d[i]->splits;
+    if (nb[i] > (1 << 24)) return SVAE_EINVAL;
+    p.total3 = (int)nb[i];
+    p.desync = 0;
+    p.relaxed = 1;
+  }
+  q.nb0 = (int)((nb[0] + 7) / 8 * 8);   // block ranges start on an XCD boundary (block id % 8)
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL((gemm256_pair_kernel<true, true, SVAE_EPI_F32>), dim3((unsigned)(q.nb0 + nb[1])), dim3(512), 0, s,
+                     q);
+  SVAE_LAUNCH_CHECK();
+  if (const int rc = launch_slab_reduce(d0, s)) return rc;
+  return launch_slab_reduce(d1, s);
 }
 
 #ifdef SVAE_STAMPS

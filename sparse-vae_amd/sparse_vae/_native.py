@@ -61,6 +61,7 @@ class AttnDesc(ctypes.Structure):
 
 _SIGS = {
     'svae_gemm': [ctypes.POINTER(GemmDesc), c_void_p],
+    'svae_gemm_pair': [ctypes.POINTER(GemmDesc), ctypes.POINTER(GemmDesc), c_void_p],
     'svae_layernorm_fwd': [c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32,
                            c_void_p],
     'svae_layernorm_bwd': [c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

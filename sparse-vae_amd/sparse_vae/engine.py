@@ -235,6 +235,9 @@ class VAEEngine:
         # them into dlogits in place (ce_grad) -- the round-1 path, kept for A/B runs (SVAE_HEAD=logits)
         self.head_mode = os.environ.get('SVAE_HEAD', 'prob')
         assert self.head_mode in ('prob', 'logits'), self.head_mode
+        # the two dW GEMMs of the FFN, and the attention output projection's with the Q/K/V projection's, run as one
+        # paired launch each (kernels.linear_dw_pair); SVAE_DW_PAIR=0 launches them one by one (A/B runs)
+        self.dw_pair = os.environ.get('SVAE_DW_PAIR', '1') != '0'
         self.side = None
         if flat.device.type == 'cuda' and os.environ.get('SVAE_DW_STREAM', '0') != '0':
             self.side = torch.cuda.Stream(device=flat.device)
@@ -280,6 +283,24 @@ class VAEEngine:
         ev = torch.cuda.Event()
         ev.record(side)
         self.ws.busy[dY.untyped_storage().data_ptr()] = ev   # the next writer of dY's buffer waits for this read
+
+    def _dw_pair(self, j0, j1):
+        """Two _dw's ((dY, X, wname, rows, n_out, n_in[, ldy, ldx, bias])) in one paired launch (svae_gemm_pair):
+        half the split-K slab traffic of two separate launches. SVAE_DW_PAIR=0 (or the side stream) runs them apart."""
+        if self.side is not None or not self.dw_pair:
+            for j in (j0, j1):
+                self._dw(*j[:6], *(tuple(j[6:]) + (None,) * (9 - len(j))))
+            return
+        args = []
+        for j in (j0, j1):
+            dY, X, wname, rows, n_out, n_in = j[:6]
+            ldy, ldx, bias = tuple(j[6:]) + (None,) * (9 - len(j))
+            bg = None
+            if bias is not None:
+                off = self.P.offsets[bias][0]
+                bg = self.P.grad[off:off + n_out]
+            args.append((dY, X, self.P.g(wname), rows, n_out, n_in, ldy, ldx, bg))
+        K.linear_dw_pair(*args)
 
     def join_side(self):
         """The caller's stream waits for every weight-gradient GEMM issued so far."""
@@ -391,11 +412,12 @@ class VAEEngine:
         # ---- FFN (transformer_layer.py:56-61)
         g2 = ws.get('b.g2', (rows_q, d))
         K.dropout_bwd_cast(dout, g2, st['drop_p'], st['seed'], rows_q, d)
-        self._dw(g2, st['f'], pre + 'ffn.2.weight', rows_q, d, 4 * d)
         dpre = ws.get('b.dpre', (rows_q, 4 * d))
         K.gemm(g2, P.wT(pre + 'ffn.2.weight', d, 4 * d), dpre, rows_q, 4 * d, d, epi=EPI_GELU_BWD, aux=st['gprime'],
                ldaux=4 * d)
-        self._dw(dpre, st['h2'], pre + 'ffn.0.weight', rows_q, 4 * d, d, bias=pre + 'ffn.0.bias')
+        # (g2 stays intact until the next layer's backward)
+        self._dw_pair((g2, st['f'], pre + 'ffn.2.weight', rows_q, d, 4 * d),
+                      (dpre, st['h2'], pre + 'ffn.0.weight', rows_q, 4 * d, d, None, None, pre + 'ffn.0.bias'))
         dh2 = ws.get('b.dh2', (rows_q, d))
         K.gemm(dpre, P.wT(pre + 'ffn.0.weight', 4 * d, d), dh2, rows_q, d, 4 * d, epi=EPI_BF16)
         dxc = ws.get('b.dxc', (rows_q, d), f32)
@@ -405,7 +427,6 @@ class VAEEngine:
         if st['cross']:
             c = pre + 'cross_attention.'
             rows_c = B * L
-            self._dw(gxc, st['Oc'], c + 'output_linear.weight', rows_q, d, d, bias=c + 'output_linear.bias')
             dOc = ws.get('b.dO', (rows_q, d))
             K.gemm(gxc, P.wT(c + 'output_linear.weight', d, d), dOc, rows_q, d, d, epi=EPI_BF16)
             dqc = ws.get('b.dqc', (rows_q, d))
@@ -417,7 +438,9 @@ class VAEEngine:
                         dout=dOc, sdo=d, bdo=Lq * d, delta=delta, dq_bf=dqc, ldq_bf=d, dk=dkvc, dv=dkvc[:, d:],
                         sdk=2 * d, sdv=2 * d, bdk=L * 2 * d, bdv=L * 2 * d, rot=rot, rot_d=d, o32=st['Oc32'],
                         so32=d, bo32=Lq * d, dq_part=self._dq_part(B, heads, Lq, L, hd))
-            self._dw(dqc, st['hq'], c + 'q_linear.weight', rows_q, d, d, bias=c + 'q_linear.bias')
+            self._dw_pair((gxc, st['Oc'], c + 'output_linear.weight', rows_q, d, d, None, None,
+                           c + 'output_linear.bias'),
+                          (dqc, st['hq'], c + 'q_linear.weight', rows_q, d, d, None, None, c + 'q_linear.bias'))
             dhq = ws.get('b.dhq', (rows_q, d))
             K.gemm(dqc, P.wT(c + 'q_linear.weight', d, d), dhq, rows_q, d, d, epi=EPI_BF16)
             self._dw(dkvc, st['cx'], c + 'k_linear.weight', rows_c, 2 * d, d, bias=c + 'k_linear.bias')
@@ -428,7 +451,7 @@ class VAEEngine:
             self._ln_bwd(pre + 'cross_attn_layer_norm', dhq, st['ln_cross'], rows_q, dxc, dx1, gx1)
             self._ln_bwd(pre + 'context_layer_norm', dcx, st['ln_ctx'], rows_c, dctx, dctx)
         # ---- self / learned-query attention (attention.py:51-105)
-        self._dw(gx1, st['O'], a + 'output_linear.weight', rows_q, d, d, bias=a + 'output_linear.bias')
+        wo_dw = (gx1, st['O'], a + 'output_linear.weight', rows_q, d, d, None, None, a + 'output_linear.bias')
         dO = ws.get('b.dO', (rows_q, d))
         K.gemm(gx1, P.wT(a + 'output_linear.weight', d, d), dO, rows_q, d, d, epi=EPI_BF16)
         delta = ws.get('b.delta', (B, heads, Lq), f32)
@@ -443,7 +466,8 @@ class VAEEngine:
                         bdk=Sx * 2 * d, bdv=Sx * 2 * d, rot=rot, rot_d=d, o32=st['O32'], so32=d, bo32=Lq * d,
                         dq_part=self._dq_part(B, heads, Lq, Sx, hd))
             K.colsum(dq32, B, Lq * d, Lq * d, P.g(a + 'learned_queries').view(-1))
-            self._dw(dkv, st['h'], a + 'k_linear.weight', rows_x, 2 * d, d, bias=a + 'k_linear.bias')
+            self._dw_pair(wo_dw, (dkv, st['h'], a + 'k_linear.weight', rows_x, 2 * d, d, None, None,
+                                  a + 'k_linear.bias'))
             dh = ws.get('b.dh', (rows_x, d))
             K.gemm(dkv, P.wT(a + 'k_linear.weight', 2 * d, d), dh, rows_x, d, 2 * d, epi=EPI_BF16)
         else:
@@ -456,7 +480,8 @@ class VAEEngine:
                         delta=delta, dq_bf=dqkv, ldq_bf=3 * d, dk=dqkv[:, d:], dv=dqkv[:, 2 * d:], sdk=3 * d,
                         sdv=3 * d, bdk=Sx * 3 * d, bdv=Sx * 3 * d, rot=rot, rot_d=d, o32=st['O32'], so32=d,
                         bo32=Lq * d, dq_part=self._dq_part(B, heads, Lq, Sx, hd))
-            self._dw(dqkv, st['h'], a + 'q_linear.weight', rows_x, 3 * d, d, bias=a + 'q_linear.bias')
+            self._dw_pair(wo_dw, (dqkv, st['h'], a + 'q_linear.weight', rows_x, 3 * d, d, None, None,
+                                  a + 'q_linear.bias'))
             dh = ws.get('b.dh', (rows_x, d))
             K.gemm(dqkv, P.wT(a + 'q_linear.weight', 3 * d, d), dh, rows_x, d, 3 * d, epi=EPI_BF16)
         if st['resid']:

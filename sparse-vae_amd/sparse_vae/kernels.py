@@ -24,9 +24,20 @@ def gemm(A, B, C, M, N_, K, *, a_t=False, b_t=False, lda=None, ldb=None, ldc=Non
          rot_d=0, rot_seq=0, labels=None, label_logit=None, batch=1, sA=0, sB=0, sC=0, a_rowsum=None, k_weight=None,
          row_a=None, row_b=None, gather=None, ldg=0):
     """C = epi(alpha * A . B) with A [M,K] (a_t: stored [K,M]) and B [K,N] (b_t: stored [K,N], else [N,K])."""
+    d = _fill_desc(_gemm_desc, A, B, C, M, N_, K, a_t=a_t, b_t=b_t, lda=lda, ldb=ldb, ldc=ldc, epi=epi, bias=bias,
+                   resid=resid, ldr=ldr, aux=aux, ldaux=ldaux, alpha=alpha, splits=splits, drop_p=drop_p, seed=seed,
+                   rot=rot, rot_cols=rot_cols, rot_d=rot_d, rot_seq=rot_seq, labels=labels, label_logit=label_logit,
+                   batch=batch, sA=sA, sB=sB, sC=sC, a_rowsum=a_rowsum, k_weight=k_weight, row_a=row_a, row_b=row_b,
+                   gather=gather, ldg=ldg)
+    check(lib.svae_gemm(ctypes.byref(d), stream()), 'svae_gemm')
+
+
+def _fill_desc(d, A, B, C, M, N_, K, *, a_t=False, b_t=False, lda=None, ldb=None, ldc=None, epi=N.EPI_BF16,
+               bias=None, resid=None, ldr=0, aux=None, ldaux=0, alpha=1.0, splits=1, drop_p=0.0, seed=0, rot=None,
+               rot_cols=0, rot_d=0, rot_seq=0, labels=None, label_logit=None, batch=1, sA=0, sB=0, sC=0,
+               a_rowsum=None, k_weight=None, row_a=None, row_b=None, gather=None, ldg=0):
     _dev(A, B, C)
     assert A.dtype == bf16 and B.dtype == bf16
-    d = _gemm_desc
     d.A, d.B = A.data_ptr(), B.data_ptr()
     d.lda = lda if lda is not None else (M if a_t else K)
     d.ldb = ldb if ldb is not None else (N_ if b_t else K)
@@ -54,7 +65,18 @@ def gemm(A, B, C, M, N_, K, *, a_t=False, b_t=False, lda=None, ldb=None, ldc=Non
     d.k_weight = ptr(k_weight)
     d.row_a, d.row_b = ptr(row_a), ptr(row_b)
     d.gather, d.ldg = ptr(gather), ldg
-    check(lib.svae_gemm(ctypes.byref(d), stream()), 'svae_gemm')
+    return d
+
+
+_pair_desc = (N.GemmDesc(), N.GemmDesc())
+
+
+def gemm_pair(g0, g1):
+    """Two GEMMs in one launch (svae_gemm_pair): g0, g1 are (args, kwargs) of gemm() for two split-K slab weight
+    gradients (a_t, b_t, epi F32_ATOMIC, splits >= 2, aux = slab workspace)."""
+    d0 = _fill_desc(_pair_desc[0], *g0[0], **g0[1])
+    d1 = _fill_desc(_pair_desc[1], *g1[0], **g1[1])
+    check(lib.svae_gemm_pair(ctypes.byref(d0), ctypes.byref(d1), stream()), 'svae_gemm_pair')
 
 
 def auto_splits(M, N_, K, target=512):
@@ -83,6 +105,35 @@ def linear_dw(dY, X, Wgrad, rows, n_out, n_in, ldy=None, ldx=None, bgrad=None):
     slab = _slab_workspace(s * n_out * n_in, dY.device) if s > 1 else None
     gemm(dY, X, Wgrad, n_out, n_in, rows, a_t=True, b_t=True, lda=ldy or n_out, ldb=ldx or n_in, ldc=n_in,
          epi=N.EPI_F32_ATOMIC if s > 1 else N.EPI_F32_ACC, splits=s, a_rowsum=bgrad, aux=slab)
+
+
+def pair_splits(shapes):
+    """Split-K count for two weight gradients launched together ((n_out, n_in, rows) each): one round of <= 256
+    256x256 blocks over both, K-slices >= 512 rows. None when either would not split (then run them apart)."""
+    tiles = sum(-(-m // 256) * -(-n // 256) for m, n, _ in shapes)
+    s = 256 // tiles if tiles else 0
+    s = min([s] + [rows // 512 for _, _, rows in shapes])
+    return s if s >= 2 else None
+
+
+def linear_dw_pair(j0, j1):
+    """Two linear_dw's (each (dY, X, Wgrad, rows, n_out, n_in, ldy, ldx, bgrad)) as one paired launch: each needs
+    only ~half the split-K slices it would take alone to fill the chip (half the slab bytes written and reduced).
+    Falls back to two linear_dw calls for shapes that would not split."""
+    s = pair_splits([(j[4], j[5], j[3]) for j in (j0, j1)])
+    if s is None:
+        linear_dw(*j0[:8], bgrad=j0[8])
+        linear_dw(*j1[:8], bgrad=j1[8])
+        return
+    n0, n1 = s * j0[4] * j0[5], s * j1[4] * j1[5]
+    slab = _slab_workspace(n0 + n1, j0[0].device)
+    gs = []
+    for j, aux in ((j0, slab[:n0]), (j1, slab[n0:n0 + n1])):
+        dY, X, Wg, rows, n_out, n_in, ldy, ldx, bg = j
+        gs.append(((dY, X, Wg, n_out, n_in, rows),
+                   dict(a_t=True, b_t=True, lda=ldy or n_out, ldb=ldx or n_in, ldc=n_in, epi=N.EPI_F32_ATOMIC,
+                        splits=s, a_rowsum=bg, aux=aux)))
+    gemm_pair(*gs)
 
 
 _slabs = {}

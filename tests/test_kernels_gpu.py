@@ -68,6 +68,31 @@ def test_gemm256_split_k_rowsum_exact():
         assert torch.equal(rs, 3 + A.sum(0))
 
 
+@pytest.mark.parametrize('shapes', [((2048, 512, True), (512, 2048, False), 32768),    # FFN pair (8 splits)
+                                    ((512, 512, True), (1536, 512, True), 32768),     # out-proj + QKV (16 splits)
+                                    ((512, 512, True), (1024, 520, True), 4104),      # ragged N / K tail
+                                    ((512, 512, True), (1536, 512, False), 600)])     # too short to split: apart
+def test_linear_dw_pair_exact(shapes):
+    """Two weight gradients in one paired launch (svae_gemm_pair, split-K slabs) equal dY^T X (+ the bias row sums)
+    exactly on integer data, each into its own destination."""
+    (m0, n0, b0), (m1, n1, b1), rows = shapes
+    g = torch.Generator(device=dev).manual_seed(m0 + n1 + rows)
+    jobs, refs = [], []
+    for n_out, n_in, with_bias in ((m0, n0, b0), (m1, n1, b1)):
+        dY = torch.randint(-2, 3, (rows, n_out), device=dev, generator=g).float()
+        X = torch.randint(-2, 3, (rows, n_in), device=dev, generator=g).float()
+        Wg = torch.full((n_out, n_in), 0.5, device=dev)
+        bg = torch.full((n_out,), 1.5, device=dev) if with_bias else None
+        jobs.append((dY.bfloat16(), X.bfloat16(), Wg, rows, n_out, n_in, None, None, bg))
+        refs.append((0.5 + dY.t() @ X, 1.5 + dY.sum(0) if with_bias else None))
+    K.linear_dw_pair(*jobs)
+    torch.cuda.synchronize()
+    for j, (w_ref, b_ref) in zip(jobs, refs):
+        assert torch.equal(j[2], w_ref)
+        if b_ref is not None:
+            assert torch.equal(j[8], b_ref)
+
+
 @pytest.mark.parametrize('M,Nn,Kk', [(300, 256, 192), (4000, 3072, 520)])   # small: 128-tile kernels; big: gemm256
 def test_gemm_epilogues(M, Nn, Kk):
     torch.manual_seed(0)
