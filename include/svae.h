@@ -103,6 +103,17 @@ int svae_layernorm_fwd(const void* x, int32_t x_dtype, const float* w, const flo
 int svae_layernorm_bwd(const void* dy, const void* x, int32_t x_dtype, const float* w, const float* mean,
                        const float* rstd, const float* dres, float* dx, void* dx_bf, float* part,
                        int32_t nblk, int32_t rows, int32_t D, int32_t zero_mod, svae_stream_t stream);
+/* svae_layernorm_bwd for the last LayerNorm of a decoder layer's backward, with the two passes that followed it
+ * fused in: (1) the bf16 copy dx_bf carries the NEXT layer's dropout backward (replaces svae_dropout_bwd_cast of
+ * dx): dx_bf = bf16(keep(bf_seed, (row*D + c)/4) * dx / (1 - bf_drop_p)), the mask of the forward's
+ * SVAE_EPI_DROPOUT_RESID epilogue with the same seed (transformer_layer.py:61, nn.Dropout), and dx_bf = 0 on rows
+ * with row % bf_zero_mod == 0 (bf_zero_mod > 0); bf_drop_p in [0, 1). (2) with zero_mod > 0, the rows it zeroes in
+ * dx are first written to zrow[row / zero_mod] (f32) and zrow_bf (bf16), either may be NULL: the gradient of the
+ * position-0 z splice (transformer_vae.py:89-90; replaces svae_extract_rows + svae_cast_bf16). */
+int svae_layernorm_bwd_drop(const void* dy, const void* x, int32_t x_dtype, const float* w, const float* mean,
+                            const float* rstd, const float* dres, float* dx, void* dx_bf, float* part, int32_t nblk,
+                            int32_t rows, int32_t D, int32_t zero_mod, float bf_drop_p, uint64_t bf_seed,
+                            int32_t bf_zero_mod, float* zrow, void* zrow_bf, svae_stream_t stream);
 int svae_layernorm_nblk(int32_t rows);
 
 /* ---- column sums: out[j] (+)= sum_i in[i*ld + j] (bias grads, LN affine grads, batch sums) ----------

@@ -140,7 +140,12 @@ __device__ __forceinline__ void wait_vmcnt(int n) {
 // XCD-aware block order: hardware dispatch sends block i to XCD i % 8; remap so that logically consecutive blocks
 // (the query tiles, or key blocks, of one (batch, head)) run on the same XCD and share its L2 for K/V (Q/dO).
 // C2 decoder shape (scripts/attn_probe.py): fwd 71.7 -> 67.5 us, bwd 227.6 -> 222.5 us; L = 1024: fwd 208 -> 171 us.
-__device__ __forceinline__ void xcd_block(int& x, int& y, int& z) {
+// Causal work order (lpt != 0): a block's work grows with x (lpt = 1: forward query tiles) or shrinks with x
+// (lpt = 2: backward key blocks). Inside an XCD's range of whole (batch, head) pairs the blocks are then dispatched
+// longest first, x-major per chunk of pairs (the pair-major order put the longest blocks of the last pairs at the
+// end: a tail of idle CUs; list-scheduling model of the C2 decoder shape: backward makespan 29 -> 24 block-tiles,
+// forward 21 -> 17; measured at C2: forward 59.3 -> 52.6 us, backward + delta + dQ reduce 202 -> 182 us).
+__device__ __forceinline__ void xcd_block(int& x, int& y, int& z, int lpt = 0) {
 #ifndef SVAE_ATTN_NO_XCD
   const int gx = gridDim.x, gy = gridDim.y;
   const int n = gx * gy * gridDim.z;
@@ -148,7 +153,19 @@ __device__ __forceinline__ void xcd_block(int& x, int& y, int& z) {
   int l = lin;
   if (n >= 16) {
     const int q = n / 8, r = n % 8, xcd = lin % 8, idx = lin / 8;
-    l = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+    const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q, cnt = xcd < r ? q + 1 : q;
+    l = base + idx;
+    if (lpt && gx > 1 && base % gx == 0 && cnt % gx == 0) {
+      // in chunks of 32 pairs (their K/V, or Q/dO, stay L2-resident while the chunk runs; x-major over all the
+      // XCD's pairs made the B = 256 forward 7 % slower)
+      constexpr int CH = 32;
+      const int np = cnt / gx, c = idx / (CH * gx), local = idx - c * CH * gx, cp = min(CH, np - c * CH);
+      const int rank = local / cp, pair = base / gx + c * CH + (local - rank * cp);
+      x = lpt == 1 ? gx - 1 - rank : rank;
+      y = pair % gy;
+      z = pair / gy;
+      return;
+    }
   }
   x = l % gx;
   y = (l / gx) % gy;
@@ -388,7 +405,7 @@ template <int HDP, int HDC = HDP>
 __global__ __launch_bounds__(256, HDP == 64 ? 3 : 2) void attn_fwd_kernel(AP p) {
   __shared__ __attribute__((aligned(16))) char smem[ATTN_NS * 2 * Tile<HDP>::BYTES + ATTN_NS * 64 * 4];
   int bx, h, b;
-  xcd_block(bx, h, b);
+  xcd_block(bx, h, b, p.causal ? 1 : 0);
   attn_fwd_tile<HDP, HDC>(p, smem, bx, h, b);
 }
 
@@ -491,9 +508,9 @@ __device__ __forceinline__ void attn_bwd_tile(const AP& p, char* smem, int kb, i
   float* part = p.dq_part + ((long long)kb * p.B + b) * p.Lq * p.H * p.hd + (long long)h * p.hd;
   const long long ldp = (long long)p.H * p.hd;
   const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc((void*)part, 0, 0x7FFFFFF0, 0x00020000);
-  // Every wave issues exactly DQ_STORES dQ-partial stores per query tile after the next tile's DMA, so the
-  // end-of-tile wait can leave exactly those in flight (vmcnt retires in issue order).
-  constexpr int DQ_STORES = NT * 4;
+  // Every wave issues exactly DQ_STORES dQ-partial stores (16 B per lane) per query tile after the next tile's DMA,
+  // so the end-of-tile wait can leave exactly those in flight (vmcnt retires in issue order).
+  constexpr int DQ_STORES = NT;
 
   // the row constants (lse, delta) of a query tile ride along with its Q / dO DMA into cst[buf][lse | delta]
   const u32x4 lser = buffer_rsrc(lse, (unsigned)p.Lq * 4u), der = buffer_rsrc(delta, (unsigned)p.Lq * 4u);
@@ -609,7 +626,8 @@ __device__ __forceinline__ void attn_bwd_tile(const AP& p, char* smem, int kb, i
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();   // dS^T complete (a raw barrier: __syncthreads' vmcnt(0) would drain the DMA)
-    // partial dQ[q = qb + 16w + 4g + r][d = 16u + li] = sum over the block's 128 keys of dS[q][key] K[key][d]
+    // partial dQ[q = qb + 16w + li][d = 16u + 4g + r] = sum over the block's 128 keys of dS[q][key] K[key][d]
+    // (K fragment as the MFMA's first operand: a lane holds 4 consecutive dims of one query, one 16-B store each)
     f32x4 dq[NT];
 #pragma unroll
     for (int u = 0; u < NT; ++u) dq[u] = (f32x4){0.f, 0.f, 0.f, 0.f};
@@ -624,21 +642,18 @@ __device__ __forceinline__ void attn_bwd_tile(const AP& p, char* smem, int kb, i
       for (int u = 0; u < NT; ++u) {
         const int uk = 4 * u + (li & 3);
         const bf16x8 bk = cat44(lds_read_tr(Ks + T::uoff(kr, uk)), lds_read_tr(Ks + T::uoff(kr + 4, uk)));
-        dq[u] = mfma16(a, bk, dq[u]);
+        dq[u] = mfma16(bk, a, dq[u]);
       }
     }
     // buffer stores, always DQ_STORES per wave: rows past Lq / dims past hd get an out-of-range offset and are dropped
     // by the range check (no branches, and a fixed count for the wait below)
     {
-      const int qrow = (qb + 16 * w + 4 * g) * (int)ldp + li;
+      const bool qok = qb + 16 * w + li < p.Lq;
+      const int qrow = (qb + 16 * w + li) * (int)ldp + 4 * g;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const bool qok = qb + 16 * w + 4 * g + r < p.Lq;
-#pragma unroll
-        for (int u = 0; u < NT; ++u) {
-          const int off = (qok && 16 * u + li < p.hd) ? (qrow + r * (int)ldp + 16 * u) * 4 : 0x7FFFFFF0;
-          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(dq[u][r]), prs, off, 0, 0);
-        }
+      for (int u = 0; u < NT; ++u) {
+        const int off = (qok && 16 * u + 4 * g < p.hd) ? (qrow + 16 * u) * 4 : 0x7FFFFFF0;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, dq[u]), prs, off, 0, 0);
       }
     }
     // the next tile's DMA (issued before this tile's stores) has landed; the stores stay in flight
@@ -737,7 +752,7 @@ __device__ __forceinline__ void attn_bwd_tile_wide(const AP& p, char* smem, int 
   // On a full query tile (all 64 queries < Lq, hd == HDC) every wave issues exactly DQ_STORES dQ-partial stores
   // after the next tile's DMA, so the end-of-tile wait can leave exactly those in flight (vmcnt retires in
   // issue order); edge tiles wait for everything.
-  constexpr int DQ_STORES = NT * 4;
+  constexpr int DQ_STORES = NT;
 
   // the row constants (lse, delta) of a query tile ride along with its Q / dO DMA into cst[buf][lse | delta]
   const u32x4 lser = buffer_rsrc(lse, (unsigned)p.Lq * 4u), der = buffer_rsrc(delta, (unsigned)p.Lq * 4u);
@@ -832,7 +847,7 @@ __device__ __forceinline__ void attn_bwd_tile_wide(const AP& p, char* smem, int 
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();   // dS^T complete (a raw barrier: __syncthreads' vmcnt(0) would drain the DMA)
-    // partial dQ[q = qb + 16w + 4g + r][d = 16u + li] = sum over the block's 128 keys of dS[q][key] K[key][d]
+    // partial dQ[q = qb + 16w + li][d = 16u + 4g + r] = sum over the block's 128 keys of dS[q][key] K[key][d]
     f32x4 dq[NT];
 #pragma unroll
     for (int u = 0; u < NT; ++u) dq[u] = (f32x4){0.f, 0.f, 0.f, 0.f};
@@ -847,17 +862,16 @@ __device__ __forceinline__ void attn_bwd_tile_wide(const AP& p, char* smem, int 
       for (int u = 0; u < NT; ++u) {
         const int uk = 4 * u + (li & 3);
         const bf16x8 bk = cat44(lds_read_tr(Ks + T::uoff(kr, uk)), lds_read_tr(Ks + T::uoff(kr + 4, uk)));
-        dq[u] = mfma16(a, bk, dq[u]);
+        dq[u] = mfma16(bk, a, dq[u]);
       }
     }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int q = qb + 16 * w + 4 * g + r;
+    {
+      const int q = qb + 16 * w + li;
       if (q < p.Lq) {
 #pragma unroll
         for (int u = 0; u < NT; ++u) {
-          const int d = 16 * u + li;
-          if (d < p.hd) part[(long long)q * ldp + d] = dq[u][r];
+          const int d = 16 * u + 4 * g;
+          if (d < p.hd) *(f32x4*)(part + (long long)q * ldp + d) = dq[u];
         }
       }
     }
@@ -905,7 +919,7 @@ template <int HDP, int HDC = HDP>
 __global__ __launch_bounds__(256, HDP == 64 ? 2 : 1) void attn_bwd_kernel(AP p) {
   __shared__ __attribute__((aligned(16))) char smem[6 * Tile<HDP>::BYTES + 2 * Tile<64>::BYTES + 4 * 64 * 4];
   int kb, h, b;
-  xcd_block(kb, h, b);
+  xcd_block(kb, h, b, p.causal ? 2 : 0);
   if constexpr (HDP == 64) attn_bwd_tile<HDP>(p, smem, kb, h, b);
   else attn_bwd_tile_wide<HDP, HDC>(p, smem, kb, h, b);
 }

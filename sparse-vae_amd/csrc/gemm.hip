@@ -754,6 +754,9 @@ __device__ __forceinline__ void g3_reg_epilogue(const GP& p, const f32x4 (&acc)[
   f32x4 b4[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) b4[j] = *(const f32x4*)(sbias + wc * 64 + j * 16 + 4 * g);
+  f32x4 bl4[4];   // CE_PROB: bias * log2(e)
+#pragma unroll
+  for (int j = 0; j < 4; ++j) bl4[j] = b4[j] * G3_LOG2E;
   // ROTARY: a lane's 4 consecutive columns are two whole (2i, 2i+1) rotary pairs, rotated in registers. The table
   // offsets of its 4 column groups are per tile, the table row (position m mod rot_seq) steps by 16 per fragment
   // row, and row i + 1's (cos, sin) are loaded before row i is rotated (columns >= rot_cols get the identity).
@@ -828,8 +831,11 @@ __device__ __forceinline__ void g3_reg_epilogue(const GP& p, const f32x4 (&acc)[
         }
       } else if constexpr (EPI == SVAE_EPI_CE_PROB) {
         // p = exp(logit - c_row) for rows with a target (0 elsewhere); the f32 values feed the per-tile sums below
+        // exponent in packed f32 pairs: x = acc (alpha log2e) + (bias log2e - off), one v_pk_fma_f32 per two logits
+        // (the row's offset folded into the per-column constants with one v_pk_add_f32 per pair), sums by v_pk_add
         const float off = sstat[1024 + rl] * G3_LOG2E;   // +inf for rows without a target: P = 0
-        float se = 0.f;
+        const f32x2 sa2 = {p.alpha * G3_LOG2E, p.alpha * G3_LOG2E}, noff = {-off, -off};
+        f32x2 se2 = {0.f, 0.f};
         // the column bound is checked per element only on a wave whose 64 columns cross N (a scalar branch between
         // two copies: if-converted into the one loop it cost 4 VALU per element, as much as the exp's arithmetic)
         auto body = [&](auto rag) {
@@ -839,21 +845,27 @@ __device__ __forceinline__ void g3_reg_epilogue(const GP& p, const f32x4 (&acc)[
 #pragma unroll
             for (int h = 0; h < 2; ++h)
 #pragma unroll
-              for (int e = 0; e < 4; ++e) {
+              for (int e = 0; e < 4; e += 2) {
                 const int j = 2 * jp + h;
-                float x = __builtin_amdgcn_exp2f(fminf(fmaf(v[j][e], G3_LOG2E, -off), 127.0f));
+                const f32x2 a2 = {acc[i][j][e], acc[i][j][e + 1]};
+                const f32x2 c2 = (f32x2){bl4[j][e], bl4[j][e + 1]} + noff;
+                const f32x2 t2 = a2 * sa2 + c2;
+                f32x2 x = {__builtin_amdgcn_exp2f(fminf(t2[0], 127.0f)), __builtin_amdgcn_exp2f(fminf(t2[1], 127.0f))};
                 if constexpr (decltype(rag)::value) {
-                  if (n0 + wc * 64 + j * 16 + 4 * g + e >= p.N) x = 0.f;
+                  const int n = n0 + wc * 64 + j * 16 + 4 * g + e;
+                  if (n >= p.N) x[0] = 0.f;
+                  if (n + 1 >= p.N) x[1] = 0.f;
                 }
-                x2[h][e] = x;
-                se += x;
+                x2[h][e] = x[0];
+                x2[h][e + 1] = x[1];
+                se2 += x;
               }
             store_pair_bf16<SVAE_P_NT != 0>(crow, 32 * jp, row_ok ? nleft : 0, x2[0], x2[1], g);
           }
         };
         if (__builtin_amdgcn_readfirstlane((int)(n0 + wc * 64 + 64 > p.N))) body(BoolC<true>{});
         else body(BoolC<false>{});
-        se = sum_x16_x32(se);
+        float se = sum_x16_x32(se2[0] + se2[1]);
         if (g == 0) sstat[rl * 4 + wc] = se;
       } else if (EPI != SVAE_EPI_CE_STATS || p.C) {   // CE statistics with C == nullptr: no logits stored
 #pragma unroll

@@ -11,7 +11,8 @@ using namespace svae;
 
 namespace {
 
-constexpr int MAXV = 4;  // float4 chunks per lane: D <= 64 * 4 * MAXV = 1024
+// MAXV = float4 chunks per lane: D <= 64 * 4 * MAXV (instantiated for 2, 3, 4: D <= 512 / 768 / 1024, so the
+// per-lane arrays, and the registers, fit the model width: the D <= 1024 copy held 112-136 VGPRs, 3-4 waves / SIMD)
 
 template <typename T>
 __device__ __forceinline__ f32x4 load4(const T* p);
@@ -26,7 +27,7 @@ __device__ __forceinline__ void store4_bf(bf16* p, f32x4 v) {
   *(bf16x4*)p = (bf16x4){f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
 }
 
-template <typename T>
+template <typename T, int MAXV>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, const float* __restrict__ w,
                                                      const float* __restrict__ b, bf16* __restrict__ y,
                                                      float* __restrict__ mean_out, float* __restrict__ rstd_out,
@@ -68,13 +69,15 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, co
   if (lane == 0) { mean_out[row] = mean; rstd_out[row] = rstd; }
 }
 
-template <typename T>
+template <typename T, int MAXV>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16* __restrict__ dy, const T* __restrict__ x,
                                                      const float* __restrict__ w, const float* __restrict__ mean_in,
                                                      const float* __restrict__ rstd_in, const float* __restrict__ dres,
                                                      float* __restrict__ dx, bf16* __restrict__ dx_bf,
-                                                     float* __restrict__ part, int rows, int D, int zero_mod) {
-  __shared__ float red[4][2][1024];
+                                                     float* __restrict__ part, int rows, int D, int zero_mod,
+                                                     float bf_drop_p, unsigned long long bf_seed, int bf_zero_mod,
+                                                     float* __restrict__ zrow, bf16* __restrict__ zrow_bf) {
+  __shared__ float red[4][2][256 * MAXV];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   f32x4 adw[MAXV], adb[MAXV];
 #pragma unroll
@@ -104,6 +107,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16* __restrict__ dy
     }
     const float m1 = wave_sum(s1) / D, m2 = wave_sum(s2) / D;
     const bool zero = zero_mod > 0 && (row % zero_mod) == 0;
+    const bool bf_zero = bf_zero_mod > 0 && (row % bf_zero_mod) == 0;
 #pragma unroll
     for (int j = 0; j < MAXV; ++j) {
       const int c = (lane + 64 * j) * 4;
@@ -116,9 +120,25 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16* __restrict__ dy
 #pragma unroll
           for (int e = 0; e < 4; ++e) o[e] += r[e];
         }
-        if (zero) o = (f32x4){0.f, 0.f, 0.f, 0.f};
+        if (zero) {   // (the row's value first goes to zrow[row / zero_mod]: the z splice's gradient)
+          if (zrow) *(f32x4*)(zrow + (long long)(row / zero_mod) * D + c) = o;
+          if (zrow_bf) store4_bf(zrow_bf + (long long)(row / zero_mod) * D + c, o);
+          o = (f32x4){0.f, 0.f, 0.f, 0.f};
+        }
         *(f32x4*)(dx + base + c) = o;
-        if (dx_bf) store4_bf(dx_bf + base + c, o);
+        if (dx_bf) {
+          // the bf16 copy may carry the next consumer's dropout backward (mask of the forward's DROPOUT_RESID
+          // epilogue: counter (row * D + c) / 4 of bf_seed) and its position-0 zeroing
+          if (bf_zero) o = (f32x4){0.f, 0.f, 0.f, 0.f};
+          else if (bf_drop_p > 0.f) {
+            float u[4];
+            rand_uniform4(bf_seed, ((unsigned long long)row * D + c) >> 2, u);
+            const float sc = 1.0f / (1.0f - bf_drop_p);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[e] = u[e] >= bf_drop_p ? o[e] * sc : 0.f;
+          }
+          store4_bf(dx_bf + base + c, o);
+        }
       }
     }
   }
@@ -139,26 +159,35 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16* __restrict__ dy
   }
 }
 
-// out[j] += sum_i in[i*ld + j]; block = 4 row-waves x 64 lanes x 4 columns; grid (colblocks, rowsplits).
+// out[j] += sum_i in[i*ld + j]. Block = 64 columns (16 column threads x 4) x 16 row threads, grid (column blocks,
+// row splits): every thread keeps 8 rows' loads in flight, the block reduces its 16 row threads in LDS and adds
+// its 64 sums with one atomic each. (Row-wave blocks with a serial row loop ran 7.9 us on the LayerNorm slabs'
+// 1024 x 1024 floats; with 4x the splits, 8.6 us: same-address atomics from many blocks serialise.)
 template <typename T>
 __global__ __launch_bounds__(256) void colsum_kernel(const T* __restrict__ in, int rows, int cols, long long ld,
                                                      float* __restrict__ out, int rows_per_split) {
-  __shared__ f32x4 red[4][64];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int c = (blockIdx.x * 64 + lane) * 4;
+  __shared__ f32x4 red[16][17];
+  const int ct = threadIdx.x & 15, rt = threadIdx.x >> 4;
+  const int c = (blockIdx.x * 16 + ct) * 4;
   const int r0 = blockIdx.y * rows_per_split;
   const int r1 = min(rows, r0 + rows_per_split);
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   if (c < cols) {
-    for (int r = r0 + wave; r < r1; r += 4) {
-      const f32x4 v = load4<T>(in + (long long)r * ld + c);
-      acc += v;
+    int r = r0 + rt;
+    for (; r + 112 < r1; r += 128) {
+      f32x4 v[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = load4<T>(in + (long long)(r + 16 * i) * ld + c);
+      acc += ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
     }
+    for (; r < r1; r += 16) acc += load4<T>(in + (long long)r * ld + c);
   }
-  red[wave][lane] = acc;
+  red[rt][ct] = acc;
   __syncthreads();
-  if (wave == 0 && c < cols) {
-    const f32x4 s = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+  if (threadIdx.x < 16 && c < cols) {
+    f32x4 s = red[0][ct];
+#pragma unroll
+    for (int i = 1; i < 16; ++i) s += red[i][ct];
 #pragma unroll
     for (int e = 0; e < 4; ++e) atomicAdd(out + c + e, s[e]);
   }
@@ -171,10 +200,19 @@ SVAE_EXPORT int svae_layernorm_fwd(const void* x, int32_t x_dtype, const float* 
   if (!x || !w || !b || !y || !mean || !rstd || rows <= 0 || D <= 0 || D % 4 || D > 1024) return SVAE_EINVAL;
   dim3 grid((rows + 3) / 4);
   hipStream_t s = (hipStream_t)stream;
-  if (x_dtype == 0)
-    hipLaunchKernelGGL(ln_fwd_kernel<float>, grid, dim3(256), 0, s, (const float*)x, w, b, (bf16*)y, mean, rstd, rows, D);
-  else
-    hipLaunchKernelGGL(ln_fwd_kernel<bf16>, grid, dim3(256), 0, s, (const bf16*)x, w, b, (bf16*)y, mean, rstd, rows, D);
+#define SVAE_LN_FWD(MV)                                                                                            \
+  do {                                                                                                             \
+    if (x_dtype == 0)                                                                                              \
+      hipLaunchKernelGGL((ln_fwd_kernel<float, MV>), grid, dim3(256), 0, s, (const float*)x, w, b, (bf16*)y, mean, \
+                         rstd, rows, D);                                                                           \
+    else                                                                                                           \
+      hipLaunchKernelGGL((ln_fwd_kernel<bf16, MV>), grid, dim3(256), 0, s, (const bf16*)x, w, b, (bf16*)y, mean,   \
+                         rstd, rows, D);                                                                           \
+  } while (0)
+  if (D <= 512) SVAE_LN_FWD(2);
+  else if (D <= 768) SVAE_LN_FWD(3);
+  else SVAE_LN_FWD(4);
+#undef SVAE_LN_FWD
   SVAE_LAUNCH_CHECK();
   return SVAE_OK;
 }
@@ -184,20 +222,40 @@ SVAE_EXPORT int svae_layernorm_nblk(int32_t rows) {
   return n < 1024 ? n : 1024;
 }
 
+SVAE_EXPORT int svae_layernorm_bwd_drop(const void* dy, const void* x, int32_t x_dtype, const float* w,
+                                        const float* mean, const float* rstd, const float* dres, float* dx, void* dx_bf,
+                                        float* part, int32_t nblk, int32_t rows, int32_t D, int32_t zero_mod,
+                                        float bf_drop_p, uint64_t bf_seed, int32_t bf_zero_mod, float* zrow,
+                                        void* zrow_bf, svae_stream_t stream) {
+  if (!dy || !x || !w || !mean || !rstd || !dx || !part || rows <= 0 || D <= 0 || D % 4 || D > 1024 || nblk <= 0)
+    return SVAE_EINVAL;
+  if (bf_drop_p < 0.f || bf_drop_p >= 1.f || ((bf_drop_p > 0.f || bf_zero_mod > 0) && !dx_bf)) return SVAE_EINVAL;
+  if ((zrow || zrow_bf) && zero_mod <= 0) return SVAE_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+#define SVAE_LN_BWD(MV)                                                                                            \
+  do {                                                                                                             \
+    if (x_dtype == 0)                                                                                              \
+      hipLaunchKernelGGL((ln_bwd_kernel<float, MV>), dim3(nblk), dim3(256), 0, s, (const bf16*)dy, (const float*)x, \
+                         w, mean, rstd, dres, dx, (bf16*)dx_bf, part, rows, D, zero_mod, bf_drop_p,                 \
+                         (unsigned long long)bf_seed, bf_zero_mod, zrow, (bf16*)zrow_bf);                           \
+    else                                                                                                           \
+      hipLaunchKernelGGL((ln_bwd_kernel<bf16, MV>), dim3(nblk), dim3(256), 0, s, (const bf16*)dy, (const bf16*)x,   \
+                         w, mean, rstd, dres, dx, (bf16*)dx_bf, part, rows, D, zero_mod, bf_drop_p,                 \
+                         (unsigned long long)bf_seed, bf_zero_mod, zrow, (bf16*)zrow_bf);                           \
+  } while (0)
+  if (D <= 512) SVAE_LN_BWD(2);
+  else if (D <= 768) SVAE_LN_BWD(3);
+  else SVAE_LN_BWD(4);
+#undef SVAE_LN_BWD
+  SVAE_LAUNCH_CHECK();
+  return SVAE_OK;
+}
+
 SVAE_EXPORT int svae_layernorm_bwd(const void* dy, const void* x, int32_t x_dtype, const float* w, const float* mean,
                                    const float* rstd, const float* dres, float* dx, void* dx_bf, float* part,
                                    int32_t nblk, int32_t rows, int32_t D, int32_t zero_mod, svae_stream_t stream) {
-  if (!dy || !x || !w || !mean || !rstd || !dx || !part || rows <= 0 || D <= 0 || D % 4 || D > 1024 || nblk <= 0)
-    return SVAE_EINVAL;
-  hipStream_t s = (hipStream_t)stream;
-  if (x_dtype == 0)
-    hipLaunchKernelGGL(ln_bwd_kernel<float>, dim3(nblk), dim3(256), 0, s, (const bf16*)dy, (const float*)x, w, mean,
-                       rstd, dres, dx, (bf16*)dx_bf, part, rows, D, zero_mod);
-  else
-    hipLaunchKernelGGL(ln_bwd_kernel<bf16>, dim3(nblk), dim3(256), 0, s, (const bf16*)dy, (const bf16*)x, w, mean,
-                       rstd, dres, dx, (bf16*)dx_bf, part, rows, D, zero_mod);
-  SVAE_LAUNCH_CHECK();
-  return SVAE_OK;
+  return svae_layernorm_bwd_drop(dy, x, x_dtype, w, mean, rstd, dres, dx, dx_bf, part, nblk, rows, D, zero_mod, 0.f, 0,
+                                 0, nullptr, nullptr, stream);
 }
 
 SVAE_EXPORT int svae_colsum(const void* in, int32_t in_dtype, int32_t rows, int32_t cols, int64_t ld, float* out,
@@ -205,9 +263,10 @@ SVAE_EXPORT int svae_colsum(const void* in, int32_t in_dtype, int32_t rows, int3
   if (!in || !out || rows <= 0 || cols <= 0 || cols % 4 || ld % 4) return SVAE_EINVAL;
   hipStream_t s = (hipStream_t)stream;
   if (!accumulate && hipMemsetAsync(out, 0, sizeof(float) * cols, s) != hipSuccess) return SVAE_ELAUNCH;
-  const int colblocks = (cols + 255) / 256;
-  int splits = (512 + colblocks - 1) / colblocks;
-  int max_splits = (rows + 63) / 64;
+  const int colblocks = (cols + 63) / 64;
+  // ~256 blocks, >= 128 rows (one unrolled group of loads per thread) per split
+  int splits = (256 + colblocks - 1) / colblocks;
+  int max_splits = (rows + 127) / 128;
   if (splits > max_splits) splits = max_splits;
   if (splits < 1) splits = 1;
   const int rps = (rows + splits - 1) / splits;

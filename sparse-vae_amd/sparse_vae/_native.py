@@ -66,6 +66,9 @@ _SIGS = {
                            c_void_p],
     'svae_layernorm_bwd': [c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                            c_void_p, c_int32, c_int32, c_int32, c_int32, c_void_p],
+    'svae_layernorm_bwd_drop': [c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                c_void_p, c_void_p, c_int32, c_int32, c_int32, c_int32, c_float, c_uint64, c_int32,
+                                c_void_p, c_void_p, c_void_p],
     'svae_layernorm_nblk': [c_int32],
     'svae_colsum': [c_void_p, c_int32, c_int32, c_int32, c_int64, c_void_p, c_int32, c_void_p],
     'svae_attn_fwd': [ctypes.POINTER(AttnDesc), c_void_p],

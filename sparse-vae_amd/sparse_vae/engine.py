@@ -261,12 +261,13 @@ class VAEEngine:
         K.layernorm_fwd(x, self.P.f(name + '.weight'), self.P.f(name + '.bias'), y, mean, rstd, rows, D)
         return y, (x, mean, rstd)
 
-    def _ln_bwd(self, name, dy, st, rows, dres, dx, dx_bf=None):
+    def _ln_bwd(self, name, dy, st, rows, dres, dx, dx_bf=None, bf_drop=None, zsplice=None):
         x, mean, rstd = st
         D = self.d
         part = self.ws.get('ln.part', (1024 * 2 * D,), f32)
         wg = self.P.grad[self.P.offsets[name + '.weight'][0]:][:2 * D]   # [weight | bias] grads (adjacent)
-        K.layernorm_bwd(dy, x, self.P.f(name + '.weight'), mean, rstd, dres, dx, dx_bf, wg, rows, D, part)
+        K.layernorm_bwd(dy, x, self.P.f(name + '.weight'), mean, rstd, dres, dx, dx_bf, wg, rows, D, part,
+                        bf_drop=bf_drop, zsplice=zsplice)
 
     def _dw(self, dY, X, wname, rows, n_out, n_in, ldy=None, ldx=None, bias=None, on_side=True):
         bg = None
@@ -399,10 +400,15 @@ class VAEEngine:
         t = self.ws.bufs.get('b.dqpart')
         return t if t is not None and t.numel() >= n else self.ws.get('b.dqpart', (n,), f32)
 
-    def layer_bwd(self, st, dout, dx_out, *, dx_accumulate=False, dctx=None):
+    def layer_bwd(self, st, dout, dx_out, *, dx_accumulate=False, dctx=None, g2_ready=False, next_drop=None,
+                  zsplice=None):
         """Backward of layer_fwd. dout f32 [B*Lq, d] (consumed as scratch). Writes d x into dx_out
         (accumulating into it when dx_accumulate and the layer has no residual); cross-attention context
-        gradients accumulate into dctx."""
+        gradients accumulate into dctx. g2_ready: the dropout-masked bf16 dout is already in the 'b.g2' buffer
+        (written by the previous layer_bwd's last LayerNorm backward); next_drop = (p, seed, zero_mod): this
+        layer's last LayerNorm backward writes that buffer for the next layer_bwd (residual layers only).
+        zsplice = (L, zrow, zrow_bf): that LayerNorm backward also moves rows r % L == 0 of dx_out into zrow / zrow_bf
+        and zeroes them (the z splice's gradient, extract_rows + cast_bf16)."""
         d, ws, P = self.d, self.ws, self.P
         pre, B, Sx, L, Lq = st['pre'], st['B'], st['Sx'], st['L'], st['Lq']
         heads, hd = st['heads'], st['hd']
@@ -411,7 +417,8 @@ class VAEEngine:
         a = pre + 'attention.'
         # ---- FFN (transformer_layer.py:56-61)
         g2 = ws.get('b.g2', (rows_q, d))
-        K.dropout_bwd_cast(dout, g2, st['drop_p'], st['seed'], rows_q, d)
+        if not g2_ready:
+            K.dropout_bwd_cast(dout, g2, st['drop_p'], st['seed'], rows_q, d)
         dpre = ws.get('b.dpre', (rows_q, 4 * d))
         K.gemm(g2, P.wT(pre + 'ffn.2.weight', d, 4 * d), dpre, rows_q, 4 * d, d, epi=EPI_GELU_BWD, aux=st['gprime'],
                ldaux=4 * d)
@@ -485,7 +492,10 @@ class VAEEngine:
             dh = ws.get('b.dh', (rows_x, d))
             K.gemm(dqkv, P.wT(a + 'q_linear.weight', 3 * d, d), dh, rows_x, d, 3 * d, epi=EPI_BF16)
         if st['resid']:
-            self._ln_bwd(pre + 'attn_layer_norm', dh, st['ln_a'], rows_x, dx1, dx_out)
+            # the next layer's dropout-masked bf16 dout and the z splice's rows ride along (no separate passes)
+            self._ln_bwd(pre + 'attn_layer_norm', dh, st['ln_a'], rows_x, dx1, dx_out,
+                         dx_bf=ws.get('b.g2', (rows_x, d)) if next_drop is not None else None, bf_drop=next_drop,
+                         zsplice=zsplice)
             if dx_accumulate:
                 raise NotImplementedError('residual + accumulate is handled by the caller')
         else:
@@ -856,14 +866,25 @@ class VAEEngine:
         dzh = ws.get('b.dzh', (B, d), f32)
         dzh_bf = ws.get('b.dzh_bf', (B, d))
         dx_prev = ws.get('b.dx_prev', (T, d), f32)
+        g2_ready = False
         for i in reversed(range(hp.num_layers)):
             st = sv['dec_layers'][i]
-            self.layer_bwd(st, dx, dx_prev)
-            # position-0 splice: its gradient feeds z_projections[i]; earlier layers see zero there
-            K.extract_rows(dx_prev, d, T, L, d, dzh)
-            K.cast_bf16(dzh, dzh_bf)
-            self._dw(dzh_bf, sv['z_bf'], f'z_projections.{i}.weight', B, d, Z)
-            self._db(dzh, f'z_projections.{i}.bias', B, d)
+            # the next (lower) layer's FFN dropout backward + position-0 zeroing (extract_rows below) fused into this
+            # layer's last LayerNorm backward (same rows: a residual layer maps B*L rows to B*L rows)
+            nd = None
+            if i > 0 and st['resid'] and sv['dec_layers'][i - 1]['rows_q'] == T:
+                nst = sv['dec_layers'][i - 1]
+                nd = (nst['drop_p'], nst['seed'], L)
+            # position-0 splice: its gradient feeds z_projections[i]; earlier layers see zero there (moved out of dx by
+            # the layer's last LayerNorm backward when it is a residual layer)
+            zs = (L, None, dzh_bf) if st['resid'] and st['rows_q'] == T else None
+            self.layer_bwd(st, dx, dx_prev, g2_ready=g2_ready, next_drop=nd, zsplice=zs)
+            g2_ready = nd is not None
+            if zs is None:
+                K.extract_rows(dx_prev, d, T, L, d, dzh)
+                K.cast_bf16(dzh, dzh_bf)
+            # (bias gradient = the dW GEMM's fused row sums of dzh)
+            self._dw(dzh_bf, sv['z_bf'], f'z_projections.{i}.weight', B, d, Z, bias=f'z_projections.{i}.bias')
             # dz += dzh . W_i: a 64 x 64 output over K = d -> split K over blocks (f32 atomics into dz)
             K.gemm(dzh_bf, P.w(f'z_projections.{i}.weight'), dz, B, Z, d, b_t=True, epi=EPI_F32_ATOMIC,
                    splits=max(1, min(8, d // 64)))

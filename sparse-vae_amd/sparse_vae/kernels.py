@@ -154,13 +154,25 @@ def layernorm_fwd(x, w, b, y, mean, rstd, rows, D):
                                  mean.data_ptr(), rstd.data_ptr(), rows, D, stream()), 'svae_layernorm_fwd')
 
 
-def layernorm_bwd(dy, x, w, mean, rstd, dres, dx, dx_bf, wgrad2, rows, D, part_ws):
-    """dx = dres + LN'(dy); wgrad2 (the adjacent [weight | bias] grads, 2D floats) += sum of affine grads."""
+def layernorm_bwd(dy, x, w, mean, rstd, dres, dx, dx_bf, wgrad2, rows, D, part_ws, bf_drop=None, zsplice=None):
+    """dx = dres + LN'(dy); wgrad2 (the adjacent [weight | bias] grads, 2D floats) += sum of affine grads.
+    bf_drop = (p, seed, zero_mod): the bf16 copy dx_bf carries the next consumer's dropout backward and position-0
+    zeroing (svae_layernorm_bwd_drop), replacing a dropout_bwd_cast pass over dx. zsplice = (L, zrow f32 | None,
+    zrow_bf bf16 | None): rows r % L == 0 of dx go to zrow[r / L] / zrow_bf and are zeroed in dx (extract_rows)."""
     nblk = lib.svae_layernorm_nblk(rows)
     part = part_ws[: nblk * 2 * D]
-    check(lib.svae_layernorm_bwd(dy.data_ptr(), x.data_ptr(), 0 if x.dtype == f32 else 1, w.data_ptr(),
-                                 mean.data_ptr(), rstd.data_ptr(), ptr(dres), dx.data_ptr(), ptr(dx_bf),
-                                 part.data_ptr(), nblk, rows, D, 0, stream()), 'svae_layernorm_bwd')
+    if bf_drop is None and zsplice is None:
+        check(lib.svae_layernorm_bwd(dy.data_ptr(), x.data_ptr(), 0 if x.dtype == f32 else 1, w.data_ptr(),
+                                     mean.data_ptr(), rstd.data_ptr(), ptr(dres), dx.data_ptr(), ptr(dx_bf),
+                                     part.data_ptr(), nblk, rows, D, 0, stream()), 'svae_layernorm_bwd')
+    else:
+        p, seed, zmod = bf_drop if bf_drop is not None else (0.0, 0, 0)
+        zm, zrow, zrow_bf = zsplice if zsplice is not None else (0, None, None)
+        check(lib.svae_layernorm_bwd_drop(dy.data_ptr(), x.data_ptr(), 0 if x.dtype == f32 else 1, w.data_ptr(),
+                                          mean.data_ptr(), rstd.data_ptr(), ptr(dres), dx.data_ptr(), ptr(dx_bf),
+                                          part.data_ptr(), nblk, rows, D, int(zm), float(p),
+                                          int(seed) & 0xFFFFFFFFFFFFFFFF, int(zmod), ptr(zrow), ptr(zrow_bf),
+                                          stream()), 'svae_layernorm_bwd_drop')
     colsum(part, nblk, 2 * D, 2 * D, wgrad2, accumulate=True)
 
 

@@ -217,6 +217,60 @@ def test_layernorm(D, xdt):
     assert _rel(wg[:D], wr.grad) < 1e-4 and _rel(wg[D:], br.grad) < 1e-4
 
 
+@pytest.mark.parametrize('p', [0.0, 0.1, 0.5])
+def test_layernorm_bwd_fused_dropout_cast(p):
+    # the bf16 copy with the next layer's dropout backward + position-0 zeroing equals the unfused sequence
+    # (layernorm_bwd, then dropout_bwd_cast of dx with rows % L == 0 zeroed) bit for bit; dx itself is unchanged
+    D, L, rows = 512, 64, 64 * 7
+    torch.manual_seed(11)
+    x = torch.randn(rows, D, device=dev) * 2 + 0.5
+    w = torch.randn(D, device=dev) * 0.1 + 1
+    bb = torch.randn(D, device=dev) * 0.1
+    y = torch.empty(rows, D, device=dev, dtype=torch.bfloat16)
+    mean, rstd = torch.empty(rows, device=dev), torch.empty(rows, device=dev)
+    K.layernorm_fwd(x, w, bb, y, mean, rstd, rows, D)
+    dy = torch.randn(rows, D, device=dev).bfloat16()
+    dres = torch.randn(rows, D, device=dev)
+    part = torch.empty(1024 * 2 * D, device=dev)
+    seed = 0x9E3779B97F4A7C15
+    dx0, wg0 = torch.empty(rows, D, device=dev), torch.zeros(2 * D, device=dev)
+    K.layernorm_bwd(dy, x, w, mean, rstd, dres, dx0, None, wg0, rows, D, part)
+    ref = torch.empty(rows, D, device=dev, dtype=torch.bfloat16)
+    dxz = dx0.clone()
+    dxz[::L] = 0
+    K.dropout_bwd_cast(dxz, ref, p, seed, rows, D)
+    dx1, wg1 = torch.empty(rows, D, device=dev), torch.zeros(2 * D, device=dev)
+    got = torch.empty(rows, D, device=dev, dtype=torch.bfloat16)
+    K.layernorm_bwd(dy, x, w, mean, rstd, dres, dx1, got, wg1, rows, D, part, bf_drop=(p, seed, L))
+    torch.cuda.synchronize()
+    assert torch.equal(dx1, dx0) and torch.equal(got, ref)
+    assert torch.allclose(wg1, wg0, rtol=1e-6, atol=1e-6)
+    if p > 0:
+        assert (got.float() == 0).float().mean().item() > p * 0.8
+    # + the z splice: rows r % L == 0 move to zrow / zrow_bf and are zeroed in dx (extract_rows + cast_bf16)
+    zr, zb = torch.full((rows // L, D), 7.0, device=dev), torch.zeros(rows // L, D, device=dev, dtype=torch.bfloat16)
+    dx2, got2 = torch.empty(rows, D, device=dev), torch.empty(rows, D, device=dev, dtype=torch.bfloat16)
+    K.layernorm_bwd(dy, x, w, mean, rstd, dres, dx2, got2, torch.zeros(2 * D, device=dev), rows, D, part,
+                    bf_drop=(p, seed, L), zsplice=(L, zr, zb))
+    torch.cuda.synchronize()
+    assert torch.equal(zr, dx0[::L]) and torch.equal(zb, dx0[::L].bfloat16())
+    assert torch.equal(dx2, dxz) and torch.equal(got2, ref)
+
+
+@pytest.mark.parametrize('rows,cols,ld,dt', [(1024, 1024, 1024, torch.float32), (1000, 512, 520, torch.float32),
+                                            (37, 1024, 1024, torch.float32), (5, 8, 8, torch.float32),
+                                            (32768, 512, 512, torch.bfloat16), (4093, 2048, 2048, torch.bfloat16)])
+def test_colsum(rows, cols, ld, dt):
+    # column sums (bias / LayerNorm-affine gradients): unrolled row groups + ragged tails, accumulate into out
+    torch.manual_seed(rows + cols)
+    x = torch.randn(rows, ld, device=dev).to(dt)
+    out = torch.randn(cols, device=dev)
+    ref = out + x[:, :cols].double().sum(0).float()
+    K.colsum(x, rows, cols, ld, out, accumulate=True)
+    torch.cuda.synchronize()
+    assert _rel(out, ref) < 1e-5
+
+
 def _attn_ref(q, k, v, pad, causal, scale):
     s = q @ k.transpose(-1, -2) * scale
     mask = None
