@@ -252,6 +252,12 @@ int svae_transpose_blocks(const void* src, void* dst, const int64_t* table, int3
  * (the position-0 gradient of the z-projection splice, transformer_vae.py:89-90). */
 int svae_extract_rows(float* x, int64_t ld, int32_t rows, int32_t mod, int32_t D, float* out,
                       svae_stream_t stream);
+/* z_projections[i] backward (transformer_vae.py:89-90, x[:, 0] = nn.Linear(Z, d)(z)) from the position-0 gradient
+ * g f32 [B][d]: dW f32 [d][Z] += g^T z, db f32 [d] += sum_b g[b], dz f32 [B][Z] += g W, with z bf16 [B][Z] and
+ * W bf16 [d][Z] the forward's operands; f32 accumulation in a fixed order (deterministic), one launch (replaces the
+ * dW GEMM with fused bias row sums and the split-K dz GEMM of a decoder layer). */
+int svae_zproj_bwd(const float* g, const void* z, const void* W, float* dW, float* db, float* dz, int32_t B,
+                   int32_t d, int32_t Z, svae_stream_t stream);
 
 /* ---- optimiser (RAdam, rectified_adam.py:16-88; clip_grad_norm_, language_model.py:120-122) -------
  * sumsq: partial sums of g^2 over n elements into part[nblk]; radam: reads part to form the global

@@ -842,6 +842,59 @@ SVAE_EXPORT int svae_transpose_blocks(const void* src, void* dst, const int64_t*
   return SVAE_OK;
 }
 
+// z_projections[i] backward (svae.h): blocks [0, nbw) own 4 rows m of dW (one wave per row, lanes over n; the
+// wave's lane-strided sum over b gives db[m]); blocks [nbw, nbw + B) own one row b of dz (4 waves over quarters of m,
+// combined in LDS in a fixed order). Every output has one writer: no atomics.
+__global__ __launch_bounds__(256) void zproj_bwd_kernel(const float* __restrict__ g, const bf16* __restrict__ z,
+                                                        const bf16* __restrict__ W, float* __restrict__ dW,
+                                                        float* __restrict__ db, float* __restrict__ dz, int B, int d,
+                                                        int Z, int nbw) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if ((int)blockIdx.x < nbw) {
+    const int m = blockIdx.x * 4 + wave;
+    if (m >= d) return;   // (a whole wave; this branch has no barrier)
+    for (int n0 = 0; n0 < Z; n0 += 64) {
+      const int n = n0 + lane;
+      if (n < Z) {
+        float acc = 0.f;
+#pragma unroll 8
+        for (int b = 0; b < B; ++b) acc = fmaf(g[(long long)b * d + m], (float)z[(long long)b * Z + n], acc);
+        dW[(long long)m * Z + n] += acc;
+      }
+    }
+    float s = 0.f;
+    for (int b = lane; b < B; b += 64) s += g[(long long)b * d + m];
+    s = wave_sum(s);
+    if (lane == 0) db[m] += s;
+  } else {
+    const int b = blockIdx.x - nbw;
+    const float* gb = g + (long long)b * d;
+    for (int n0 = 0; n0 < Z; n0 += 64) {
+      const int n = n0 + lane;
+      float acc = 0.f;
+      if (n < Z) {
+#pragma unroll 8
+        for (int m = wave; m < d; m += 4) acc = fmaf(gb[m], (float)W[(long long)m * Z + n], acc);
+      }
+      red[wave][lane] = acc;
+      __syncthreads();
+      if (wave == 0 && n < Z) dz[(long long)b * Z + n] += (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+      __syncthreads();
+    }
+  }
+}
+
+SVAE_EXPORT int svae_zproj_bwd(const float* g, const void* z, const void* W, float* dW, float* db, float* dz,
+                               int32_t B, int32_t d, int32_t Z, svae_stream_t stream) {
+  if (!g || !z || !W || !dW || !db || !dz || B <= 0 || d <= 0 || Z <= 0) return SVAE_EINVAL;
+  const int nbw = (d + 3) / 4;
+  hipLaunchKernelGGL(zproj_bwd_kernel, dim3(nbw + B), dim3(256), 0, (hipStream_t)stream, g, (const bf16*)z,
+                     (const bf16*)W, dW, db, dz, B, d, Z, nbw);
+  SVAE_LAUNCH_CHECK();
+  return SVAE_OK;
+}
+
 SVAE_EXPORT int svae_extract_rows(float* x, int64_t ld, int32_t rows, int32_t mod, int32_t D, float* out,
                                   svae_stream_t stream) {
   if (!x || !out || rows <= 0 || mod <= 0 || rows % mod || D <= 0) return SVAE_EINVAL;

@@ -100,6 +100,7 @@ _SIGS = {
     'svae_gelu_bwd': [c_void_p, c_void_p, c_void_p, c_int64, c_void_p],
     'svae_cast_bf16': [c_void_p, c_void_p, c_int64, c_void_p],
     'svae_extract_rows': [c_void_p, c_int64, c_int32, c_int32, c_int32, c_void_p, c_void_p],
+    'svae_zproj_bwd': [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_int32, c_void_p],
     'svae_sumsq': [c_void_p, c_int64, c_void_p, c_int32, c_void_p],
     'svae_radam': [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_int32, c_void_p,
                    c_void_p, c_void_p],

@@ -877,17 +877,18 @@ class VAEEngine:
                 nd = (nst['drop_p'], nst['seed'], L)
             # position-0 splice: its gradient feeds z_projections[i]; earlier layers see zero there (moved out of dx by
             # the layer's last LayerNorm backward when it is a residual layer)
-            zs = (L, None, dzh_bf) if st['resid'] and st['rows_q'] == T else None
+            zs = (L, dzh, None) if st['resid'] and st['rows_q'] == T else None
             self.layer_bwd(st, dx, dx_prev, g2_ready=g2_ready, next_drop=nd, zsplice=zs)
             g2_ready = nd is not None
-            if zs is None:
+            wz, bz = f'z_projections.{i}.weight', f'z_projections.{i}.bias'
+            if zs is not None:   # dW, d bias and dz of z_projections[i] in one f32 launch
+                K.zproj_bwd(dzh, sv['z_bf'], P.w(wz), P.g(wz), P.g(bz), dz, B, d, Z)
+            else:
                 K.extract_rows(dx_prev, d, T, L, d, dzh)
                 K.cast_bf16(dzh, dzh_bf)
-            # (bias gradient = the dW GEMM's fused row sums of dzh)
-            self._dw(dzh_bf, sv['z_bf'], f'z_projections.{i}.weight', B, d, Z, bias=f'z_projections.{i}.bias')
-            # dz += dzh . W_i: a 64 x 64 output over K = d -> split K over blocks (f32 atomics into dz)
-            K.gemm(dzh_bf, P.w(f'z_projections.{i}.weight'), dz, B, Z, d, b_t=True, epi=EPI_F32_ATOMIC,
-                   splits=max(1, min(8, d // 64)))
+                self._dw(dzh_bf, sv['z_bf'], wz, B, d, Z, bias=bz)   # (bias gradient = the fused row sums)
+                # dz += dzh . W_i: a 64 x 64 output over K = d -> split K over blocks (f32 atomics into dz)
+                K.gemm(dzh_bf, P.w(wz), dz, B, Z, d, b_t=True, epi=EPI_F32_ATOMIC, splits=max(1, min(8, d // 64)))
             ready(P.end(f'z_projections.{i}.bias'))
             dx, dx_prev = dx_prev, dx
         dx_emb = dx                                   # decoder part of d x_emb (rows 0 already zero)

@@ -355,6 +355,14 @@ def extract_rows(x, ld, rows, mod, D, out):
     check(lib.svae_extract_rows(x.data_ptr(), ld, rows, mod, D, out.data_ptr(), stream()), 'svae_extract_rows')
 
 
+def zproj_bwd(g, z, W, dW, db, dz, B, d, Z):
+    """z_projections backward (svae_zproj_bwd): dW += g^T z, db += sum_b g, dz += g W (g f32 [B, d]; z, W bf16)."""
+    _dev(g, z, W, dW, db, dz)
+    assert g.dtype == f32 and z.dtype == bf16 and W.dtype == bf16 and dW.dtype == f32 and dz.dtype == f32
+    check(lib.svae_zproj_bwd(g.data_ptr(), z.data_ptr(), W.data_ptr(), dW.data_ptr(), db.data_ptr(), dz.data_ptr(),
+                             B, d, Z, stream()), 'svae_zproj_bwd')
+
+
 def sumsq(g, n, part):
     check(lib.svae_sumsq(g.data_ptr(), n, part.data_ptr(), part.numel(), stream()), 'svae_sumsq')
 

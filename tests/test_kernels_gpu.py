@@ -257,6 +257,22 @@ def test_layernorm_bwd_fused_dropout_cast(p):
     assert torch.equal(dx2, dxz) and torch.equal(got2, ref)
 
 
+@pytest.mark.parametrize('B,d,Z', [(64, 512, 64), (3, 200, 70), (130, 768, 128)])
+def test_zproj_bwd(B, d, Z):
+    # z_projections backward in one launch: dW += g^T z, db += sum_b g, dz += g W (f32 accumulation; z, W bf16)
+    torch.manual_seed(B + d + Z)
+    g = torch.randn(B, d, device=dev)
+    z = torch.randn(B, Z, device=dev).bfloat16()
+    W = (torch.randn(d, Z, device=dev) * 0.1).bfloat16()
+    dW, db, dz = torch.randn(d, Z, device=dev), torch.randn(d, device=dev), torch.randn(B, Z, device=dev)
+    rW = dW + g.double().t().mm(z.double()).float()
+    rb = db + g.double().sum(0).float()
+    rz = dz + g.double().mm(W.double()).float()
+    K.zproj_bwd(g, z, W, dW, db, dz, B, d, Z)
+    torch.cuda.synchronize()
+    assert _rel(dW, rW) < 1e-6 and _rel(db, rb) < 1e-6 and _rel(dz, rz) < 1e-6
+
+
 @pytest.mark.parametrize('rows,cols,ld,dt', [(1024, 1024, 1024, torch.float32), (1000, 512, 520, torch.float32),
                                             (37, 1024, 1024, torch.float32), (5, 8, 8, torch.float32),
                                             (32768, 512, 512, torch.bfloat16), (4093, 2048, 2048, torch.bfloat16)])
