@@ -48,6 +48,7 @@ def main():
     r = torch.rand(T, device=dev) * 1e-4
     q = torch.rand(T, device=dev) * 1e-4
     dhh = torch.empty(T, d, dtype=bf16, device=dev)
+    hhT = hh.t().contiguous()
     fl = 2.0 * T * d * V
     cases = {
         'fwd CE_STATS': lambda: K.gemm(hh, W, out, T, V, d, epi=N.EPI_CE_STATS, bias=bias, aux=part2, labels=labels,
@@ -61,6 +62,10 @@ def main():
                                     epi=N.EPI_F32_ACC, a_rowsum=db),
         'dW rowsum kw': lambda: K.gemm(out, hh, dW, V, d, T, a_t=True, b_t=True, lda=V, ldb=d, ldc=d,
                                        epi=N.EPI_F32_ACC, a_rowsum=db, k_weight=r),
+        'dW kw, B K-contig': lambda: K.gemm(out, hhT, dW, V, d, T, a_t=True, b_t=False, lda=V, ldb=T, ldc=d,
+                                            epi=N.EPI_F32_ACC, a_rowsum=db, k_weight=r),
+        'dW, B K-contig': lambda: K.gemm(out, hhT, dW, V, d, T, a_t=True, b_t=False, lda=V, ldb=T, ldc=d,
+                                         epi=N.EPI_F32_ACC),
         'dX BF16': lambda: K.gemm(out, WT, dhh, T, d, V, epi=N.EPI_BF16),
         'dX ROWSCALE_GATHER': lambda: K.gemm(out, WT, dhh, T, d, V, epi=N.EPI_ROWSCALE_GATHER, labels=labels,
                                              row_a=r, row_b=q, gather=W, ldg=d),
