@@ -591,9 +591,6 @@ constexpr int G3_T = 256 * 64 * 2;   // 32 KiB per operand K-tile
 #ifndef SVAE_G3_PRIO
 #define SVAE_G3_PRIO 0
 #endif
-#ifndef SVAE_G3_SPREAD
-#define SVAE_G3_SPREAD 0   // A/B: -DSVAE_G3_SPREAD=1 issues the next K-tile's DMA pieces 2 per quadrant
-#endif
 #if SVAE_G3_PRIO
 #define G3_PRIO_HI() __builtin_amdgcn_s_setprio(1)
 #define G3_PRIO_LO() __builtin_amdgcn_s_setprio(0)
@@ -646,15 +643,6 @@ __device__ __forceinline__ void g3_issue_one(const bf16* tile_base, const G3Src&
     const int off = (krem >= 64 || src.kq[i] < krem) ? src.off[i] : 0x7FFFFFF0;
     dma16_lds(rs, dst + (wave * 4 + i) * 1024, off);
   }
-}
-
-// One piece (i) of one operand's K-tile (the spread issue order: a piece of A and one of B before each quadrant)
-template <bool MN>
-__device__ __forceinline__ void g3_issue_piece(const bf16* tile_base, const G3Src& src, int krem, char* dst, int wave,
-                                               int i) {
-  const u32x4 rs = buffer_rsrc(tile_base, 0x7FFFFFF0u);
-  const int off = (krem >= 64 || src.kq[i] < krem) ? src.off[i] : 0x7FFFFFF0;
-  dma16_lds(rs, dst + (wave * 4 + i) * 1024, off);
 }
 
 template <bool AT, bool BT>
@@ -1205,40 +1193,6 @@ __device__ __forceinline__ void gemm256_run(const GP& p, int blk, int nwg) {
       const char* la = smem + (g & 1) * G3_STAGE;
       const char* lb = la + G3_T;
       char* nxt = smem + ((g + 1) & 1) * G3_STAGE;
-#if SVAE_G3_SPREAD
-      // the next K-tile's 8 pieces are issued 2 per quadrant (one of A, one of B) instead of all 8 up front
-      const bf16* pA = nullptr;
-      const bf16* pB = nullptr;
-      int pkrem = 0;
-      G3Src qa = sa, qb = sb;
-      {
-        int k0n = -1;
-        const G3Tile* X = &T;
-        G3Tile TN;
-        if (kt + 1 < T.nk) k0n = T.kbeg + (kt + 1) * 64;
-        else if (has_next) {
-          TN = g3_tile(p, t3n);
-          if (TN.nk > 0) {
-            srcs(TN, qa, qb);
-            X = &TN;
-            k0n = TN.kbeg;
-          }
-        }
-        if (k0n >= 0) {
-          pA = AT ? X->A + (long long)k0n * p.lda + X->m0 : X->A + (long long)X->m0 * p.lda + k0n;
-          pB = BT ? X->B + (long long)k0n * p.ldb + X->n0 : X->B + (long long)X->n0 * p.ldb + k0n;
-          pkrem = X->kend - k0n;
-          issue_kw(*X, k0n, (g + 1) & 1);
-        }
-      }
-      auto issue_q = [&](int i) {
-        if (pA) {
-          g3_issue_piece<AT>(pA, qa, pkrem, nxt, wave, i);
-          g3_issue_piece<BT>(pB, qb, pkrem, nxt + G3_T, wave, i);
-        }
-      };
-#else
-      auto issue_q = [&](int) {};
       if (kt + 1 < T.nk) {
         g3_issue<AT, BT>(p, T.A, T.B, sa, sb, T.m0, T.n0, T.kbeg + (kt + 1) * 64, T.kend, nxt, wave);
         issue_kw(T, T.kbeg + (kt + 1) * 64, (g + 1) & 1);
@@ -1251,7 +1205,6 @@ __device__ __forceinline__ void gemm256_run(const GP& p, int blk, int nwg) {
           issue_kw(TN, TN.kbeg, (g + 1) & 1);
         }
       }
-#endif
       // Quadrant walk (mh, nh) = (0,0) (0,1) (1,1) (1,0): A fragments of a half reused by two quadrants, B
       // fragments of a half by the turn. The next quadrant's fragment reads are issued ahead of the current
       // quadrant's MFMAs.
@@ -1294,7 +1247,6 @@ __device__ __forceinline__ void gemm256_run(const GP& p, int blk, int nwg) {
       for (int j = 0; j < 2; ++j)
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) b1[j][ks] = g3_bfrag<BT>(lb, wc * 64 + 32 + j * 16, ks, lane);
-      issue_q(0);
       G3_PRIO_HI();
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
@@ -1303,7 +1255,6 @@ __device__ __forceinline__ void gemm256_run(const GP& p, int blk, int nwg) {
 #pragma unroll
           for (int j = 0; j < 2; ++j) acc[i][j] = mfma16(b0[j][ks], a0[i][ks], acc[i][j]);
       G3_PRIO_LO();
-      issue_q(1);
       if constexpr (!AT) {   // (AT: transposed A reads need the registers; load after the a0 quadrants)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
@@ -1329,14 +1280,12 @@ __device__ __forceinline__ void gemm256_run(const GP& p, int blk, int nwg) {
           for (int ks = 0; ks < 2; ++ks) a1[i][ks] = g3_afrag<AT>(la, wr * 128 + 64 + i * 16, ks, lane);
         G3_PRIO_HI();
       }
-      issue_q(2);
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int j = 0; j < 2; ++j) acc[4 + i][2 + j] = mfma16(b1[j][ks], a1[i][ks], acc[4 + i][2 + j]);
-      issue_q(3);
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
 #pragma unroll

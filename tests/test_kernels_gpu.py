@@ -56,7 +56,7 @@ def test_gemm256_at_kcontig_b_exact():
     A = torch.randint(-2, 3, (Kk, M), device=dev, generator=g).float()
     B = torch.randint(-2, 3, (Kk, Nn), device=dev, generator=g).float()
     kw = torch.randint(-2, 3, (Kk,), device=dev, generator=g).float()
-    for use_kw in (False, True):
+    for use_kw in (False, True, True, True):   # (k-weighted row sums repeated: a DMA-order experiment raced there)
         C = torch.ones(M, Nn, device=dev)
         rs = torch.full((M,), 3.0, device=dev)
         K.gemm(A.bfloat16(), B.t().contiguous().bfloat16(), C, M, Nn, Kk, a_t=True, b_t=False, ldb=Kk,
