@@ -170,6 +170,10 @@ int svae_dq_finalize(const float* dq, void* out, int64_t ldo, int32_t rows, int3
 /* ---- embedding (transformer_language_model.py:40-48): gather rows / scatter-add grads ------------- */
 int svae_embedding_fwd(const int32_t* ids, const void* table_bf, float* out, void* out_bf, int32_t rows,
                        int32_t D, svae_stream_t stream);
+/* the same gather into two f32 destinations (the encoder's input and the decoder's, whose position-0 rows the z
+ * splice overwrites): replaces a device copy of the [rows, D] result */
+int svae_embedding_fwd_dual(const int32_t* ids, const void* table, float* out, float* out2, int32_t rows, int32_t D,
+                            svae_stream_t stream);
 int svae_embedding_bwd(const int32_t* ids, const float* dout, float* dtable, int32_t rows, int32_t D,
                        svae_stream_t stream);
 

@@ -14,7 +14,7 @@ namespace {
 // ------------------------------------------------------------------ embedding
 __global__ __launch_bounds__(256) void emb_fwd_kernel(const int* __restrict__ ids, const float* __restrict__ table,
                                                       float* __restrict__ out, bf16* __restrict__ out_bf, int rows,
-                                                      int D) {
+                                                      int D, float* __restrict__ out2) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -22,6 +22,7 @@ __global__ __launch_bounds__(256) void emb_fwd_kernel(const int* __restrict__ id
   for (int c = lane * 4; c < D; c += 256) {
     const f32x4 v = *(const f32x4*)(table + src + c);
     *(f32x4*)(out + (long long)row * D + c) = v;
+    if (out2) *(f32x4*)(out2 + (long long)row * D + c) = v;
     if (out_bf)
       *(bf16x4*)(out_bf + (long long)row * D + c) = (bf16x4){f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
   }
@@ -658,7 +659,16 @@ SVAE_EXPORT int svae_embedding_fwd(const int32_t* ids, const void* table, float*
                                    int32_t D, svae_stream_t stream) {
   if (!ids || !table || !out || rows <= 0 || D % 4) return SVAE_EINVAL;
   hipLaunchKernelGGL(emb_fwd_kernel, dim3((rows + 3) / 4), dim3(256), 0, (hipStream_t)stream, ids, (const float*)table,
-                     out, (bf16*)out_bf, rows, D);
+                     out, (bf16*)out_bf, rows, D, (float*)nullptr);
+  SVAE_LAUNCH_CHECK();
+  return SVAE_OK;
+}
+
+SVAE_EXPORT int svae_embedding_fwd_dual(const int32_t* ids, const void* table, float* out, float* out2, int32_t rows,
+                                        int32_t D, svae_stream_t stream) {
+  if (!ids || !table || !out || !out2 || rows <= 0 || D % 4) return SVAE_EINVAL;
+  hipLaunchKernelGGL(emb_fwd_kernel, dim3((rows + 3) / 4), dim3(256), 0, (hipStream_t)stream, ids, (const float*)table,
+                     out, (bf16*)nullptr, rows, D, out2);
   SVAE_LAUNCH_CHECK();
   return SVAE_OK;
 }

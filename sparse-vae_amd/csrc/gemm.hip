@@ -591,6 +591,9 @@ constexpr int G3_T = 256 * 64 * 2;   // 32 KiB per operand K-tile
 #ifndef SVAE_G3_PRIO
 #define SVAE_G3_PRIO 0
 #endif
+#ifndef SVAE_G3_RS_EARLY
+#define SVAE_G3_RS_EARLY 0   // A/B: bias-gradient row sums between quadrants 1|2 and 3|4 instead of after 2 and 4
+#endif
 #if SVAE_G3_PRIO
 #define G3_PRIO_HI() __builtin_amdgcn_s_setprio(1)
 #define G3_PRIO_LO() __builtin_amdgcn_s_setprio(0)
@@ -1255,6 +1258,14 @@ __device__ __forceinline__ void gemm256_run(const GP& p, int blk, int nwg) {
 #pragma unroll
           for (int j = 0; j < 2; ++j) acc[i][j] = mfma16(b0[j][ks], a0[i][ks], acc[i][j]);
       G3_PRIO_LO();
+#if SVAE_G3_RS_EARLY
+      if constexpr (AT) {   // the row sums between two quadrants, under the MFMAs already in the pipe
+        if (do_rs) {
+          if (wc == 0) rowsum2(a0[0], a0[1]);
+          else if (wc == 1) rowsum2(a0[2], a0[3]);
+        }
+      }
+#endif
       if constexpr (!AT) {   // (AT: transposed A reads need the registers; load after the a0 quadrants)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
@@ -1270,10 +1281,12 @@ __device__ __forceinline__ void gemm256_run(const GP& p, int blk, int nwg) {
           for (int j = 0; j < 2; ++j) acc[i][2 + j] = mfma16(b1[j][ks], a0[i][ks], acc[i][2 + j]);
       if constexpr (AT) {
         G3_PRIO_LO();
+#if !SVAE_G3_RS_EARLY
         if (do_rs) {
           if (wc == 0) rowsum2(a0[0], a0[1]);
           else if (wc == 1) rowsum2(a0[2], a0[3]);
         }
+#endif
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -1286,6 +1299,14 @@ __device__ __forceinline__ void gemm256_run(const GP& p, int blk, int nwg) {
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int j = 0; j < 2; ++j) acc[4 + i][2 + j] = mfma16(b1[j][ks], a1[i][ks], acc[4 + i][2 + j]);
+#if SVAE_G3_RS_EARLY
+      if constexpr (AT) {
+        if (do_rs) {
+          if (wc == 2) rowsum2(a1[0], a1[1]);
+          else if (wc == 3) rowsum2(a1[2], a1[3]);
+        }
+      }
+#endif
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
@@ -1294,10 +1315,12 @@ __device__ __forceinline__ void gemm256_run(const GP& p, int blk, int nwg) {
           for (int j = 0; j < 2; ++j) acc[4 + i][j] = mfma16(b0[j][ks], a1[i][ks], acc[4 + i][j]);
       G3_PRIO_LO();
       if constexpr (AT) {
+#if !SVAE_G3_RS_EARLY
         if (do_rs) {
           if (wc == 2) rowsum2(a1[0], a1[1]);
           else if (wc == 3) rowsum2(a1[2], a1[3]);
         }
+#endif
       }
     }
     G3_STAMP(1);

@@ -77,6 +77,7 @@ _SIGS = {
     'svae_transpose_blocks': [c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p],
     'svae_dq_finalize': [c_void_p, c_void_p, c_int64, c_int32, c_int32, c_void_p, c_int32, c_void_p],
     'svae_embedding_fwd': [c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p],
+    'svae_embedding_fwd_dual': [c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p],
     'svae_embedding_bwd': [c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p],
     'svae_reparam_kl_fwd': [c_void_p, c_void_p, c_uint64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                             c_void_p, c_int32, c_int32, c_void_p],

@@ -524,7 +524,8 @@ class VAEEngine:
         sv = {'B': B, 'L': L, 'dropout': dropout, 'seed': seed}
 
         x_emb = ws.get('x_emb', (T, d), f32)
-        K.embedding_fwd(ids32, P.f('input_layer.0.weight'), x_emb, T, d)
+        # (the decoder's input copy is written by the same gather: _decode's x_dec0)
+        K.embedding_fwd(ids32, P.f('input_layer.0.weight'), x_emb, T, d, out2=ws.get('x_dec0', (T, d), f32))
 
         # ---- encoder (perceiver.py:39-50) + q(z|x) (conditional_gaussian.py:18)
         enc_bf, stats, sv['enc_layers'] = self._encode(x_emb, B, L, padm, dropout, seed)
@@ -542,7 +543,7 @@ class VAEEngine:
         sv.update(enc_bf=enc_bf, stats=stats, z_bf=zb, eps=eps_buf)
 
         # ---- decoder (transformer_vae.py:85-93), position 0 replaced by z_projections[i](z) every layer
-        xs, sv['dec_layers'] = self._decode(x_emb, zb, padm, B, L, dropout, seed)
+        xs, sv['dec_layers'] = self._decode(x_emb, zb, padm, B, L, dropout, seed, x_ready=True)
 
         # ---- output head + cross entropy (transformer_language_model.py:55-63, language_model.py:161-170)
         xf = ws.get('xf_bf', (T, d))
@@ -723,14 +724,15 @@ class VAEEngine:
         hh, _ = self._ln_fwd('output_layer.2', h0, T, 'head.ln')
         return hh
 
-    def _decode(self, x_emb, zb, padm, B, L, dropout, seed):
+    def _decode(self, x_emb, zb, padm, B, L, dropout, seed, x_ready=False):
         hp, d, ws, P = self.hp, self.d, self.ws, self.P
         T, Z = B * L, hp.latent_depth
         if self.window and L % 32:
             raise ValueError(f'sparse decoder attention needs seq_len % 32 == 0 (SparseAttention block_size 32, '
                              f'sparse_attention.py:81), got {L}')
         xs = ws.get('x_dec0', (T, d), f32)
-        xs.copy_(x_emb)
+        if not x_ready:   # (the training forward's embedding gather wrote it already)
+            xs.copy_(x_emb)
         dec = []
         for i in range(hp.num_layers):
             K.gemm(zb, P.w(f'z_projections.{i}.weight'), xs, B, d, Z, ldc=L * d, epi=EPI_F32,

@@ -225,7 +225,12 @@ def dq_finalize(dq, out, ldo, rows, D, rot=None, seq=0):
           'svae_dq_finalize')
 
 
-def embedding_fwd(ids, table, out, rows, D):
+def embedding_fwd(ids, table, out, rows, D, out2=None):
+    if out2 is not None:
+        _dev(ids, table, out, out2)
+        check(lib.svae_embedding_fwd_dual(ids.data_ptr(), table.data_ptr(), out.data_ptr(), out2.data_ptr(), rows, D,
+                                          stream()), 'svae_embedding_fwd_dual')
+        return
     check(lib.svae_embedding_fwd(ids.data_ptr(), table.data_ptr(), out.data_ptr(), None, rows, D, stream()),
           'svae_embedding_fwd')
 
