@@ -852,36 +852,36 @@ SVAE_EXPORT int svae_transpose_blocks(const void* src, void* dst, const int64_t*
   return SVAE_OK;
 }
 
-// z_projections[i] backward (svae.h): blocks [0, nbw) own 4 rows m of dW (one wave per row, lanes over n; the
-// wave's lane-strided sum over b gives db[m]); blocks [nbw, nbw + B) own one row b of dz (4 waves over quarters of m,
-// combined in LDS in a fixed order). Every output has one writer: no atomics. Operands are staged through LDS in
-// 64-row chunks (a chain of dependent global loads per output ran 10.7 us per launch at C2).
-__global__ __launch_bounds__(256) void zproj_bwd_kernel(const float* __restrict__ g, const bf16* __restrict__ z,
-                                                        const bf16* __restrict__ W, float* __restrict__ dW,
-                                                        float* __restrict__ db, float* __restrict__ dz, int B, int d,
-                                                        int Z, int nbw) {
+// z_projections[i] backward (svae.h): 1024-thread blocks. Blocks [0, nbw) own 16 rows m of dW (one wave per row,
+// lanes over n; the wave's lane-strided sum over b gives db[m]); blocks [nbw, nbw + B) own one row b of dz (16 waves
+// over slices of m, combined in LDS in a fixed order). Every output has one writer: no atomics. Operands are staged
+// through LDS in 64-row chunks. (256-thread blocks: 10.7 us per launch at C2, the dz row's 128 dependent steps.)
+__global__ __launch_bounds__(1024) void zproj_bwd_kernel(const float* __restrict__ g, const bf16* __restrict__ z,
+                                                         const bf16* __restrict__ W, float* __restrict__ dW,
+                                                         float* __restrict__ db, float* __restrict__ dz, int B, int d,
+                                                         int Z, int nbw) {
   __shared__ float zs[64][65];
   __shared__ float gs[1024];
-  __shared__ float red[4][64];
+  __shared__ float red[16][64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if ((int)blockIdx.x < nbw) {
-    const int m0 = blockIdx.x * 4, m = m0 + wave;
+    const int m0 = blockIdx.x * 16, m = m0 + wave;
     for (int n0 = 0; n0 < Z; n0 += 64) {
       const int n = n0 + lane;
       float acc = 0.f;
       for (int b0 = 0; b0 < B; b0 += 64) {
         const int nb = min(64, B - b0);
-        for (int e = tid; e < 64 * 64; e += 256) {
+        for (int e = tid; e < 64 * 64; e += 1024) {
           const int i = e >> 6, j = e & 63;
           zs[i][j] = (i < nb && n0 + j < Z) ? (float)z[(long long)(b0 + i) * Z + n0 + j] : 0.f;
         }
         {
-          const int i = tid >> 2, w = tid & 3;
+          const int i = tid >> 4, w = tid & 15;
           gs[tid] = (i < nb && m0 + w < d) ? g[(long long)(b0 + i) * d + m0 + w] : 0.f;
         }
         __syncthreads();
 #pragma unroll 16
-        for (int i = 0; i < 64; ++i) acc = fmaf(gs[4 * i + wave], zs[i][lane], acc);
+        for (int i = 0; i < 64; ++i) acc = fmaf(gs[16 * i + wave], zs[i][lane], acc);
         __syncthreads();
       }
       if (m < d && n < Z) dW[(long long)m * Z + n] += acc;
@@ -900,17 +900,22 @@ __global__ __launch_bounds__(256) void zproj_bwd_kernel(const float* __restrict_
       float acc = 0.f;
       for (int c0 = 0; c0 < d; c0 += 1024) {   // the row's g in LDS, 1024 columns at a time
         const int nc = min(1024, d - c0);
-        for (int e = tid; e < nc; e += 256) gs[e] = gb[c0 + e];
+        if (tid < nc) gs[tid] = gb[c0 + tid];
         __syncthreads();
         if (n < Z) {
-#pragma unroll 16
-          for (int mm = wave; mm < nc; mm += 4) acc = fmaf(gs[mm], (float)W[(long long)(c0 + mm) * Z + n], acc);
+#pragma unroll 8
+          for (int mm = wave; mm < nc; mm += 16) acc = fmaf(gs[mm], (float)W[(long long)(c0 + mm) * Z + n], acc);
         }
         __syncthreads();
       }
       red[wave][lane] = acc;
       __syncthreads();
-      if (wave == 0 && n < Z) dz[(long long)b * Z + n] += (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+      if (wave == 0 && n < Z) {
+        float t = 0.f;
+#pragma unroll
+        for (int w = 0; w < 16; ++w) t += red[w][lane];
+        dz[(long long)b * Z + n] += t;
+      }
       __syncthreads();
     }
   }
@@ -919,8 +924,8 @@ __global__ __launch_bounds__(256) void zproj_bwd_kernel(const float* __restrict_
 SVAE_EXPORT int svae_zproj_bwd(const float* g, const void* z, const void* W, float* dW, float* db, float* dz,
                                int32_t B, int32_t d, int32_t Z, svae_stream_t stream) {
   if (!g || !z || !W || !dW || !db || !dz || B <= 0 || d <= 0 || Z <= 0) return SVAE_EINVAL;
-  const int nbw = (d + 3) / 4;
-  hipLaunchKernelGGL(zproj_bwd_kernel, dim3(nbw + B), dim3(256), 0, (hipStream_t)stream, g, (const bf16*)z,
+  const int nbw = (d + 15) / 16;
+  hipLaunchKernelGGL(zproj_bwd_kernel, dim3(nbw + B), dim3(1024), 0, (hipStream_t)stream, g, (const bf16*)z,
                      (const bf16*)W, dW, db, dz, B, d, Z, nbw);
   SVAE_LAUNCH_CHECK();
   return SVAE_OK;
