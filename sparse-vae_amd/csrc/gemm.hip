@@ -1399,321 +1399,6 @@ __global__ __launch_bounds__(512, 1) void gemm256_pair_kernel(GP2 q) {
   else gemm256_run<AT, BT, EPI>(q.p[1], b - q.nb0, (int)gridDim.x - q.nb0);
 }
 
-// ===================================================================================================
-// gemm_ov: the K = 512-class GEMMs (A, B K-contiguous) with the epilogue beside the MFMAs. Persistent, one 4-wave
-// block per CU (one wave per SIMD, up to 512 VGPRs), 256 x 128 tiles, each wave 128 x 64 (the gemm256 wave tile),
-// BK = 64 with a 2-stage LDS-DMA ring. A wave keeps the previous tile's accumulators and finishes their epilogue one
-// 16-row fragment row per K-tile of the current tile (the operands of row i + 1 -- residual, GELU' or rotary table
-// -- loaded during row i), so the epilogue VALU and stores issue between this tile's MFMAs instead of after them.
-// The epilogue never touches LDS, so it needs no barrier of its own.
-constexpr int OV_TA = 256 * 64 * 2, OV_TB = 128 * 64 * 2, OV_STAGE = OV_TA + OV_TB;
-
-template <int I>
-struct IntC {
-  static constexpr int value = I;
-};
-
-// per-lane DMA source offsets of an operand of NP * 4 pieces (8 rows x 128 B each, 4 waves)
-template <int NP>
-struct OvSrc {
-  int off[NP];
-  int kq[NP];
-};
-template <int NP>
-__device__ __forceinline__ OvSrc<NP> ov_src(long long ld, int row0, int nrows, int wave, int lane) {
-  OvSrc<NP> s;
-#pragma unroll
-  for (int i = 0; i < NP; ++i) {
-    const int piece = wave * NP + i;
-    const int r = piece * 8 + (lane >> 3), c = (lane & 7) ^ ((r >> 1) & 7);
-    s.off[i] = (row0 + r < nrows) ? (r * (int)ld + c * 8) * 2 : 0x7FFFFFF0;
-    s.kq[i] = c * 8;
-  }
-  return s;
-}
-template <int NP>
-__device__ __forceinline__ void ov_issue(const bf16* tile_base, const OvSrc<NP>& src, int krem, char* dst, int wave) {
-  const u32x4 rs = buffer_rsrc(tile_base, 0x7FFFFFF0u);
-#pragma unroll
-  for (int i = 0; i < NP; ++i) {
-    const int off = (krem >= 64 || src.kq[i] < krem) ? src.off[i] : 0x7FFFFFF0;
-    dma16_lds(rs, dst + (wave * NP + i) * 1024, off);
-  }
-}
-
-// the previous tile of a wave: origin, bias columns and the prefetched operand of its next epilogue row
-struct OvPrev {
-  int m0, n0;
-  f32x4 b4[4];
-  f32x4 op[4];   // F32 / DROPOUT_RESID: residual row; GELU_BWD: aux (2 x 16 B); ROTARY: (cos, sin) pairs
-};
-
-template <int EPI>
-__device__ __forceinline__ void ov_load(const GP& p, OvPrev& s, int i, int wr, int wc, int lane) {
-  const int g = lane >> 4, li = lane & 15;
-  const int m = s.m0 + wr * 128 + i * 16 + li, nb = s.n0 + wc * 64;
-  const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
-  if constexpr (EPI == SVAE_EPI_F32 || EPI == SVAE_EPI_DROPOUT_RESID) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int n = nb + j * 16 + 4 * g;
-      s.op[j] = (p.resid && m < p.M && n < p.N) ? *(const f32x4*)(p.resid + (long long)m * p.ldr + n) : zero;
-    }
-  } else if constexpr (EPI == SVAE_EPI_GELU_BWD) {
-    const int cs = ((g & 1) ? 16 : 0) + ((g & 2) ? 8 : 0);
-#pragma unroll
-    for (int jp = 0; jp < 2; ++jp) {
-      const int n = nb + 32 * jp + cs;
-      const u32x4 r = (m < p.M && n + 8 <= p.N) ? *(const u32x4*)((const bf16*)p.aux + (long long)m * p.ldaux + n)
-                                                : (u32x4){0u, 0u, 0u, 0u};
-      s.op[jp] = __builtin_bit_cast(f32x4, r);
-    }
-  } else if constexpr (EPI == SVAE_EPI_ROTARY_BF16) {
-    const int pos = (m < p.M ? m : 0) % p.rot_seq;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int n = nb + j * 16 + 4 * g;
-      s.op[j] = n < p.rot_cols ? *(const f32x4*)(p.rot_tab + (long long)pos * p.rot_d + (n % p.rot_d))
-                               : (f32x4){1.f, 0.f, 1.f, 0.f};
-    }
-  }
-}
-
-// epilogue of fragment row i (16 rows x 64 columns of the wave) of the previous tile; a = its 4 accumulators
-template <int EPI>
-__device__ __forceinline__ void ov_row(const GP& p, const OvPrev& s, const f32x4 (&a)[4], int i, int wr, int wc,
-                                       int lane) {
-  const int g = lane >> 4, li = lane & 15;
-  const int m = s.m0 + wr * 128 + i * 16 + li;
-  const bool row_ok = m < p.M;
-  const int nb = s.n0 + wc * 64, nleft = p.N - nb;
-  if constexpr (EPI == SVAE_EPI_GELU_BWD) {
-    const int cs = ((g & 1) ? 16 : 0) + ((g & 2) ? 8 : 0);
-#pragma unroll
-    for (int jp = 0; jp < 2; ++jp) {
-      const f32x4 x = p.alpha * a[2 * jp] + s.b4[2 * jp], y = p.alpha * a[2 * jp + 1] + s.b4[2 * jp + 1];
-      float w[8];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(x[e]), __float_as_uint(y[e]), false, false);
-        w[e] = __uint_as_float(sw[0]);
-        w[4 + e] = __uint_as_float(sw[1]);
-      }
-      const bf16x8 av = __builtin_bit_cast(bf16x8, s.op[jp]);
-      const u32x4 o = {pack_bf16x2(w[0] * (float)av[0], w[1] * (float)av[1]),
-                       pack_bf16x2(w[2] * (float)av[2], w[3] * (float)av[3]),
-                       pack_bf16x2(w[4] * (float)av[4], w[5] * (float)av[5]),
-                       pack_bf16x2(w[6] * (float)av[6], w[7] * (float)av[7])};
-      const int n = nb + 32 * jp + cs;
-      if (row_ok && n + 8 <= p.N) *(u32x4*)((bf16*)p.C + (long long)m * p.ldc + n) = o;
-      else if (row_ok && n < p.N) *(u32x2*)((bf16*)p.C + (long long)m * p.ldc + n) = (u32x2){o[0], o[1]};
-    }
-    return;
-  }
-  f32x4 v[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) v[j] = p.alpha * a[j] + s.b4[j];
-  if constexpr (EPI == SVAE_EPI_F32 || EPI == SVAE_EPI_DROPOUT_RESID) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int n = nb + j * 16 + 4 * g;
-      f32x4 x = v[j];
-      if constexpr (EPI == SVAE_EPI_DROPOUT_RESID) {
-        if (p.drop_p > 0.f) dropout4(p, x, m, n);
-      }
-      x += s.op[j];
-      if (row_ok && n < p.N) *(f32x4*)((float*)p.C + (long long)m * p.ldc + n) = x;
-    }
-    return;
-  } else {
-    if constexpr (EPI == SVAE_EPI_ROTARY_BF16) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const f32x4 cs2 = s.op[j];
-        const float a0 = v[j][0], b0 = v[j][1], a1 = v[j][2], b1 = v[j][3];
-        v[j][0] = a0 * cs2[0] + (-b0) * cs2[1];
-        v[j][1] = b0 * cs2[0] + a0 * cs2[1];
-        v[j][2] = a1 * cs2[2] + (-b1) * cs2[3];
-        v[j][3] = b1 * cs2[2] + a1 * cs2[3];
-      }
-    }
-    bf16* crow = (bf16*)p.C + (long long)(row_ok ? m : 0) * p.ldc + nb;
-    if constexpr (EPI == SVAE_EPI_GELU) {
-      f32x4 gg[4], dg[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int e = 0; e < 4; e += 2) {
-          f32x2 ge, de;
-          gelu_pair2((f32x2){v[j][e], v[j][e + 1]}, ge, de);
-          gg[j][e] = ge[0];
-          gg[j][e + 1] = ge[1];
-          dg[j][e] = de[0];
-          dg[j][e + 1] = de[1];
-        }
-      bf16* arow = (bf16*)p.aux + (long long)(row_ok ? m : 0) * p.ldaux + nb;
-#pragma unroll
-      for (int jp = 0; jp < 2; ++jp) {
-        store_pair_bf16(crow, 32 * jp, row_ok ? nleft : 0, gg[2 * jp], gg[2 * jp + 1], g);
-        store_pair_bf16(arow, 32 * jp, row_ok ? nleft : 0, dg[2 * jp], dg[2 * jp + 1], g);
-      }
-    } else {
-#pragma unroll
-      for (int jp = 0; jp < 2; ++jp) store_pair_bf16(crow, 32 * jp, row_ok ? nleft : 0, v[2 * jp], v[2 * jp + 1], g);
-    }
-  }
-}
-
-template <int EPI>
-__global__ __launch_bounds__(256, 1) void gemm_ov_kernel(GP p) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * OV_STAGE];
-  const int tid = threadIdx.x, lane = tid & 63, g4 = lane >> 4;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wave >> 1, wc = wave & 1;
-  const int nwg = gridDim.x;
-  int bid = blockIdx.x;
-  if (nwg >= 16) {   // XCD-aware bijective remap (as gemm256)
-    const int q = nwg / 8, r = nwg % 8, xcd = bid % 8, idx = bid / 8;
-    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
-  }
-  const int tn = (p.N + 127) / 128, tm = (p.M + 255) / 256, total = tn * tm;
-  int t = bid;
-  if (t >= total) return;
-  const int nk = (p.K + 63) / 64;
-  auto coords = [&](int tt, int& m0, int& n0) {
-    int bm, bn;
-    group_tile(tt, tm, tn, p.group, bm, bn);
-    m0 = bm * 256;
-    n0 = bn * 128;
-  };
-  int m0, n0;
-  coords(t, m0, n0);
-  OvSrc<8> sa = ov_src<8>(p.lda, m0, p.M, wave, lane);
-  OvSrc<4> sb = ov_src<4>(p.ldb, n0, p.N, wave, lane);
-  auto issue = [&](int mm, int nn, const OvSrc<8>& xa, const OvSrc<4>& xb, int k0, char* dst) {
-    ov_issue<8>(p.A + (long long)mm * p.lda + k0, xa, p.K - k0, dst, wave);
-    ov_issue<4>(p.B + (long long)nn * p.ldb + k0, xb, p.K - k0, dst + OV_TA, wave);
-  };
-  issue(m0, n0, sa, sb, 0, smem);
-
-  f32x4 acc[8][4], pacc[8][4];
-  OvPrev prev;
-  bool have_prev = false;
-  int gk = 0;   // K-tiles consumed by this block (stage = gk & 1)
-  while (true) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    const int tnext = t + nwg;
-    const bool has_next = tnext < total;
-    int nm0 = 0, nn0 = 0;
-    if (has_next) coords(tnext, nm0, nn0);
-    OvSrc<8> na = sa;
-    OvSrc<4> nbs = sb;
-    if (has_next) {
-      na = ov_src<8>(p.lda, nm0, p.M, wave, lane);
-      nbs = ov_src<4>(p.ldb, nn0, p.N, wave, lane);
-    }
-    // one K-tile: wait for its DMA, issue the next one, the previous tile's epilogue row R (R < 0: none), 64 MFMAs
-    auto kstep = [&](int kt, auto R) {
-      constexpr int row = decltype(R)::value;
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      const char* la = smem + (gk & 1) * OV_STAGE;
-      const char* lb = la + OV_TA;
-      char* nxt = smem + ((gk + 1) & 1) * OV_STAGE;
-      if (kt + 1 < nk) issue(m0, n0, sa, sb, (kt + 1) * 64, nxt);
-      else if (has_next) issue(nm0, nn0, na, nbs, 0, nxt);
-      bf16x8 a0[4][2], a1[4][2], b0[2][2], b1[2][2];
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) a0[i][ks] = g3_afrag<false>(la, wr * 128 + i * 16, ks, lane);
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) b0[j][ks] = g3_bfrag<false>(lb, wc * 64 + j * 16, ks, lane);
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) b1[j][ks] = g3_bfrag<false>(lb, wc * 64 + 32 + j * 16, ks, lane);
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j) acc[i][j] = mfma16(b0[j][ks], a0[i][ks], acc[i][j]);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) a1[i][ks] = g3_afrag<false>(la, wr * 128 + 64 + i * 16, ks, lane);
-      if constexpr (row >= 0) {   // the previous tile's row, between the quadrants
-        ov_row<EPI>(p, prev, pacc[row], row, wr, wc, lane);
-        if constexpr (row + 1 < 8) ov_load<EPI>(p, prev, row + 1, wr, wc, lane);
-      }
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j) acc[i][2 + j] = mfma16(b1[j][ks], a0[i][ks], acc[i][2 + j]);
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j) acc[4 + i][2 + j] = mfma16(b1[j][ks], a1[i][ks], acc[4 + i][2 + j]);
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j) acc[4 + i][j] = mfma16(b0[j][ks], a1[i][ks], acc[4 + i][j]);
-      ++gk;
-    };
-    // the first 8 K-tiles carry the previous tile's 8 epilogue rows (compile-time row index), the rest none
-    int kt = 0;
-    if (have_prev) {
-#define SVAE_OV_STEP(R) if (kt < nk) { kstep(kt, IntC<R>{}); ++kt; }
-      SVAE_OV_STEP(0) SVAE_OV_STEP(1) SVAE_OV_STEP(2) SVAE_OV_STEP(3)
-      SVAE_OV_STEP(4) SVAE_OV_STEP(5) SVAE_OV_STEP(6) SVAE_OV_STEP(7)
-#undef SVAE_OV_STEP
-      // rows a short K-loop (< 8 K-tiles) left over
-#define SVAE_OV_TAIL(R) if (R >= nk) { ov_row<EPI>(p, prev, pacc[R], R, wr, wc, lane); if (R + 1 < 8) ov_load<EPI>(p, prev, R + 1, wr, wc, lane); }
-      SVAE_OV_TAIL(0) SVAE_OV_TAIL(1) SVAE_OV_TAIL(2) SVAE_OV_TAIL(3)
-      SVAE_OV_TAIL(4) SVAE_OV_TAIL(5) SVAE_OV_TAIL(6) SVAE_OV_TAIL(7)
-#undef SVAE_OV_TAIL
-    }
-    for (; kt < nk; ++kt) kstep(kt, IntC<-1>{});
-    // this tile becomes the previous one: accumulators, origin, bias, the operand of its row 0
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) pacc[i][j] = acc[i][j];
-    prev.m0 = m0;
-    prev.n0 = n0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int n = n0 + wc * 64 + j * 16 + 4 * g4;
-      prev.b4[j] = (p.bias && n < p.N) ? *(const f32x4*)(p.bias + n) : (f32x4){0.f, 0.f, 0.f, 0.f};
-    }
-    ov_load<EPI>(p, prev, 0, wr, wc, lane);
-    have_prev = true;
-    if (!has_next) break;
-    t = tnext;
-    m0 = nm0;
-    n0 = nn0;
-    sa = na;
-    sb = nbs;
-  }
-  // the last tile's epilogue
-#define SVAE_OV_LAST(R) { ov_row<EPI>(p, prev, pacc[R], R, wr, wc, lane); if (R + 1 < 8) ov_load<EPI>(p, prev, R + 1, wr, wc, lane); }
-  SVAE_OV_LAST(0) SVAE_OV_LAST(1) SVAE_OV_LAST(2) SVAE_OV_LAST(3)
-  SVAE_OV_LAST(4) SVAE_OV_LAST(5) SVAE_OV_LAST(6) SVAE_OV_LAST(7)
-#undef SVAE_OV_LAST
-}
-
 // C[m][n] += sum over splits of slab[s][m][n] (slab rows of N floats); 4 columns per thread
 __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restrict__ slab, float* __restrict__ C,
                                                           int M, int N, long long ldc, int splits) {
@@ -1840,38 +1525,6 @@ SVAE_EXPORT int svae_gemm(const svae_gemm_desc* d, svae_stream_t stream) {
     epi_run = G3_EPI_ACC_KW;
   }
   if (impl == 3 && !ok3) impl = 1;
-  // gemm_ov (epilogue beside the MFMAs) for the K-contiguous single GEMMs with a register epilogue, when there are
-  // several tiles per CU to overlap (SVAE_GEMM_OV=1 enables it; A/B runs)
-  static const int ov_env = [] { const char* e = getenv("SVAE_GEMM_OV"); return e ? atoi(e) : 0; }();
-  {
-    const int e = d->epi;
-    const bool ov_epi = e == SVAE_EPI_BF16 || e == SVAE_EPI_GELU || e == SVAE_EPI_GELU_BWD ||
-                        e == SVAE_EPI_DROPOUT_RESID || e == SVAE_EPI_F32 || e == SVAE_EPI_ROTARY_BF16;
-    const long long tiles_ov = (long long)((d->N + 127) / 128) * ((d->M + 255) / 256);
-    if (ov_env && !forced && ov_epi && !d->a_t && !d->b_t && d->batch == 1 && d->splits == 1 && !d->a_rowsum &&
-        d->C && tiles_ov >= 512 && !slab) {
-      static const int ncu_ov = [] {
-        int dev = 0, n = 0;
-        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-          n = 256;
-        return n > 0 ? n : 256;
-      }();
-      p.group = ((d->N + 127) / 128) >= 32 ? 4 : 0;
-      dim3 grid_ov((unsigned)std::min<long long>(tiles_ov, ncu_ov));
-      switch (e) {
-        case SVAE_EPI_BF16: hipLaunchKernelGGL(gemm_ov_kernel<SVAE_EPI_BF16>, grid_ov, dim3(256), 0, s, p); break;
-        case SVAE_EPI_GELU: hipLaunchKernelGGL(gemm_ov_kernel<SVAE_EPI_GELU>, grid_ov, dim3(256), 0, s, p); break;
-        case SVAE_EPI_GELU_BWD: hipLaunchKernelGGL(gemm_ov_kernel<SVAE_EPI_GELU_BWD>, grid_ov, dim3(256), 0, s, p); break;
-        case SVAE_EPI_DROPOUT_RESID:
-          hipLaunchKernelGGL(gemm_ov_kernel<SVAE_EPI_DROPOUT_RESID>, grid_ov, dim3(256), 0, s, p);
-          break;
-        case SVAE_EPI_F32: hipLaunchKernelGGL(gemm_ov_kernel<SVAE_EPI_F32>, grid_ov, dim3(256), 0, s, p); break;
-        default: hipLaunchKernelGGL(gemm_ov_kernel<SVAE_EPI_ROTARY_BF16>, grid_ov, dim3(256), 0, s, p); break;
-      }
-      SVAE_LAUNCH_CHECK();
-      return SVAE_OK;
-    }
-  }
   if (impl == 3) {
     int kc3 = (d->K + d->splits - 1) / d->splits;
     p.kchunk = (kc3 + 63) / 64 * 64;

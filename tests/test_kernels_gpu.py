@@ -164,7 +164,45 @@ def test_gemm_epilogues(M, Nn, Kk):
     assert agree.all()
 
 
-@pytest.mark.parametrize('B,L,d', [(2, 96, 256), (16, 512, 512)])
+@pytest.mark.parametrize('M,Nn,Kk', [(8200, 2056, 520), (8192, 2048, 512)])
+def test_gemm_many_tiles_epilogues(M, Nn, Kk):
+    # >= 512 tiles of 256 x 128: the shapes gemm_ov takes when enabled (SVAE_GEMM_OV=1; ragged M, N, K in the first)
+    torch.manual_seed(M + Kk)
+    Ai = torch.randint(-2, 3, (M, Kk), device=dev).float()
+    Bi = torch.randint(-2, 3, (Nn, Kk), device=dev).float()
+    C32 = torch.empty(M, Nn, device=dev)
+    K.gemm(Ai.bfloat16(), Bi.bfloat16(), C32, M, Nn, Kk, epi=N.EPI_F32)
+    torch.cuda.synchronize()
+    assert torch.equal(C32, Ai @ Bi.t())
+    X = torch.randn(M, Kk, device=dev).bfloat16()
+    W = (torch.randn(Nn, Kk, device=dev) * 0.1).bfloat16()
+    b = torch.randn(Nn, device=dev)
+    acc = X.float() @ W.float().t()
+    ref = acc + b
+    C = torch.empty(M, Nn, device=dev, dtype=torch.bfloat16)
+    K.gemm(X, W, C, M, Nn, Kk, epi=N.EPI_BF16, bias=b)
+    assert _rel(C, ref) < 4e-3
+    gp = torch.empty_like(C)
+    K.gemm(X, W, C, M, Nn, Kk, epi=N.EPI_GELU, bias=b, aux=gp, ldaux=Nn)
+    r = ref.clone().requires_grad_()
+    F.gelu(r).backward(torch.ones_like(r))
+    assert _rel(C, F.gelu(ref)) < 4e-3 and _rel(gp, r.grad) < 4e-3
+    G = torch.empty_like(C)
+    K.gemm(X, W, G, M, Nn, Kk, epi=N.EPI_GELU_BWD, aux=gp, ldaux=Nn)
+    assert _rel(G, acc * gp.float()) < 4e-3
+    R = torch.randn(M, Nn, device=dev)
+    K.gemm(X, W, C32, M, Nn, Kk, epi=N.EPI_F32, bias=b, resid=R, ldr=Nn)
+    assert _rel(C32, ref + R) < 1e-5
+    K.gemm(X, W, C32, M, Nn, Kk, epi=N.EPI_DROPOUT_RESID, resid=R, ldr=Nn, drop_p=0.1, seed=123)
+    keep = (C32 - R).abs() > 1e-6
+    assert 0.87 < keep.float().mean().item() < 0.93
+    assert _rel((C32 - R)[keep], (acc / 0.9)[keep]) < 1e-5
+    gb = torch.empty(M, Nn, device=dev, dtype=torch.bfloat16)
+    K.dropout_bwd_cast(torch.ones(M, Nn, device=dev), gb, 0.1, 123, M, Nn)
+    assert (((gb.float() != 0) == keep) | (acc.abs() < 1e-4)).all()
+
+
+@pytest.mark.parametrize('B,L,d', [(2, 96, 256), (16, 512, 512), (24, 512, 512)])
 def test_gemm_rotary_matches_reference_rotation(B, L, d):
     torch.manual_seed(1)
     X = torch.randn(B * L, d, device=dev).bfloat16()
