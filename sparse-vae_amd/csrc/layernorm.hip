@@ -36,6 +36,49 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, co
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
   const T* xr = x + (long long)row * D;
+  if constexpr (MAXV % 2 == 0) {
+    // D % 8 == 0 (checked by the launcher): each lane owns runs of 8 consecutive columns, so the bf16 output is one
+    // 16-B store per run (the 4-column layout below stores 8 B per lane)
+    constexpr int NR = MAXV / 2;
+    f32x4 v[NR][2];
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < NR; ++j) {
+      const int c = (lane + 64 * j) * 8;
+      v[j][0] = (c < D) ? load4<T>(xr + c) : (f32x4){0.f, 0.f, 0.f, 0.f};
+      v[j][1] = (c < D) ? load4<T>(xr + c + 4) : (f32x4){0.f, 0.f, 0.f, 0.f};
+      s += (v[j][0][0] + v[j][0][1]) + (v[j][0][2] + v[j][0][3]) + (v[j][1][0] + v[j][1][1]) + (v[j][1][2] + v[j][1][3]);
+    }
+    const float mean = wave_sum(s) / D;
+    float sq = 0.f;
+#pragma unroll
+    for (int j = 0; j < NR; ++j) {
+      const int c = (lane + 64 * j) * 8;
+      if (c < D) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) { const float t = v[j][h][e] - mean; sq += t * t; }
+      }
+    }
+    const float rstd = rsqrtf(wave_sum(sq) / D + 1e-5f);
+#pragma unroll
+    for (int j = 0; j < NR; ++j) {
+      const int c = (lane + 64 * j) * 8;
+      if (c < D) {
+        bf16x8 o;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const f32x4 ww = *(const f32x4*)(w + c + 4 * h), bb = *(const f32x4*)(b + c + 4 * h);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[4 * h + e] = f2bf((v[j][h][e] - mean) * rstd * ww[e] + bb[e]);
+        }
+        *(bf16x8*)(y + (long long)row * D + c) = o;
+      }
+    }
+    if (lane == 0) { mean_out[row] = mean; rstd_out[row] = rstd; }
+    return;
+  }
   f32x4 v[MAXV];
   float s = 0.f;
 #pragma unroll
@@ -209,9 +252,11 @@ SVAE_EXPORT int svae_layernorm_fwd(const void* x, int32_t x_dtype, const float* 
       hipLaunchKernelGGL((ln_fwd_kernel<bf16, MV>), grid, dim3(256), 0, s, (const bf16*)x, w, b, (bf16*)y, mean,   \
                          rstd, rows, D);                                                                           \
   } while (0)
-  if (D <= 512) SVAE_LN_FWD(2);
+  // (even MAXV = the 8-column layout, which needs D % 8 == 0 and 16-B aligned rows)
+  if (D % 8 == 0 && D <= 512) SVAE_LN_FWD(2);
+  else if (D % 8 == 0) SVAE_LN_FWD(4);
   else if (D <= 768) SVAE_LN_FWD(3);
-  else SVAE_LN_FWD(4);
+  else SVAE_LN_FWD(5);
 #undef SVAE_LN_FWD
   SVAE_LAUNCH_CHECK();
   return SVAE_OK;
