@@ -46,7 +46,7 @@ def main():
         orig_pair(g0, g1)
         e1.record()
         (a0, k0), (a1, k1) = g0, g1
-        key = ((a0[3], a1[3]), (a0[4], a1[4]), a0[5], 1, 1, k0.get('epi', 0), k0.get('splits', 1),
+        key = ((a0[3], a1[3]), (a0[4], a1[4]), (a0[5], a1[5]), 1, 1, k0.get('epi', 0), k0.get('splits', 1),
                int(k0.get('a_rowsum') is not None), 0)
         rec.append((key, e0, e1))
 
@@ -66,7 +66,7 @@ def main():
     for key, (n, us) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
         M, N_, K_, at, bt, epi, sp, rs, kwt = key
         per = us / n
-        fl = 2.0 * (sum(a * b for a, b in zip(M, N_)) if isinstance(M, tuple) else M * N_) * K_
+        fl = 2.0 * (sum(a * b * c for a, b, c in zip(M, N_, K_)) if isinstance(M, tuple) else M * N_ * K_)
         print(f'{us / steps / 1e3:7.3f} ms  x{n // steps:2d} {per:9.1f} us {fl / per / 1e6:8.1f} TF/s  '
               f'M={M} N={N_} K={K_} a_t={at} b_t={bt} epi={EPI[epi] if epi < len(EPI) else epi} splits={sp} '
               f'rowsum={rs} k_weight={kwt}')

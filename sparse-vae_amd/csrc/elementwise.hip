@@ -605,13 +605,13 @@ __global__ __launch_bounds__(256) void radam_kernel(float* __restrict__ p, bf16*
               wd = scal[7];
   const float step = lr / bcm, decay = 1.0f - lr * wd;
   const long long n4 = n / 4;   // n % 4 == 0 (checked on the host): 16-B vectors
-  auto update = [&](long long i, f32x4 gi, f32x4 mi, f32x4 vi, f32x4 pi) {
-    gi *= coef;
-    mi = mi * b1 + (1.0f - b1) * gi;
-    vi = vi * b2 + (1.0f - b2) * gi * gi;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
+    const f32x4 gi = ((const f32x4*)g)[i] * coef;
+    const f32x4 mi = ((const f32x4*)m)[i] * b1 + (1.0f - b1) * gi;
+    const f32x4 vi = ((const f32x4*)v)[i] * b2 + (1.0f - b2) * gi * gi;
     ((f32x4*)m)[i] = mi;
     ((f32x4*)v)[i] = vi;
-    pi *= decay;
+    f32x4 pi = ((const f32x4*)p)[i] * decay;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       if (rho_ok != 0.f) pi[e] -= step * (mi[e] / (sqrtf(vi[e]) / bcv + eps));
@@ -619,18 +619,7 @@ __global__ __launch_bounds__(256) void radam_kernel(float* __restrict__ p, bf16*
     }
     ((f32x4*)p)[i] = pi;
     if (pbf) ((bf16x4*)pbf)[i] = (bf16x4){f2bf(pi[0]), f2bf(pi[1]), f2bf(pi[2]), f2bf(pi[3])};
-  };
-  // two vectors per thread per iteration, all eight loads issued before either update (more bytes in flight)
-  const long long stride = (long long)gridDim.x * 256;
-  long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-  for (; i + stride < n4; i += 2 * stride) {
-    const f32x4 g0 = ((const f32x4*)g)[i], m0 = ((const f32x4*)m)[i], v0 = ((const f32x4*)v)[i], p0 = ((const f32x4*)p)[i];
-    const f32x4 g1 = ((const f32x4*)g)[i + stride], m1 = ((const f32x4*)m)[i + stride];
-    const f32x4 v1 = ((const f32x4*)v)[i + stride], p1 = ((const f32x4*)p)[i + stride];
-    update(i, g0, m0, v0, p0);
-    update(i + stride, g1, m1, v1, p1);
   }
-  if (i < n4) update(i, ((const f32x4*)g)[i], ((const f32x4*)m)[i], ((const f32x4*)v)[i], ((const f32x4*)p)[i]);
 }
 
 // In-place clip_grad_norm_ (language_model.py:120-122) for a micro-step that is not followed by an optimiser step
