@@ -1399,6 +1399,98 @@ __global__ __launch_bounds__(512, 1) void gemm256_pair_kernel(GP2 q) {
   else gemm256_run<AT, BT, EPI>(q.p[1], b - q.nb0, (int)gridDim.x - q.nb0);
 }
 
+// ===================================================================================================
+// gemm_skinny: M <= 64 rows (the encoder bottleneck layer, q(z|x), the z projections: one row per sequence).
+// A 128-row tile leaves such a GEMM to a handful of blocks that walk all of K serially (a 64 x 512 x 2048 dropout +
+// residual GEMM took 33 us). Here a block owns 32 columns, its 16 waves split K into contiguous slices (fragments
+// loaded straight from global memory, the next k-step's loads issued before the current MFMAs), the 16 partial
+// 64 x 32 tiles are summed in LDS in a fixed order and 512 threads run the epilogue (4 columns of one row each).
+// (8 waves: 20.8 us for the 64 x 512 x 2048 dropout + residual GEMM, the k-step latency chain.)
+// A [M][K] and B [N][K] K-contiguous, K % 8 == 0.
+constexpr int SK_BN = 32, SK_WAVES = 16;
+
+template <int EPI>
+__global__ __launch_bounds__(1024) void gemm_skinny_kernel(GP p) {
+  __shared__ __attribute__((aligned(16))) float red[SK_WAVES][64][SK_BN + 4];
+  const int tid = threadIdx.x, lane = tid & 63, li = lane & 15, g = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int n0 = blockIdx.x * SK_BN;
+  const int nks = (p.K + 31) / 32;                       // k-steps of 32
+  const int per = (nks + SK_WAVES - 1) / SK_WAVES;
+  const int ks0 = wave * per, ks1 = min(nks, ks0 + per);
+  f32x4 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) acc[i][0] = acc[i][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  // lane's fragment rows / columns and the k offset of its 8 elements
+  auto load = [&](int ks, bf16x8 (&a)[4], bf16x8 (&b)[2]) {
+    const int k = ks * 32 + 8 * g;
+    const bool kok = k < p.K;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = 16 * i + li;
+      u32x4 v = {0u, 0u, 0u, 0u};
+      if (kok && m < p.M) v = *(const u32x4*)(p.A + (long long)m * p.lda + k);
+      a[i] = __builtin_bit_cast(bf16x8, v);
+    }
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const int n = n0 + 16 * jj + li;
+      u32x4 v = {0u, 0u, 0u, 0u};
+      if (kok && n < p.N) v = *(const u32x4*)(p.B + (long long)n * p.ldb + k);
+      b[jj] = __builtin_bit_cast(bf16x8, v);
+    }
+  };
+  if (ks0 < ks1) {
+    bf16x8 a[4], b[2], an[4], bn[2];
+    load(ks0, a, b);
+    for (int ks = ks0; ks < ks1; ++ks) {
+      if (ks + 1 < ks1) load(ks + 1, an, bn);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) acc[i][jj] = mfma16(b[jj], a[i], acc[i][jj]);
+      if (ks + 1 < ks1) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a[i] = an[i];
+        b[0] = bn[0];
+        b[1] = bn[1];
+      }
+    }
+  }
+  // acc[i][jj]: row 16 i + li, columns 16 jj + 4 g + (0..3)
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) *(f32x4*)&red[wave][16 * i + li][16 * jj + 4 * g] = acc[i][jj];
+  __syncthreads();
+  const int row = tid >> 3, c4 = (tid & 7) * 4, m = row, n = n0 + c4;
+  if (tid >= 512 || m >= p.M || n >= p.N) return;
+  f32x4 x = *(const f32x4*)&red[0][row][c4];
+#pragma unroll
+  for (int w = 1; w < SK_WAVES; ++w) x += *(const f32x4*)&red[w][row][c4];
+  x *= p.alpha;
+  if (p.bias) x += *(const f32x4*)(p.bias + n);
+  if constexpr (EPI == SVAE_EPI_F32 || EPI == SVAE_EPI_DROPOUT_RESID) {
+    if constexpr (EPI == SVAE_EPI_DROPOUT_RESID) {
+      if (p.drop_p > 0.f) dropout4(p, x, m, n);
+    }
+    if (p.resid) x += *(const f32x4*)(p.resid + (long long)m * p.ldr + n);
+    *(f32x4*)((float*)p.C + (long long)m * p.ldc + n) = x;
+  } else if constexpr (EPI == SVAE_EPI_GELU) {
+    f32x2 g0, d0, g1, d1;
+    gelu_pair2((f32x2){x[0], x[1]}, g0, d0);
+    gelu_pair2((f32x2){x[2], x[3]}, g1, d1);
+    *(bf16x4*)((bf16*)p.C + (long long)m * p.ldc + n) = (bf16x4){f2bf(g0[0]), f2bf(g0[1]), f2bf(g1[0]), f2bf(g1[1])};
+    *(bf16x4*)((bf16*)p.aux + (long long)m * p.ldaux + n) = (bf16x4){f2bf(d0[0]), f2bf(d0[1]), f2bf(d1[0]), f2bf(d1[1])};
+  } else if constexpr (EPI == SVAE_EPI_GELU_BWD) {
+    const bf16x4 a4 = *(const bf16x4*)((const bf16*)p.aux + (long long)m * p.ldaux + n);
+    *(bf16x4*)((bf16*)p.C + (long long)m * p.ldc + n) =
+        (bf16x4){f2bf(x[0] * (float)a4[0]), f2bf(x[1] * (float)a4[1]), f2bf(x[2] * (float)a4[2]), f2bf(x[3] * (float)a4[3])};
+  } else {
+    *(bf16x4*)((bf16*)p.C + (long long)m * p.ldc + n) = (bf16x4){f2bf(x[0]), f2bf(x[1]), f2bf(x[2]), f2bf(x[3])};
+  }
+}
+
 // C[m][n] += sum over splits of slab[s][m][n] (slab rows of N floats); 4 columns per thread
 __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restrict__ slab, float* __restrict__ C,
                                                           int M, int N, long long ldc, int splits) {
@@ -1501,6 +1593,24 @@ SVAE_EXPORT int svae_gemm(const svae_gemm_desc* d, svae_stream_t stream) {
   if (nblocks > 0x7FFFFFFF) return SVAE_EINVAL;
   dim3 grid((unsigned)nblocks);
   hipStream_t s = (hipStream_t)stream;
+  // M <= 64 (one row per sequence): the skinny kernel (SVAE_GEMM_SKINNY=0 turns it off for A/B runs)
+  static const int skinny_env = [] { const char* e = getenv("SVAE_GEMM_SKINNY"); return e ? atoi(e) : 1; }();
+  if (skinny_env && d->M <= 64 && !d->a_t && !d->b_t && d->batch == 1 && d->splits == 1 && !d->a_rowsum &&
+      d->C && d->K % 8 == 0 && d->lda % 8 == 0 && d->ldb % 8 == 0 && ((uintptr_t)d->A & 15) == 0 &&
+      ((uintptr_t)d->B & 15) == 0 &&
+      (d->epi == SVAE_EPI_BF16 || d->epi == SVAE_EPI_F32 || d->epi == SVAE_EPI_GELU || d->epi == SVAE_EPI_GELU_BWD ||
+       d->epi == SVAE_EPI_DROPOUT_RESID)) {
+    const dim3 gs((unsigned)((d->N + SK_BN - 1) / SK_BN));
+    switch (d->epi) {
+      case SVAE_EPI_BF16: hipLaunchKernelGGL(gemm_skinny_kernel<SVAE_EPI_BF16>, gs, dim3(1024), 0, s, p); break;
+      case SVAE_EPI_F32: hipLaunchKernelGGL(gemm_skinny_kernel<SVAE_EPI_F32>, gs, dim3(1024), 0, s, p); break;
+      case SVAE_EPI_GELU: hipLaunchKernelGGL(gemm_skinny_kernel<SVAE_EPI_GELU>, gs, dim3(1024), 0, s, p); break;
+      case SVAE_EPI_GELU_BWD: hipLaunchKernelGGL(gemm_skinny_kernel<SVAE_EPI_GELU_BWD>, gs, dim3(1024), 0, s, p); break;
+      default: hipLaunchKernelGGL(gemm_skinny_kernel<SVAE_EPI_DROPOUT_RESID>, gs, dim3(1024), 0, s, p); break;
+    }
+    SVAE_LAUNCH_CHECK();
+    return SVAE_OK;
+  }
   const int lay = (d->a_t ? 2 : 0) | (d->b_t ? 1 : 0);
   // short-K GEMMs: the 3-stage LDS-DMA kernel (3 blocks/CU overlap prologues/epilogues); long-K GEMMs: the
   // BK=64 register-staged kernel (half the barriers per MFMA). SVAE_GEMM_IMPL=1/2 forces one (A/B runs).

@@ -164,6 +164,47 @@ def test_gemm_epilogues(M, Nn, Kk):
     assert agree.all()
 
 
+@pytest.mark.parametrize('M,Nn,Kk', [(64, 512, 2048), (37, 520, 72), (1, 2048, 512), (64, 512, 64)])
+def test_gemm_skinny_epilogues(M, Nn, Kk):
+    # M <= 64: the K-split skinny kernel (one row per sequence: encoder bottleneck, q(z|x), z projections)
+    torch.manual_seed(M + Nn + Kk)
+    Ai = torch.randint(-2, 3, (M, Kk), device=dev).float()
+    Bi = torch.randint(-2, 3, (Nn, Kk), device=dev).float()
+    C32 = torch.empty(M, Nn, device=dev)
+    K.gemm(Ai.bfloat16(), Bi.bfloat16(), C32, M, Nn, Kk, epi=N.EPI_F32)
+    torch.cuda.synchronize()
+    assert torch.equal(C32, Ai @ Bi.t())
+    X = torch.randn(M, Kk, device=dev).bfloat16()
+    W = (torch.randn(Nn, Kk, device=dev) * 0.1).bfloat16()
+    b = torch.randn(Nn, device=dev)
+    acc = X.float() @ W.float().t()
+    ref = acc + b
+    C = torch.empty(M, Nn, device=dev, dtype=torch.bfloat16)
+    K.gemm(X, W, C, M, Nn, Kk, epi=N.EPI_BF16, bias=b)
+    assert _rel(C, ref) < 4e-3
+    gp = torch.empty_like(C)
+    K.gemm(X, W, C, M, Nn, Kk, epi=N.EPI_GELU, bias=b, aux=gp, ldaux=Nn)
+    r = ref.clone().requires_grad_()
+    F.gelu(r).backward(torch.ones_like(r))
+    assert _rel(C, F.gelu(ref)) < 4e-3 and _rel(gp, r.grad) < 4e-3
+    G = torch.empty_like(C)
+    K.gemm(X, W, G, M, Nn, Kk, epi=N.EPI_GELU_BWD, aux=gp, ldaux=Nn)
+    assert _rel(G, acc * gp.float()) < 4e-3
+    R = torch.randn(M, Nn, device=dev)
+    K.gemm(X, W, C32, M, Nn, Kk, epi=N.EPI_F32, bias=b, resid=R, ldr=Nn)
+    assert _rel(C32, ref + R) < 1e-5
+    K.gemm(X, W, C32, M, Nn, Kk, epi=N.EPI_DROPOUT_RESID, resid=R, ldr=Nn, drop_p=0.25, seed=7)
+    gb = torch.empty(M, Nn, device=dev, dtype=torch.bfloat16)
+    K.dropout_bwd_cast(torch.ones(M, Nn, device=dev), gb, 0.25, 7, M, Nn)
+    keep = gb.float() != 0
+    assert torch.allclose((C32 - R)[keep], (acc / 0.75)[keep], rtol=1e-4, atol=1e-4)
+    assert torch.allclose((C32 - R)[~keep], torch.zeros_like(R)[~keep], atol=1e-6)
+    # strided f32 output rows (the z splice writes row 0 of every sequence: ldc = L * d)
+    Cs = torch.zeros(M, 2 * Nn, device=dev)
+    K.gemm(X, W, Cs, M, Nn, Kk, epi=N.EPI_F32, bias=b, ldc=2 * Nn)
+    assert _rel(Cs[:, :Nn], ref) < 1e-5 and torch.all(Cs[:, Nn:] == 0)
+
+
 @pytest.mark.parametrize('M,Nn,Kk', [(8200, 2056, 520), (8192, 2048, 512)])
 def test_gemm_many_tiles_epilogues(M, Nn, Kk):
     # >= 512 tiles of 256 x 128: the shapes gemm_ov takes when enabled (SVAE_GEMM_OV=1; ragged M, N, K in the first)
