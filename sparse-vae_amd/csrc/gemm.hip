@@ -1154,20 +1154,9 @@ __device__ __forceinline__ void gemm256_run(const GP& p, int blk, int nwg) {
     else xb = g3_src_k(p.ldb, X.n0, p.N, wave, lane);
   };
   srcs(T, sa, sb);
-  // ACC_KW: wave 0 also DMAs the K-tile's 64 k_weight floats into the side ring (sstat, [2][64]) with the tile, so
-  // the weighted row sums read them from LDS behind the same counted wait + barrier (no scalar loads in the loop)
-  auto issue_kw = [&](const G3Tile& X, int k0, int parity) {
-    if constexpr (EPI == G3_EPI_ACC_KW) {
-      if (wave == 0 && p.a_rowsum && X.bn < 2) {
-        const u32x4 rs = buffer_rsrc(p.k_weight + k0, 0x7FFFFFF0u);
-        dma4_lds(rs, sstat + parity * 64, k0 + lane < X.kend ? lane * 4 : 0x7FFFFFF0);
-      }
-    }
-  };
   int g = 0;   // K-tiles consumed so far by this block: the stage of K-tile g is g & 1
   if (T.nk > 0) {
     g3_issue<AT, BT>(p, T.A, T.B, sa, sb, T.m0, T.n0, T.kbeg, T.kend, smem, wave);
-    issue_kw(T, T.kbeg, 0);
   }
   if (p.desync > 0 && (bid & 1)) {   // stagger the epilogues of neighbouring blocks (HBM write bursts)
     for (int i = 0; i < p.desync; ++i) __builtin_amdgcn_s_sleep(127);
@@ -1196,16 +1185,15 @@ __device__ __forceinline__ void gemm256_run(const GP& p, int blk, int nwg) {
       const char* la = smem + (g & 1) * G3_STAGE;
       const char* lb = la + G3_T;
       char* nxt = smem + ((g + 1) & 1) * G3_STAGE;
+      const bool do_rs = AT && p.a_rowsum && T.bn < 2;
       if (kt + 1 < T.nk) {
         g3_issue<AT, BT>(p, T.A, T.B, sa, sb, T.m0, T.n0, T.kbeg + (kt + 1) * 64, T.kend, nxt, wave);
-        issue_kw(T, T.kbeg + (kt + 1) * 64, (g + 1) & 1);
       } else if (has_next) {   // the next tile's first K-tile, in flight during this tile's epilogue
         const G3Tile TN = g3_tile(p, t3n);
         if (TN.nk > 0) {
           G3Src xa, xb;
           srcs(TN, xa, xb);
           g3_issue<AT, BT>(p, TN.A, TN.B, xa, xb, TN.m0, TN.n0, TN.kbeg, TN.kend, nxt, wave);
-          issue_kw(TN, TN.kbeg, (g + 1) & 1);
         }
       }
       // Quadrant walk (mh, nh) = (0,0) (0,1) (1,1) (1,0): A fragments of a half reused by two quadrants, B
@@ -1215,20 +1203,23 @@ __device__ __forceinline__ void gemm256_run(const GP& p, int blk, int nwg) {
       // AT: sum_k A[m][k] (* k_weight[k]) from the A fragments already in registers (no extra LDS reads): lane l of
       // a fragment holds row 16i + (l & 15), k = 32 ks + 8 (l >> 4) + (0..7); column wave wc takes row groups
       // 2 wc, 2 wc + 1 of its wave row's eight (balanced over the SIMDs; a0's right after their last MFMA use),
-      // summed over the lane groups at the end of the tile. ACC_KW: the K-tile's 64 weights arrived with its DMA
-      // into the side ring, stage g & 1. The first two column tiles (blocks bn = 0, 1 hold the same A rows) split
+      // summed over the lane groups at the end of the tile. ACC_KW: the lane's 8 weights per k-step are global loads
+      // at the use (L2-resident; the wait for them also covers the next K-tile's DMA pieces issued before them). Two
+      // cheaper schemes were wrong or slower: a side ring in LDS filled by wave 0's DMA read stale weights now and then
+      // (a bit-exact test of the k-weighted sums failed 1 run in ~8), and registers loaded a K-tile ahead spilled
+      // (34 VGPRs; head dW 1129 -> 1691 us). The first two column tiles (blocks bn = 0, 1 hold the same A rows) split
       // the work by k-step, so neither runs much longer than the blocks without row sums.
-      const bool do_rs = AT && p.a_rowsum && T.bn < 2;
       const int ks0 = p.tn2 >= 2 ? T.bn : 0, ks1 = p.tn2 >= 2 ? T.bn + 1 : 2;
       auto rowsum2 = [&](const bf16x8 (&x)[2], const bf16x8 (&y)[2]) {
-        const float* kws = sstat + (g & 1) * 64 + 8 * (lane >> 4);
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
           if (ks < ks0 || ks >= ks1) continue;   // (block-uniform)
           f32x4 k0 = {1.f, 1.f, 1.f, 1.f}, k1 = k0;
           if constexpr (EPI == G3_EPI_ACC_KW) {
-            k0 = *(const f32x4*)(kws + 32 * ks);
-            k1 = *(const f32x4*)(kws + 32 * ks + 4);
+            const int kk = T.kbeg + kt * 64 + 32 * ks + 8 * (lane >> 4);   // (K % 8 == 0: 8 inside or 8 past)
+            const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+            k0 = kk < T.kend ? *(const f32x4*)(p.k_weight + kk) : z4;
+            k1 = kk < T.kend ? *(const f32x4*)(p.k_weight + kk + 4) : z4;
           }
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
@@ -1373,7 +1364,6 @@ __device__ __forceinline__ void gemm256_run(const GP& p, int blk, int nwg) {
     srcs(T, sa, sb);
     if (!prefetched && T.nk > 0) {   // (an empty split-K slice prefetched nothing)
       g3_issue<AT, BT>(p, T.A, T.B, sa, sb, T.m0, T.n0, T.kbeg, T.kend, smem + (g & 1) * G3_STAGE, wave);
-      issue_kw(T, T.kbeg, g & 1);
     }
   }
 }

@@ -48,22 +48,28 @@ def test_gemm_split_k_atomic_and_acc():
     assert torch.equal(C, 1 + 2 * (A.t() @ B))
 
 
-def test_gemm256_at_kcontig_b_exact():
-    """a_t with a K-contiguous B on the 256x256 kernel (the vocabulary head's dW layout with B = (r hh)^T): f32
-    accumulate, plain and k-weighted row sums, bit-exact on integer data."""
+@pytest.mark.parametrize('b_t', [True, False])
+def test_gemm256_at_rowsum_k_weight_exact(b_t):
+    """a_t on the 256x256 kernel with both B layouts (the vocabulary head's dW: MN-contiguous B; or K-contiguous):
+    f32 accumulate with plain and k-weighted row sums, bit-exact on integer data, repeated (the k-weighted sums once
+    mismatched in a DMA-order experiment)."""
     g = torch.Generator(device=dev).manual_seed(5)
     Kk, M, Nn = 2048, 16384, 776   # 64 x 4 = 256 tiles (>= 192: gemm256 with and without k_weight), ragged N
     A = torch.randint(-2, 3, (Kk, M), device=dev, generator=g).float()
     B = torch.randint(-2, 3, (Kk, Nn), device=dev, generator=g).float()
     kw = torch.randint(-2, 3, (Kk,), device=dev, generator=g).float()
-    for use_kw in (False, True, True, True):   # (k-weighted row sums repeated: a DMA-order experiment raced there)
+    Bs = (B if b_t else B.t().contiguous()).bfloat16()
+    ref_c = 1 + A.t() @ B
+    for use_kw in (False, True, True, True, True):
         C = torch.ones(M, Nn, device=dev)
         rs = torch.full((M,), 3.0, device=dev)
-        K.gemm(A.bfloat16(), B.t().contiguous().bfloat16(), C, M, Nn, Kk, a_t=True, b_t=False, ldb=Kk,
+        K.gemm(A.bfloat16(), Bs, C, M, Nn, Kk, a_t=True, b_t=b_t, ldb=Nn if b_t else Kk,
                epi=N.EPI_F32_ACC, a_rowsum=rs, k_weight=kw if use_kw else None)
         torch.cuda.synchronize()
-        assert torch.equal(C, 1 + A.t() @ B)
-        assert torch.equal(rs, 3 + (A * kw[:, None]).sum(0) if use_kw else 3 + A.sum(0))
+        assert torch.equal(C, ref_c)
+        ref = 3 + ((A * kw[:, None]).sum(0) if use_kw else A.sum(0))
+        bad = (rs != ref).nonzero().flatten()
+        assert bad.numel() == 0, (use_kw, bad[:16].tolist(), (rs - ref)[bad[:16]].tolist())
 
 
 def test_gemm256_split_k_rowsum_exact():
