@@ -222,13 +222,22 @@ int svae_ce_grad(void* logits, int64_t ld, const float* lse, const float* chunk_
  * ce_prob_finalize: part f32 [ntile][rows] (the per-tile sums of P) -> lse = c + log sum, row_loss = lse - c,
  *   chunk_w, nll_out: the chunked mean of means of svae_ce_finalize.
  * ce_prob_bwd_prep: r_out, q_out [rows]; hh_out bf16 [rows][D] = r * hh; dbias[label] -= q (atomics; may be NULL).
- * Exact while every labelled row's logits stay below its label logit + 88 (a token loss < 88 nats): beyond, the
- * exponent saturates at 2^127. */
+ * The GEMM caps the exponent at 2^127 (a logit more than 88 nats above the label logit); ce_prob_finalize_fix
+ * finds every labelled row whose sum of P reaches 2^100 (or is not finite), lists it in sat_ws (int32 [1 + rows]:
+ * count, then rows; the count stays readable after the call) and recomputes it exactly: the row's logits from hh, W
+ * and bias, P[row] = exp(logit - max) (bf16, into P with leading dimension ldp), lse = max + log sum, row_loss =
+ * lse - c, and row_off[row] = max -- so the backward (which reads P, row_off and lse) stays consistent.
+ * ce_prob_finalize = ce_prob_finalize_fix without the check (sat_ws = NULL). */
 int svae_ce_label_logit(const void* hh, int64_t ldh, const void* W, int64_t ldw, const float* bias,
                         const int32_t* labels, int32_t rows, int32_t D, float* out, svae_stream_t stream);
 int svae_ce_prob_finalize(const float* part, int32_t ntile, const float* row_off, const int32_t* labels,
                           int32_t rows, int32_t seq, int32_t nchunks, int32_t chunk_len, float* lse, float* row_loss,
                           float* chunk_w, float* nll_out, float* red_ws, svae_stream_t stream);
+int svae_ce_prob_finalize_fix(const float* part, int32_t ntile, float* row_off, const int32_t* labels, int32_t rows,
+                              int32_t seq, int32_t nchunks, int32_t chunk_len, float* lse, float* row_loss,
+                              float* chunk_w, float* nll_out, float* red_ws, const void* hh, int64_t ldh, const void* W,
+                              int64_t ldw, const float* bias, void* P, int64_t ldp, int32_t V, int32_t D,
+                              int32_t* sat_ws, svae_stream_t stream);
 int svae_ce_prob_bwd_prep(const void* hh, int64_t ldh, const float* lse, const float* row_off, const float* chunk_w,
                           const int32_t* labels, const float* gscale, int32_t rows, int32_t seq, int32_t nchunks,
                           int32_t chunk_len, int32_t D, void* hh_out, float* r_out, float* q_out, float* dbias,

@@ -58,47 +58,73 @@ __global__ __launch_bounds__(256) void emb_bwd_ce_kernel(const int* __restrict__
 }
 
 // ------------------------------------------------------------------ reparameterise + KL
-// One wave per sample (latent index on the lane); one block of 4 waves walks all samples so the batch
-// means come out of the same launch.
-__global__ __launch_bounds__(256) void reparam_fwd_kernel(const float* __restrict__ stats, const float* __restrict__ eps_in,
-                                                          unsigned long long seed, const long long* __restrict__ ntok,
-                                                          float* __restrict__ z, bf16* __restrict__ z_bf,
-                                                          float* __restrict__ eps_out, float* __restrict__ raw_kl,
-                                                          float* __restrict__ kl_out, int B, int Z) {
-  __shared__ float red[2][4];
+// One block of 16 waves; wave w takes samples w, w + 16, ... (latent index on the lane), 4 samples' loads in flight
+// per wave, so B = 64 is one pass of 16 waves instead of 16 dependent iterations of 4 (21 -> ~4 us); the batch means
+// come out of the same launch (a fixed-order sum over the waves' partials: deterministic).
+constexpr int REPARAM_WAVES = 16;
+
+__global__ __launch_bounds__(1024) void reparam_fwd_kernel(const float* __restrict__ stats, const float* __restrict__ eps_in,
+                                                           unsigned long long seed, const long long* __restrict__ ntok,
+                                                           float* __restrict__ z, bf16* __restrict__ z_bf,
+                                                           float* __restrict__ eps_out, float* __restrict__ raw_kl,
+                                                           float* __restrict__ kl_out, int B, int Z) {
+  __shared__ float red[2][REPARAM_WAVES];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float acc_norm = 0.f, acc_raw = 0.f;
-  for (int b = wave; b < B; b += 4) {
-    float klsum = 0.f;
+  constexpr int NB = 4;                       // samples per wave in flight
+  for (int b0 = wave; b0 < B; b0 += NB * REPARAM_WAVES) {
+    float klsum[NB];
+#pragma unroll
+    for (int k = 0; k < NB; ++k) klsum[k] = 0.f;
     for (int j = lane; j < Z; j += 64) {
-      const float mu = stats[(long long)b * 2 * Z + j];
-      const float lv = stats[(long long)b * 2 * Z + Z + j];
-      const float var = __expf(lv);
-      const float sd = sqrtf(var);
-      float e;
-      if (eps_in) {
-        e = eps_in[(long long)b * Z + j];
-      } else {  // Box-Muller over two counter-based uniforms
-        const unsigned long long idx = ((unsigned long long)b * Z + j) * 2ull;
-        const float u1 = rand_uniform(seed, idx), u2 = rand_uniform(seed, idx + 1);
-        e = sqrtf(-2.f * __logf(u1)) * __cosf(6.283185307179586f * u2);
+      float mu[NB], lv[NB], e[NB];
+#pragma unroll
+      for (int k = 0; k < NB; ++k) {
+        const int b = b0 + k * REPARAM_WAVES;
+        if (b < B) {
+          mu[k] = stats[(long long)b * 2 * Z + j];
+          lv[k] = stats[(long long)b * 2 * Z + Z + j];
+          if (eps_in) {
+            e[k] = eps_in[(long long)b * Z + j];
+          } else {  // Box-Muller over two counter-based uniforms
+            const unsigned long long idx = ((unsigned long long)b * Z + j) * 2ull;
+            const float u1 = rand_uniform(seed, idx), u2 = rand_uniform(seed, idx + 1);
+            e[k] = sqrtf(-2.f * __logf(u1)) * __cosf(6.283185307179586f * u2);
+          }
+        }
       }
-      if (eps_out) eps_out[(long long)b * Z + j] = e;
-      const float zz = mu + e * sd;
-      z[(long long)b * Z + j] = zz;
-      if (z_bf) z_bf[(long long)b * Z + j] = f2bf(zz);
-      klsum += 0.5f * (mu * mu + var - lv - 1.0f);
+#pragma unroll
+      for (int k = 0; k < NB; ++k) {
+        const int b = b0 + k * REPARAM_WAVES;
+        if (b < B) {
+          const float var = __expf(lv[k]);
+          const float zz = mu[k] + e[k] * sqrtf(var);
+          if (eps_out) eps_out[(long long)b * Z + j] = e[k];
+          z[(long long)b * Z + j] = zz;
+          if (z_bf) z_bf[(long long)b * Z + j] = f2bf(zz);
+          klsum[k] += 0.5f * (mu[k] * mu[k] + var - lv[k] - 1.0f);
+        }
+      }
     }
-    klsum = wave_sum(klsum);
-    if (lane == 0) raw_kl[b] = klsum;
-    acc_raw += klsum;
-    acc_norm += klsum / (float)ntok[b];
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+      const int b = b0 + k * REPARAM_WAVES;
+      if (b < B) {                            // wave-uniform
+        const float ks = wave_sum(klsum[k]);
+        if (lane == 0) raw_kl[b] = ks;
+        acc_raw += ks;
+        acc_norm += ks / (float)ntok[b];
+      }
+    }
   }
   if (lane == 0) { red[0][wave] = acc_norm; red[1][wave] = acc_raw; }
   __syncthreads();
   if (threadIdx.x == 0) {
-    kl_out[0] = (red[0][0] + red[0][1] + red[0][2] + red[0][3]) / B;
-    kl_out[1] = (red[1][0] + red[1][1] + red[1][2] + red[1][3]) / B;
+    float n = 0.f, r = 0.f;
+#pragma unroll
+    for (int w = 0; w < REPARAM_WAVES; ++w) { n += red[0][w]; r += red[1][w]; }
+    kl_out[0] = n / B;
+    kl_out[1] = r / B;
   }
 }
 
@@ -177,9 +203,13 @@ __global__ __launch_bounds__(256) void ce_label_logit_kernel(const bf16* __restr
 // part is tile-major [ntile][rows]. Block = 32 rows x 8 tile slices (thread (r, s) sums tiles s, s + 8, ..., 8 loads in
 // flight), the 8 slice sums combined in LDS in a fixed order. (One thread per row walking all 256 tiles: 512 waves
 // on the chip, 37.6 us at C2.)
+// A labelled row whose sum reaches 2^100 (a logit more than ~69 nats above the label logit, or a non-finite one) is
+// appended to sat[1..] (count in sat[0]) for ce_prob_fixup: the GEMM epilogue caps the exponent at 2^127, so such a
+// row's P and lse are recomputed with the row maximum as the offset instead of being silently clipped.
 __global__ __launch_bounds__(256) void ce_prob_rows_kernel(const float* __restrict__ part, int ntile,
                                                            const float* __restrict__ off, const int* __restrict__ labels,
-                                                           int rows, float* __restrict__ lse, float* __restrict__ row_loss) {
+                                                           int rows, float* __restrict__ lse, float* __restrict__ row_loss,
+                                                           int* __restrict__ sat) {
   __shared__ float red[8][33];
   const int r = threadIdx.x & 31, sl = threadIdx.x >> 5;
   const int row = blockIdx.x * 32 + r;
@@ -204,6 +234,66 @@ __global__ __launch_bounds__(256) void ce_prob_rows_kernel(const float* __restri
   const float l = live ? __logf(se) : 0.f;
   lse[row] = live ? off[row] + l : 0.f;
   row_loss[row] = l;
+  if (sat && live && !(se < 0x1p100f)) sat[1 + atomicAdd(sat, 1)] = row;
+}
+
+// The rows ce_prob_rows flagged, one block per row (blocks stride over the list; an empty list costs one launch):
+// logit = hh . W[col] + bias[col] over the whole vocabulary (bf16 operands, f32 accumulation, as the GEMM), m = the
+// row maximum; P[row] = exp(logit - m) (bf16), lse = m + log sum, row_loss = lse - c (c = the label logit, the old
+// offset), and the offset becomes m, so the backward's r = q exp(off - lse) stays consistent with the new P.
+__global__ __launch_bounds__(256) void ce_prob_fixup_kernel(const int* __restrict__ sat, const bf16* __restrict__ hh,
+                                                            long long ldh, const bf16* __restrict__ W, long long ldw,
+                                                            const float* __restrict__ bias, bf16* __restrict__ P,
+                                                            long long ldp, int V, int D, float* __restrict__ off,
+                                                            float* __restrict__ lse, float* __restrict__ row_loss) {
+  __shared__ float h[1024];
+  __shared__ float red[4];
+  const int n = sat[0];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int i = blockIdx.x; i < n; i += gridDim.x) {
+    const int row = sat[1 + i];
+    __syncthreads();
+    for (int c = threadIdx.x; c < D; c += 256) h[c] = (float)hh[(long long)row * ldh + c];
+    __syncthreads();
+    float mx = -INFINITY;
+    for (int col = threadIdx.x; col < V; col += 256) {
+      const bf16* wr = W + (long long)col * ldw;
+      float acc = 0.f;
+      for (int c = 0; c < D; c += 8) {
+        const bf16x8 b = *(const bf16x8*)(wr + c);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc = fmaf(h[c + e], (float)b[e], acc);
+      }
+      mx = fmaxf(mx, acc + (bias ? bias[col] : 0.f));
+    }
+    mx = wave_max(mx);
+    if (lane == 0) red[w] = mx;
+    __syncthreads();
+    mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    __syncthreads();
+    float se = 0.f;
+    for (int col = threadIdx.x; col < V; col += 256) {
+      const bf16* wr = W + (long long)col * ldw;
+      float acc = 0.f;
+      for (int c = 0; c < D; c += 8) {
+        const bf16x8 b = *(const bf16x8*)(wr + c);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc = fmaf(h[c + e], (float)b[e], acc);
+      }
+      const float p = __expf(acc + (bias ? bias[col] : 0.f) - mx);
+      P[(long long)row * ldp + col] = f2bf(p);
+      se += p;
+    }
+    se = wave_sum(se);
+    if (lane == 0) red[w] = se;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const float l = mx + __logf(red[0] + red[1] + red[2] + red[3]);
+      row_loss[row] = l - off[row];
+      lse[row] = l;
+      off[row] = mx;
+    }
+  }
 }
 
 // Backward prologue of the P-head, one wave per row: q = g * w_chunk, r = q * exp(c - lse) (0 for ignored rows),
@@ -723,13 +813,33 @@ SVAE_EXPORT int svae_ce_prob_finalize(const float* part, int32_t ntile, const fl
                                       int32_t rows, int32_t seq, int32_t nchunks, int32_t chunk_len, float* lse,
                                       float* row_loss, float* chunk_w, float* nll_out, float* red_ws,
                                       svae_stream_t stream) {
+  return svae_ce_prob_finalize_fix(part, ntile, (float*)row_off, labels, rows, seq, nchunks, chunk_len, lse, row_loss,
+                                   chunk_w, nll_out, red_ws, nullptr, 0, nullptr, 0, nullptr, nullptr, 0, 0, 0, nullptr,
+                                   stream);
+}
+
+SVAE_EXPORT int svae_ce_prob_finalize_fix(const float* part, int32_t ntile, float* row_off, const int32_t* labels,
+                                          int32_t rows, int32_t seq, int32_t nchunks, int32_t chunk_len, float* lse,
+                                          float* row_loss, float* chunk_w, float* nll_out, float* red_ws,
+                                          const void* hh, int64_t ldh, const void* W, int64_t ldw, const float* bias,
+                                          void* P, int64_t ldp, int32_t V, int32_t D, int32_t* sat_ws,
+                                          svae_stream_t stream) {
   if (!part || !row_off || !labels || !lse || !row_loss || !chunk_w || !nll_out || !red_ws) return SVAE_EINVAL;
   if (rows <= 0 || ntile <= 0 || seq <= 0 || rows % seq || nchunks <= 0 || nchunks > CE_MAX_CHUNKS ||
       chunk_len <= 0 || (long long)(nchunks - 1) * chunk_len >= seq)
     return SVAE_EINVAL;
+  const bool fix = sat_ws != nullptr;
+  if (fix && (!hh || !W || !P || V <= 0 || D <= 0 || D > 1024 || D % 8 || ldh % 8 || ldw % 8 ||
+              (((uintptr_t)hh | (uintptr_t)W) & 15)))
+    return SVAE_EINVAL;
   hipStream_t s = (hipStream_t)stream;
+  if (fix && hipMemsetAsync(sat_ws, 0, sizeof(int32_t), s) != hipSuccess) return SVAE_ELAUNCH;
   hipLaunchKernelGGL(ce_prob_rows_kernel, dim3((rows + 31) / 32), dim3(256), 0, s, part, ntile, row_off, labels, rows,
-                     lse, row_loss);
+                     lse, row_loss, (int*)sat_ws);
+  if (fix)
+    hipLaunchKernelGGL(ce_prob_fixup_kernel, dim3(64), dim3(256), 0, s, (const int*)sat_ws, (const bf16*)hh,
+                       (long long)ldh, (const bf16*)W, (long long)ldw, bias, (bf16*)P, (long long)ldp, V, D, row_off,
+                       lse, row_loss);
   hipLaunchKernelGGL(ce_reduce_part_kernel, dim3(CE_RED_BLOCKS, nchunks), dim3(256), 0, s, row_loss, labels,
                      (const float*)nullptr, rows, seq, nchunks, chunk_len, red_ws);
   hipLaunchKernelGGL(ce_reduce_final_kernel, dim3(1), dim3(256), 0, s, red_ws, nchunks, chunk_w, nll_out);
@@ -755,7 +865,7 @@ SVAE_EXPORT int svae_reparam_kl_fwd(const float* stats, const float* eps, uint64
                                     void* z_bf, float* eps_out, float* raw_kl, float* kl_out, int32_t B, int32_t Z,
                                     svae_stream_t stream) {
   if (!stats || !ntok || !z || !raw_kl || !kl_out || B <= 0 || Z <= 0) return SVAE_EINVAL;
-  hipLaunchKernelGGL(reparam_fwd_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, stats, eps, seed,
+  hipLaunchKernelGGL(reparam_fwd_kernel, dim3(1), dim3(64 * REPARAM_WAVES), 0, (hipStream_t)stream, stats, eps, seed,
                      (const long long*)ntok, z, (bf16*)z_bf, eps_out, raw_kl, kl_out, B, Z);
   SVAE_LAUNCH_CHECK();
   return SVAE_OK;

@@ -92,6 +92,9 @@ _SIGS = {
                             c_void_p],
     'svae_ce_prob_finalize': [c_void_p, c_int32, c_void_p, c_void_p, c_int32, c_int32, c_int32, c_int32, c_void_p,
                               c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+    'svae_ce_prob_finalize_fix': [c_void_p, c_int32, c_void_p, c_void_p, c_int32, c_int32, c_int32, c_int32, c_void_p,
+                                  c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p,
+                                  c_void_p, c_int64, c_int32, c_int32, c_void_p, c_void_p],
     'svae_ce_prob_bwd_prep': [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32,
                               c_int32, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     'svae_embedding_bwd_ce': [c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_int32, c_void_p, c_void_p, c_void_p],

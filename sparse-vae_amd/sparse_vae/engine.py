@@ -581,7 +581,11 @@ class VAEEngine:
             e1.record()
             probe.append((e0, e1))
         if head == 'prob':
-            K.ce_prob_finalize(part, ntile, coff, labels, T, L, nchunks, chunk_len, lse, row_loss, chunk_w, nll)
+            # rows whose P saturated (a logit > 88 nats above the label's) are recomputed exactly; their count
+            # stays in ce_sat[0] (out['ce_saturated'])
+            sat = ws.get('ce.sat', (T + 1,), torch.int32)
+            K.ce_prob_finalize(part, ntile, coff, labels, T, L, nchunks, chunk_len, lse, row_loss, chunk_w, nll,
+                               fix=(hh, W, bias, logits, sat))
         else:
             K.ce_finalize(part, ntile, lab_logit, labels, T, L, nchunks, chunk_len, lse, row_loss, chunk_w, nll)
         sv.update(xf=xf, gp0=gp0, h0=h0, hh=hh, ln_h=ln_h, logits=logits, lse=lse, chunk_w=chunk_w,
@@ -591,7 +595,8 @@ class VAEEngine:
         self.saved = sv
         return {'loss': loss, 'nll': nll[0], 'kl': kl[0], 'train_kl': kl[1], 'raw_kl': raw_kl,
                 'mu': stats[:, :Z], 'logvar': stats[:, Z:], 'stats': stats, 'kl_buf': kl, 'z': zf, 'eps': eps_buf,
-                'logits': logits if need_logits else None}
+                'logits': logits if need_logits else None,
+                'ce_saturated': sat[0] if head == 'prob' else None}
 
     def weighted_nll(self, tok_w):
         """robust_cross_entropy(logits, labels, weight=tok_w) of the last forward (language_model.py:106-110, the

@@ -295,12 +295,25 @@ def ce_label_logit(hh, W, bias, labels, rows, D, out):
                                   rows, D, out.data_ptr(), stream()), 'svae_ce_label_logit')
 
 
-def ce_prob_finalize(part, ntile, row_off, labels, rows, seq, nchunks, chunk_len, lse, row_loss, chunk_w, nll):
+def ce_prob_finalize(part, ntile, row_off, labels, rows, seq, nchunks, chunk_len, lse, row_loss, chunk_w, nll,
+                     fix=None):
+    """fix = (hh, W, bias, P, sat_ws): recompute the rows whose P saturated (svae_ce_prob_finalize_fix); sat_ws
+    int32 [1 + rows] holds their count (and rows) afterwards."""
     assert chunk_w.numel() >= nchunks and chunk_w.dtype == f32
     red = ce_red_ws(part.device, nchunks)
-    check(lib.svae_ce_prob_finalize(part.data_ptr(), ntile, row_off.data_ptr(), labels.data_ptr(), rows, seq, nchunks,
-                                    chunk_len, lse.data_ptr(), row_loss.data_ptr(), chunk_w.data_ptr(),
-                                    nll.data_ptr(), red.data_ptr(), stream()), 'svae_ce_prob_finalize')
+    if fix is None:
+        check(lib.svae_ce_prob_finalize(part.data_ptr(), ntile, row_off.data_ptr(), labels.data_ptr(), rows, seq,
+                                        nchunks, chunk_len, lse.data_ptr(), row_loss.data_ptr(), chunk_w.data_ptr(),
+                                        nll.data_ptr(), red.data_ptr(), stream()), 'svae_ce_prob_finalize')
+        return
+    hh, W, bias, P, sat = fix
+    _dev(hh, W, P, sat)
+    assert sat.dtype == torch.int32 and sat.numel() >= rows + 1 and P.shape[0] >= rows
+    check(lib.svae_ce_prob_finalize_fix(part.data_ptr(), ntile, row_off.data_ptr(), labels.data_ptr(), rows, seq,
+                                        nchunks, chunk_len, lse.data_ptr(), row_loss.data_ptr(), chunk_w.data_ptr(),
+                                        nll.data_ptr(), red.data_ptr(), hh.data_ptr(), hh.stride(0), W.data_ptr(),
+                                        W.stride(0), ptr(bias), P.data_ptr(), P.stride(0), W.shape[0], hh.shape[1],
+                                        sat.data_ptr(), stream()), 'svae_ce_prob_finalize_fix')
 
 
 def ce_prob_bwd_prep(hh, lse, row_off, chunk_w, labels, gscale, rows, seq, nchunks, chunk_len, D, hh_out, r_out,

@@ -53,7 +53,9 @@ class Trainer:
                  log_every_n_steps: int = 50, val_check_interval=1.0, limit_val_batches=None, gpus=None,
                  precision='bf16', **unused):
         self.max_steps = max_steps
-        self.max_epochs = max_epochs
+        # Lightning's default: 1000 epochs when neither limit is set (the cosine schedule's KeyboardInterrupt
+        # usually ends training first)
+        self.max_epochs = 1000 if max_epochs is None and (max_steps is None or max_steps <= 0) else max_epochs
         self.accumulate_grad_batches = max(1, int(accumulate_grad_batches))
         self.log_every_n_steps = log_every_n_steps
         self.val_check_interval = val_check_interval
@@ -80,17 +82,32 @@ class Trainer:
 
     @torch.no_grad()
     def validate(self, model):
+        """Mean of the val_* values over the validation batches (and, under data parallelism, over the ranks'
+        batches). The training values logged before it are restored afterwards, so the next training log line
+        carries no val_* key."""
         dm = self.datamodule
+        saved = dict(model.logged)
         sums, count = {}, 0
-        for j, batch in enumerate(dm.val_dataloader()):
-            if self.limit_val_batches is not None and j >= int(self.limit_val_batches):
-                break
+        try:
+            for j, batch in enumerate(dm.val_dataloader()):
+                if self.limit_val_batches is not None and j >= int(self.limit_val_batches):
+                    break
+                model.logged.clear()
+                model.validation_step(batch, j)
+                for k, v in model.logged.items():
+                    if k.startswith('val_'):
+                        sums[k] = sums.get(k, 0.0) + float(_scalar(v))
+                count += 1
+        finally:
             model.logged.clear()
-            model.validation_step(batch, j)
-            for k, v in model.logged.items():
-                if k.startswith('val_'):
-                    sums[k] = sums.get(k, 0.0) + float(_scalar(v))
-            count += 1
+            model.logged.update(saved)
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            keys = sorted(sums)
+            t = torch.tensor([sums[k] for k in keys] + [float(count)], dtype=torch.float64,
+                             device=model.device if dist.get_backend() == 'nccl' else 'cpu')
+            dist.all_reduce(t)
+            sums = {k: float(t[i]) for i, k in enumerate(keys)}
+            count = int(round(float(t[-1])))
         logs = {k: v / max(count, 1) for k, v in sums.items()}
         logs['step'] = self.global_step
         logs['val_batches'] = count
@@ -143,6 +160,9 @@ class Trainer:
                         opt.zero_grad()
                         micro = 0
                         self.global_step += 1
+                        model.logged['loss'] = out['loss'].detach()
+                        if world > 1 and hasattr(model, 'reduce_logged'):
+                            model.reduce_logged()          # rank means of the logged scalars
                         if rank == 0 and self.global_step % self.log_every_n_steps == 0:
                             logs = {k: _scalar(v) for k, v in model.logged.items()}
                             logs['step'] = self.global_step

@@ -292,15 +292,50 @@ class TransformerVAE(ContinuousVAEHooks, LanguageModel):
     def grad_norm(self):
         return self._norm_partials(fresh=True).sum().sqrt()
 
+    def _local_grad_scale(self):
+        """Factor from the arena's contents to the gradient the reference would clip here. Under data parallelism
+        the backward ran on loss / world, so an accumulation micro-step (no all-reduce yet) leaves G_local / world
+        in the arena, while DDP's no_sync micro-step clips the unscaled local G. After the all-reduce the arena
+        holds the rank mean, which is what DDP clips."""
+        if self._dp is not None and not self.require_backward_grad_sync:
+            return float(self._dp['world'])
+        return 1.0
+
     def on_after_backward(self):
-        super().on_after_backward()        # grad norm (+ clip inside the fused optimiser step)
+        """language_model.py:120-122 (clip_grad_norm_ + `grad_norm` log) and continuous_autoencoder.py:28-39."""
+        scale = self._local_grad_scale()
+        norm = self.grad_norm()
+        self.log('grad_norm', norm * scale if scale != 1.0 else norm)
         if not self.require_backward_grad_sync:
             # an accumulation micro-step: the reference clips after every backward (language_model.py:120-122),
-            # so this partial gradient is clipped now; the last micro-step's clip is fused into RAdam
+            # so this partial gradient is clipped now; the last micro-step's clip is fused into RAdam. The arena
+            # holds G / scale: clipping it at threshold / scale is clipping G at the threshold
             K.clip_grad(self._flat.grad, self._flat.n_live, self._norm_partials(fresh=False),
-                        float(self.hparams.get('grad_clip_threshold', 5.0)))
+                        float(self.hparams.get('grad_clip_threshold', 5.0)) / scale)
             self._norm_valid = False
         self.anneal_kl()                   # continuous_autoencoder.py:28-39
+
+    LOGGED_REDUCE_KEYS = ('loss', 'train_nll', 'train_kl', 'train_mc_mutual_info', 'grad_norm')
+
+    def reduce_logged(self, keys=LOGGED_REDUCE_KEYS):
+        """the logged scalars averaged over the data-parallel ranks for reporting (each rank's
+        training step logs its local values, language_model.py:112, continuous_autoencoder.py:50,
+        transformer_vae.py:61). One all-reduce of the stacked scalars; on RCCL `wait()` only orders the caller's
+        stream after it (no host synchronisation), so the step does not stall until a value is read. Every rank
+        calls it at the same optimiser steps (the trainer does, once per optimiser step); the keys are the same
+        on every rank because every rank runs the same training_step code on the same batch shapes."""
+        dp = self._dp
+        if dp is None:
+            return
+        names = [k for k in keys if k in self.logged]
+        if not names:
+            return
+        vals = torch.stack([torch.as_tensor(self.logged[k], dtype=torch.float32, device=self.device).reshape(())
+                            for k in names])
+        dist.all_reduce(vals, op=dist.ReduceOp.SUM, group=dp['group'], async_op=True).wait()
+        vals = vals / dp['world']
+        for i, k in enumerate(names):
+            self.logged[k] = vals[i]
 
     # ------------------------------------------------------------------ inference-side helpers
     @torch.no_grad()

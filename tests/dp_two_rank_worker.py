@@ -57,6 +57,31 @@ def main():
     if rank == 0:
         ref = _model(1)
         res['ref_loss'], res['ref_grad'] = _step(ref, batch, eps)
+    # gradient accumulation under DP (accumulate_grad_batches = 2, DDP no_sync): two micro-steps of per / 2 sequences;
+    # the first reduces nothing, the second's buckets reduce the accumulated sum once
+    m.zero_grad()
+    q = per // 2
+    for k, sync in ((0, False), (1, True)):
+        lo = rank * per + k * q
+        m.require_backward_grad_sync = sync
+        o = m.training_step(_slice(batch, lo, lo + q), 0, eps=eps[lo:lo + q], dropout=0.0)
+        o['loss'].backward()
+        if not sync:
+            assert not m._dp['works'] and m._dp['start'] == 0, 'a no_sync micro-step communicated'
+    torch.cuda.synchronize()
+    res['acc_grad'] = m._flat.grad[:m._flat.n_live].detach().cpu().clone()
+    if rank == 0:
+        # single process, no DP: micro-batch k = the ranks' k-th micro-batches together (a mean over 2q sequences of
+        # equal length = the rank mean of the q-sequence means), gradients accumulated over the two micro-steps
+        ref.zero_grad()
+        raw = batch['token_ids'].as_raw()
+        for k in (0, 1):
+            idx = torch.tensor([r * per + k * q + j for r in range(world) for j in range(q)], device=dev)
+            sub = {'token_ids': PaddedTensor.from_raw(raw[idx].contiguous()),
+                   'num_tokens': batch['num_tokens'][idx].contiguous(), 'num_bytes': batch['num_bytes'][idx].contiguous()}
+            ref.training_step(sub, 0, eps=eps[idx], dropout=0.0)['loss'].backward()
+        torch.cuda.synchronize()
+        res['ref_acc_grad'] = ref._flat.grad[:ref._flat.n_live].detach().cpu().clone()
     torch.save(res, out)
     dist.barrier()
     dist.destroy_process_group()

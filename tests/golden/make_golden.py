@@ -32,6 +32,7 @@ CONFIGS = {
     'hd96': (384, 4, 6, 128, 2, True),           # decoder hd 96, encoder 6 heads x 64
     'c2shape': (512, 8, 6, 512, 2, False),       # the C2 model at B=2
     'c4shape': (768, 8, 12, 1024, 2, True),      # the C4/C5 model (decoder hd 96, encoder 12 x 64) at L=1024, B=2
+    'c5shape': (768, 8, 12, 2048, 2, True),      # the C5 sequence length (L=2048), second sequence padded
 }
 N_SAMPLE = 64   # gradient elements sampled per parameter
 

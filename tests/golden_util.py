@@ -7,7 +7,7 @@ import torch
 from oracle.params import HParams, init_params
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden')
-CONFIG_NAMES = ['tiny', 'tiny_pad', 'small6_pad', 'hd96', 'c2shape', 'c4shape']
+CONFIG_NAMES = ['tiny', 'tiny_pad', 'small6_pad', 'hd96', 'c2shape', 'c4shape', 'c5shape']
 
 
 def load(name):

@@ -23,7 +23,7 @@ def _engine(name):
     return g, hp, VAEEngine(hp, flat), flat, ids
 
 
-@pytest.mark.parametrize('name', ['tiny', 'tiny_pad', 'small6_pad', 'hd96', 'c2shape', 'c4shape'])
+@pytest.mark.parametrize('name', ['tiny', 'tiny_pad', 'small6_pad', 'hd96', 'c2shape', 'c4shape', 'c5shape'])
 def test_fp32_mode_argmax_is_bit_exact(name):
     g, hp, eng, flat, ids = _engine(name)
     B, L = ids.shape

@@ -97,7 +97,7 @@ def test_chunked_grad_matches_autograd(nchunks):
     assert _rel(db, ref.grad.sum((0, 1))) < 1e-2
 
 
-def _prob_head(hh, W, bias, lab, T, L, V, d, nchunks, chunk_len, g=0.75):
+def _prob_head(hh, W, bias, lab, T, L, V, d, nchunks, chunk_len, g=0.75, sat=None):
     """The engine's P-head (svae.h): forward (label logits, CE_PROB GEMM, finalize) and backward (prep, dW GEMM
     with weighted row sums, ROWSCALE_GATHER dX GEMM, one-hot part through the fused embedding backward with
     zero upstream gradient). Returns nll, row_loss and the gradients (dhh bf16, dW f32, dbias f32)."""
@@ -109,7 +109,8 @@ def _prob_head(hh, W, bias, lab, T, L, V, d, nchunks, chunk_len, g=0.75):
     K.gemm(hh, W, Pm, T, V, d, epi=N.EPI_CE_PROB, bias=bias, aux=part, labels=lab, row_a=coff)
     lse, rl, cw, nll = (torch.empty(T, device=dev), torch.empty(T, device=dev), torch.empty(nchunks, device=dev),
                         torch.empty(1, device=dev))
-    K.ce_prob_finalize(part, ntile, coff, lab, T, L, nchunks, chunk_len, lse, rl, cw, nll)
+    K.ce_prob_finalize(part, ntile, coff, lab, T, L, nchunks, chunk_len, lse, rl, cw, nll,
+                       fix=None if sat is None else (hh, W, bias, Pm, sat))
     gs = torch.full((1,), g, device=dev)
     hh_r = torch.empty(T, d, dtype=torch.bfloat16, device=dev)
     r, q = torch.empty(T, device=dev), torch.empty(T, device=dev)
@@ -192,3 +193,43 @@ def test_prob_head_random_matches_autograd(nchunks):
     assert _rel(dhh, gh) < 1e-2
     assert _rel(dW, gW) < 1e-2
     assert _rel(dbias, gb) < 1e-2
+
+
+def test_prob_head_saturated_rows_are_recomputed():
+    """rows whose largest logit is > 88 nats above the label logit saturate the CE_PROB epilogue's
+    exponent (2^127). ce_prob_finalize_fix lists them and recomputes P, lse and the offset exactly, so nll and every
+    gradient still match torch fp32 autograd (which, like the reference's fp32 log-softmax, is stable there)."""
+    torch.manual_seed(5)
+    B, L, V, d = 8, 512, 32768, 256
+    T = B * L
+    hh = torch.randn(T, d, device=dev)
+    W = 0.1 * torch.randn(V, d, device=dev)
+    W[777] = 0.0
+    W[777, 0] = 1.0
+    hot = [10, 20, 3000]
+    for r in hot:
+        hh[r] = 0.0
+        hh[r, 0] = 150.0                 # logit of column 777: 150; every other logit within 15 of 0
+    hh, W = hh.bfloat16(), W.bfloat16()
+    bias = 0.5 * torch.randn(V, device=dev)
+    lab = torch.randint(3, V, (B, L), dtype=torch.int32, device=dev)
+    lab[lab == 777] = 778
+    lab[:, -1] = 0
+    lab = lab.view(T)
+    chunk_len = L - 1
+    sat = torch.empty(T + 1, dtype=torch.int32, device=dev)
+    nll, rl, dhh, dW, dbias = _prob_head(hh, W, bias, lab, T, L, V, d, 1, chunk_len, sat=sat)
+    assert sat[0].item() == len(hot)
+    assert sorted(sat[1:1 + len(hot)].tolist()) == hot
+    loss, gh, gW, gb = _torch_ref(hh, W, bias, lab, B, L, V, chunk_len)
+    assert abs(nll.item() - loss.item()) / loss.item() < 1e-5, (nll.item(), loss.item())
+    rows = torch.tensor(hot, device=dev)
+    ref_rows = torch.logsumexp(hh[rows].float() @ W.float().t() + bias, -1) - (
+        (hh[rows].float() * W[lab[rows].long()].float()).sum(-1) + bias[lab[rows].long()])
+    torch.testing.assert_close(rl[rows], ref_rows, rtol=1e-5, atol=1e-3)
+    assert _rel(dhh, gh) < 1e-2
+    assert _rel(dW, gW) < 1e-2
+    assert _rel(dbias, gb) < 1e-2
+    # without the fix-up the same rows come out clipped (the check above is not vacuous)
+    nll0, rl0, *_ = _prob_head(hh, W, bias, lab, T, L, V, d, 1, chunk_len)
+    assert (rl0[rows] - ref_rows).abs().min().item() > 1.0

@@ -55,3 +55,8 @@ def test_two_rank_data_parallel_step_matches_full_batch(tmp_path):
     assert ((g - ref).norm() / ref.norm()).item() < 1e-4
     cos = (g @ ref / (g.norm() * ref.norm())).item()
     assert cos > 0.99999
+    # two accumulated micro-steps per rank (no_sync on the first): the rank mean of the summed micro-gradients
+    assert torch.equal(r0['acc_grad'], r1['acc_grad'])
+    g, ref = r0['acc_grad'].double(), r0['ref_acc_grad'].double()
+    assert ((g - ref).norm() / ref.norm()).item() < 1e-4
+    assert (g @ ref / (g.norm() * ref.norm())).item() > 0.99999

@@ -52,16 +52,28 @@ def _grad_bars(worst, msg):
         assert abs(r - 1.0) < tol, f'{n}: norm ratio {r:.4f}\n' + msg
 
 
-@pytest.mark.parametrize('name', ['tiny_pad', 'small6_pad', 'hd96', 'c2shape', 'c4shape'])
-def test_step_matches_oracle(name):
+@pytest.mark.parametrize('name,chunk_numel', [('tiny_pad', None), ('small6_pad', None), ('hd96', None),
+                                              ('c2shape', None), ('c4shape', None), ('c5shape', None),
+                                              ('c4shape', 2 ** 25), ('c4shape', 23_000_000)])
+def test_step_matches_oracle(name, chunk_numel, monkeypatch):
+    """chunk_numel lowers robust_cross_entropy's 2**30 threshold (language_model.py:163) on both sides, so the full
+    engine runs the chunked mean of means (c4shape: 2 chunks of 512 / 511 positions, and 3 of 341, the padded
+    sequence's tail inside the last chunk) through ce_prob_finalize's chunk weights, the [CLS] / label-0 rows and
+    ce_prob_bwd_prep, against the oracle's chunked branch (itself pinned by the reference's ce_chunked.npz)."""
     torch.set_num_threads(min(16, os.cpu_count()))
     g, hp, params, ids = setup(name)
     ntok = torch.from_numpy(g['lens'])
     eps = torch.from_numpy(g['eps'])
     kw = float(g['kl_weight'])
     p = {k: v.clone().requires_grad_(True) for k, v in params.items()}
-    ref = oracle.training_step(p, hp, ids, ntok, eps, kl_weight=kw)
+    ref = oracle.training_step(p, hp, ids, ntok, eps, kl_weight=kw, ce_chunk_numel=chunk_numel or 2 ** 30)
     ref['loss'].backward()
+    if chunk_numel is not None:
+        import sparse_vae.engine as engine_mod
+        from sparse_vae import kernels as K
+        monkeypatch.setattr(engine_mod, 'CE_CHUNK_NUMEL', chunk_numel)
+        B, L = ids.shape
+        assert K.ce_chunking(B, L, hp.vocab_size, chunk_numel)[0] > 1
 
     flat, eng = _build(hp, params)
     out = eng.forward(ids.cuda(), ntok.cuda(), eps=eps.cuda(), dropout=0.0, kl_weight=kw)
@@ -76,13 +88,16 @@ def test_step_matches_oracle(name):
     assert abs(kl - ref['kl'].item()) / abs(ref['kl'].item()) < 2e-2
     # the oracle itself is pinned to the reference's logged values (test_oracle_golden); check the engine
     # against the reference's own numbers too
-    assert abs(loss - float(g['loss'])) / abs(float(g['loss'])) < 1e-3
+    if chunk_numel is None:
+        assert abs(loss - float(g['loss'])) / abs(float(g['loss'])) < 1e-3
+    else:                  # the chunking changes the loss (mean of means): it must differ from the unchunked one
+        assert abs(ref['loss'].item() - float(g['loss'])) > 1e-5
     mu = out['mu'].cpu()
     assert ((mu - ref['mu'].detach().view_as(mu)).norm() / ref['mu'].detach().norm()).item() < 2e-2
 
     worst = _grad_report(flat, p)
     msg = '\n'.join(f'{c:.5f} {r:.4f} {n}' for c, r, n in worst[:8])
-    print(f'[{name}] loss {loss:.6f} ref {ref["loss"].item():.6f} kl {kl:.6f} ref {ref["kl"].item():.6f}\n' + msg)
+    print(f'[{name} {chunk_numel}] loss {loss:.6f} ref {ref["loss"].item():.6f} kl {kl:.6f} ref {ref["kl"].item():.6f}\n' + msg)
     _grad_bars(worst, msg)
 
 

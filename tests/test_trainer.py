@@ -116,3 +116,25 @@ def test_rank_batch_sampler():
     got = [list(RankBatchSampler(S(), r, 4)) for r in range(4)]
     assert got == [[[0], [4]], [[1], [5]], [[2], [6]], [[3], [7]]]
     assert len(RankBatchSampler(S(), 0, 4)) == 2
+
+
+def test_validation_keeps_training_logs_separate():
+    """validation must not clear the training values logged before it, and its val_* keys must not
+    leak into the next training log line."""
+    class M(_Model):
+        def validation_step(self, batch, i):
+            self.logged.clear()
+            self.logged['val_loss'] = torch.tensor(7.0)
+
+    m = M()
+    tr = Trainer(max_steps=4, val_check_interval=2, limit_val_batches=1, log_every_n_steps=1)
+    tr.fit(m, datamodule=_dm(10))
+    assert [v['val_loss'] for v in tr.val_history] == [7.0, 7.0]
+    assert all('val_loss' not in h and 'train_nll' in h for h in tr.history)
+    assert 'train_nll' in m.logged and 'val_loss' not in m.logged
+
+
+def test_epoch_limit_defaults_like_lightning():
+    assert Trainer().max_epochs == 1000
+    assert Trainer(max_steps=10).max_epochs is None
+    assert Trainer(max_epochs=3).max_epochs == 3
