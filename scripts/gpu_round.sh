@@ -2,6 +2,7 @@
 # One GPU-box pass: GPU tests, the default bench line, a kernel-trace profile and the two HBM PMC passes
 # for the vocab-head GEMM. Every GPU step has its own time limit; the chain stops at the first failure.
 #   bash scripts/gpu_round.sh TAG [STAGES]     STAGES: any of t(ests) b(ench) p(rofile) m(pmc); default tbpm
+#   CFG=c4 bash scripts/gpu_round.sh ...        bench / profile / PMC on another bench.py config (default c2)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
@@ -9,15 +10,16 @@ OUT=gpurun_out/${1:-run}
 ST=${2:-tbpm}
 mkdir -p "$OUT"
 HEAD_RE="gemm256_kernel<false, false, 9>"
-PB="python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-parity"
+CFG=${CFG:-c2}
+PB="python3 bench.py --config $CFG --steps 10 --warmup 3 --no-cpu-baseline --no-parity"
 run() { echo "== $*" >&2; "$@"; }
 rc=0
 if [[ $ST == *t* && $rc == 0 ]]; then
-  timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1; rc=$?
+  timeout -k 10 900 python -u -m pytest tests -m gpu -q -rf --maxfail=10 --timeout 150 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1; rc=$?
   tail -3 "$OUT/pytest_gpu.log"
 fi
 if [[ $ST == *b* && $rc == 0 ]]; then
-  timeout -k 10 300 python -u bench.py > "$OUT/bench.log" 2>&1; rc=$?
+  timeout -k 10 300 python -u bench.py --config $CFG > "$OUT/bench.log" 2>&1; rc=$?
   tail -1 "$OUT/bench.log"
 fi
 if [[ $ST == *p* && $rc == 0 ]]; then

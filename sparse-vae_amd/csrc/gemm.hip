@@ -436,14 +436,20 @@ constexpr int NSTAGE = 3;
 
 __device__ __forceinline__ int kc2_off(int row, int c) { return row * 64 + ((c ^ ((row >> 1) & 3)) << 4); }
 
+// LDS-DMA pieces (1 KiB wave-instructions) each of the 4 waves issues per operand K-tile: 8 KiB / 4 waves / 1 KiB
+constexpr int G2_PIECES = T2 / 1024 / 4;
+// the ring's counted wait: tile kt has landed while the next tile's pieces (both operands) may still fly
+constexpr int G2_WAIT_NEXT = 2 * G2_PIECES;
+static_assert(G2_PIECES * 4 * 1024 == T2, "issue_tile2 covers the operand tile exactly");
+
 template <bool TRANS>
 __device__ __forceinline__ void issue_tile2(const bf16* __restrict__ g, long long ld, int row0, int nrows, int k0,
                                             int kend, char* lds_tile, int wave, int lane) {
   const bf16* base = TRANS ? g + (long long)k0 * ld + row0 : g + (long long)row0 * ld + k0;
   const u32x4 rsrc = buffer_rsrc(base, 0x7FFFFFF0u);
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int inst = wave * 2 + j;
+  for (int j = 0; j < G2_PIECES; ++j) {
+    const int inst = wave * G2_PIECES + j;
     const int slot = inst * 64 + lane;
     int off;
     bool ok;
@@ -508,7 +514,7 @@ __global__ __launch_bounds__(256, 3) void gemm_glds_kernel(GP p) {
   for (int kt = 0; kt < nk; ++kt) {
     // tile kt landed (this wave's 4 DMA pieces of tile kt+1 may still fly), then everyone's pieces + the
     // ring slot of tile kt+2 (last read in iteration kt-1) is free
-    if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G2_WAIT_NEXT) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if (kt + 2 < nk) {
@@ -1117,10 +1123,38 @@ __device__ unsigned long long svae_stamps[8][96][3];
 #else
 #define G3_STAMP(k) ((void)0)
 #endif
-static_assert(G3_EPI_STORES == 16, "the first K-step's s_waitcnt literal below");
 // internal instantiation: SVAE_EPI_F32_ACC whose fused bias-gradient row sums are weighted by k_weight (the
 // vocabulary head's dW, where the per-token weight r folds the softmax normalisation into the row sums)
 constexpr int G3_EPI_ACC_KW = 64;
+
+// Vector-memory operations every wave issues unconditionally in the epilogue of an interior 256 x 256 tile (stores
+// and atomics only: loads a lane may branch around are not counted), i.e. after the next tile's first K-tile DMA.
+// The next tile's relaxed first wait, vmcnt(G3_EPI_STORES), covers that DMA only if at least G3_EPI_STORES of them
+// are younger (vmcnt retires in issue order); gemm256_run static_asserts it per instantiation.
+template <int EPI>
+constexpr int g3_epi_vmem_ops() {
+  switch (EPI) {
+    case SVAE_EPI_BF16:
+    case SVAE_EPI_ROTARY_BF16:
+    case SVAE_EPI_CE_STATS:           // with C (the host clears p.relaxed when C == NULL: no logits stored)
+    case SVAE_EPI_ROWSCALE_GATHER:
+    case SVAE_EPI_GELU_BWD:
+      return 8 * 2;                   // 8 fragment rows x 2 permlane-paired 16-B stores
+    case SVAE_EPI_CE_PROB:
+      return 8 * 2 + 1;               // + the tile's per-row partial sums
+    case SVAE_EPI_GELU:
+      return 8 * 2 * 2;               // + the GELU' aux
+    case SVAE_EPI_F32:
+    case SVAE_EPI_F32_ACC:
+    case SVAE_EPI_DROPOUT_RESID:
+    case G3_EPI_ACC_KW:
+      return 8 * 4;                   // 8 fragment rows x 4 16-B f32 stores
+    case SVAE_EPI_F32_ATOMIC:
+      return 4 * 32;                  // staged: 4 passes x 32 atomics per lane
+    default:
+      return 0;
+  }
+}
 
 // The gemm256 block program over the tiles of one GEMM: block `blk` of `nwg` blocks working on p (the plain kernel
 // passes blockIdx.x / gridDim.x; the paired kernel gives each GEMM its own range of blocks).
@@ -1128,6 +1162,7 @@ template <bool AT, bool BT, int EPI>
 __device__ __forceinline__ void gemm256_run(const GP& p, int blk, int nwg) {
   // 2 ring stages + a side area: the epilogue's per-tile bias (256 f32), CE labels (256 i32) and CE row statistics
   // ([256 rows][4 column waves][max, sum]); one array
+  static_assert(g3_epi_vmem_ops<EPI>() >= G3_EPI_STORES, "the relaxed first wait would not cover the prefetch DMA");
   __shared__ __attribute__((aligned(16))) char smem[2 * G3_STAGE + 2048 + 8192];
   float* sbias = (float*)(smem + 2 * G3_STAGE);
   int* slabel = (int*)(smem + 2 * G3_STAGE + 1024);
@@ -1179,7 +1214,7 @@ __device__ __forceinline__ void gemm256_run(const GP& p, int blk, int nwg) {
     for (int kt = 0; kt < T.nk; ++kt, ++g) {
       // this wave's pieces of K-tile g landed (after an interior epilogue, up to G3_EPI_STORES younger stores may
       // still be in flight: vmcnt retires in issue order)
-      if (kt == 0 && relaxed) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+      if (kt == 0 && relaxed) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G3_EPI_STORES) : "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();                      // everyone's landed; K-tile g-1 (other stage) consumed
       const char* la = smem + (g & 1) * G3_STAGE;
