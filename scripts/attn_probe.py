@@ -34,6 +34,8 @@ def main():
     for B, L, causal, hd in cases:
       if only == 'hd96' and hd != 96:
           continue
+      if only == 'c2c4' and (B, L, causal, hd) not in ((64, 512, True, 64), (64, 1024, True, 96)):
+          continue
       for with_o32 in (True, False):
         H = 8
         if not with_o32 and (B, L, hd) != (64, 512, 64):

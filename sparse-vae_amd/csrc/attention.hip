@@ -16,6 +16,7 @@
 // through LDS once for dQ = dS K: each key block stores its f32 partial dQ into its own slice of dq_part (no
 // atomics) and attn_dq_reduce_kernel sums the slices in a fixed order (deterministic).
 #include "common.h"
+#include <algorithm>
 #include "../../include/svae.h"
 
 using namespace svae;
@@ -37,6 +38,7 @@ struct AP {
   float* o32; long long so32, bo32;
   float* dq_part; void* dq_bf; long long ldq_bf;
   int window;        // > 0: causal sliding window of `window` 32-key blocks plus key block 0 (SparseAttention)
+  int kblk;          // backward: keys per dQ partial (the key block of the kernel that wrote dq_part)
 };
 
 // Block-sparse sliding window of SparseAttention (sparse_attention.py:39-60, causal, block 32): query q sees
@@ -912,6 +914,341 @@ __device__ __forceinline__ void attn_bwd_tile_wide(const AP& p, char* smem, int 
   }
 }
 
+// ===================================================================================== backward, 8 waves
+// One workgroup = 256 keys of one (batch, head) = 8 waves x 32 keys, sweeping 64-query tiles: the same key-on-the-lane
+// algorithm as attn_bwd_tile, but twice the keys per dQ partial (the partial planes and the reduction's reads halve:
+// at C4, hd 96, they were 0.9 GB written and read per launch) and, for hd 96, two waves per SIMD instead of one (the
+// 4-wave kernel needed 128-wide LDS rows and 256-register waves). LDS rows of HDC = 64 or 96 dims (RowImg: 96 = a
+// 64-dim Tile plus a 32-dim tail image), so hd 96 keeps K, dS^T and double-buffered Q / dO in 129 KiB.
+//
+// RowImg<HDC>: 64 rows x HDC bf16. Dims 0-63: the Tile<64> image (128-B rows, chunk c ^ (r & 7)). HDC = 96: dims
+// 64-95 follow as [64 rows][4 chunks] (64-B rows) with chunk swizzle c ^ tail_swz(r): rows r, r + 4, r + 8, r + 12
+// share banks, so tail_swz takes 4 distinct values over bits 2-3 of r (the 16-row b128 reads) and differs in bit 1
+// between r and r + 4 and between r and r + 8 (the transposed reads of rows 4g + q and 8g + q): conflict-free.
+template <int HDC>
+struct RowImg {
+  static_assert(HDC == 64 || HDC == 96, "RowImg: 64 or 96 dims");
+  static constexpr int NCH = HDC / 8;               // 16-B chunks per row
+  static constexpr int BYTES = 64 * HDC * 2;        // 8 or 12 KiB
+  static constexpr int PIECES = BYTES / 1024;       // LDS-DMA wave-instructions per image
+  __device__ static __forceinline__ int tail_swz(int r) { return ((((r >> 2) ^ (r >> 3)) & 1) << 1) | ((r >> 2) & 1); }
+  // byte offset of (row r < 64, logical chunk c)
+  __device__ static __forceinline__ int off(int r, int c) {
+    if (HDC == 64 || c < 8) return r * 128 + ((c ^ (r & 7)) << 4);
+    return 8192 + r * 64 + (((c - 8) ^ tail_swz(r)) << 4);
+  }
+  // 8-B unit u (dims 4u .. 4u + 3) of row r
+  __device__ static __forceinline__ int uoff(int r, int u) { return off(r, u >> 1) + ((u & 1) << 3); }
+  // the LDS slot of lane `lane` in DMA piece i: row r and logical chunk c it receives (swizzle undone)
+  __device__ static __forceinline__ void piece_src(int i, int lane, int& r, int& c) {
+    if (HDC == 64 || i < 8) {
+      r = 8 * i + (lane >> 3);
+      c = (lane & 7) ^ (r & 7);
+    } else {
+      r = 16 * (i - 8) + (lane >> 2);
+      c = ((lane & 3) ^ tail_swz(r)) + 8;
+    }
+  }
+};
+
+// LDS-DMA of piece i of the RowImg of rows [row0, row0 + 64) of a token-major matrix whose row 0 the descriptor
+// addresses (offsets stay below 2^31 bytes: checked by svae_attn_bwd); rows >= nrows and dims >= hd land as zeros
+// (out-of-range source offset)
+template <int HDC>
+__device__ __forceinline__ void dma_img_piece(const u32x4& rsrc, long long ld, int row0, int nrows, int hd, char* img,
+                                              int i, int lane) {
+  int r, c;
+  RowImg<HDC>::piece_src(i, lane, r, c);
+  const bool ok = row0 + r < nrows && c * 8 < hd;
+  dma16_lds(rsrc, img + i * 1024, ok ? ((row0 + r) * (int)ld + c * 8) * 2 : 0x7FFFFFF0);
+}
+
+constexpr int BWD8_KEYS = 256;
+
+template <int HDC>
+__device__ __forceinline__ void attn_bwd8_tile(const AP& p, char* smem, int kb, int h, int b) {
+  using R = RowImg<HDC>;
+  using TS = Tile<64>;          // dS^T [256 keys][64 queries]
+  constexpr int NKK = HDC / 32, NT = HDC / 16;
+  constexpr int NW = 8;
+  // LDS: [buf][Q, dO] images | K: 4 images (256 keys) | dS^T | [buf][lse, delta][64]
+  char* QO = smem;
+  char* Ks = smem + 4 * R::BYTES;
+  char* dSs = Ks + 4 * R::BYTES;
+  float* cst = (float*)(dSs + 4 * TS::BYTES);
+  // LDS-DMA pieces per wave: one query tile's Q + dO images, and the K tile
+  constexpr int QO_PW = 2 * R::PIECES / NW;
+  constexpr int K_PW = 4 * R::PIECES / NW;
+  static_assert(QO_PW * NW == 2 * R::PIECES && K_PW * NW == 4 * R::PIECES, "pieces split evenly over the waves");
+
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, li = lane & 15;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int k0 = kb * BWD8_KEYS;
+  const bf16* Q = p.q + b * p.bq + (long long)h * p.hd;
+  const bf16* K = p.k + b * p.bk + (long long)h * p.hd;
+  const bf16* V = p.v + b * p.bv + (long long)h * p.hd;
+  const bf16* dO = p.dout + b * p.bdo + (long long)h * p.hd;
+  const float* lse = p.lse + ((long long)b * p.H + h) * p.Lq;
+  const float* delta = p.delta + ((long long)b * p.H + h) * p.Lq;
+  const int kw = k0 + 32 * w;                       // this wave's first key
+  bool key_ok[2];
+  bf16x8 vf[2][NKK];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int key = kw + 16 * j + li;
+    key_ok[j] = key < p.Lk && !(p.pad && p.pad[(long long)b * p.Lk + key]);
+#pragma unroll
+    for (int kk = 0; kk < NKK; ++kk) {
+      const int d = 32 * kk + 8 * g;
+      u32x4 c = {0u, 0u, 0u, 0u};
+      if (key < p.Lk && d < p.hd) c = *(const u32x4*)(V + (long long)key * p.sv + d);
+      vf[j][kk] = __builtin_bit_cast(bf16x8, c);
+    }
+  }
+  const bool keys_all_ok = __builtin_amdgcn_ballot_w64(!(key_ok[0] && key_ok[1])) == 0;
+  {  // K tile: 4 images of 64 keys
+    const u32x4 krs = buffer_rsrc(K, 0x7FFFFFF0u);
+#pragma unroll
+    for (int i = 0; i < K_PW; ++i) {
+      const int pc = w * K_PW + i, img = pc / R::PIECES;
+      dma_img_piece<HDC>(krs, p.sk, k0 + 64 * img, p.Lk, p.hd, Ks + img * R::BYTES, pc % R::PIECES, lane);
+    }
+  }
+  f32x4 dk[2][NT], dv[2][NT];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int t = 0; t < NT; ++t) { dk[j][t] = (f32x4){0.f, 0.f, 0.f, 0.f}; dv[j][t] = dk[j][t]; }
+
+  const float inv_scale = 1.0f / p.scale, c = p.scale * LOG2E;
+  const int qt0 = p.causal ? k0 / 64 : 0;
+  const int q_end = (p.window > 0 && k0 > 0) ? min(p.Lq, k0 + BWD8_KEYS - SBLK + SBLK * p.window) : p.Lq;
+  const int nqt = (q_end + 63) / 64;
+  const int band_end = p.window > 0 && kw >= SBLK ? kw + SBLK * p.window : 0x7FFFFFFF;   // first query past kw's band
+  float* part = p.dq_part + ((long long)kb * p.B + b) * p.Lq * p.H * p.hd + (long long)h * p.hd;
+  const long long ldp = (long long)p.H * p.hd;
+  const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc((void*)part, 0, 0x7FFFFFF0, 0x00020000);
+  // dQ partial of a query tile (64 queries x HDC dims): wave w owns queries 16 (w & 3) .. + 15 and dims
+  // (w >> 2) HDC / 2 .. + HDC / 2 - 1, i.e. NT / 2 fragments, stored as NT / 2 16-B buffer stores per lane (a fixed
+  // count: the end-of-tile wait leaves exactly those in flight)
+  constexpr int DQ_NT = NT / 2;
+  constexpr int DQ_STORES = DQ_NT;
+  const int dq_q16 = w & 3, dq_u0 = (w >> 2) * DQ_NT;
+
+  const u32x4 qrs = buffer_rsrc(Q, 0x7FFFFFF0u), ors = buffer_rsrc(dO, 0x7FFFFFF0u);
+  const u32x4 lser = buffer_rsrc(lse, (unsigned)p.Lq * 4u), der = buffer_rsrc(delta, (unsigned)p.Lq * 4u);
+  auto fetch = [&](int qb, int buf) {
+    char* base = QO + buf * 2 * R::BYTES;
+    const int ln = lane_id_fresh();
+#pragma unroll
+    for (int i = 0; i < QO_PW; ++i) {
+      const int pc = w * QO_PW + i;
+      if (pc < R::PIECES) dma_img_piece<HDC>(qrs, p.sq, qb, p.Lq, p.hd, base, pc, ln);
+      else dma_img_piece<HDC>(ors, p.sdo, qb, p.Lq, p.hd, base + R::BYTES, pc - R::PIECES, ln);
+    }
+    const int qo = qb + lane < p.Lq ? (qb + lane) * 4 : 0x7FFFFFF0;
+    if (w == 0) dma4_lds(lser, cst + buf * 128, qo);
+    else if (w == 1) dma4_lds(der, cst + buf * 128 + 64, qo);
+  };
+  if (qt0 < nqt) fetch(qt0 * 64, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  for (int qt = qt0; qt < nqt; ++qt) {
+    const int buf = (qt - qt0) & 1;
+    const int qb = qt * 64;
+    const char* Qs = QO + buf * 2 * R::BYTES;
+    const char* dOs = Qs + R::BYTES;
+    const float* nl = cst + buf * 128;
+    if (qt + 1 < nqt) fetch(qb + 64, buf ^ 1);
+    const bool live = (!p.causal || kw <= qb + 63) && qb < band_end && kw < p.Lk;
+    if (live) {
+      const char* Kw = Ks + (w >> 1) * R::BYTES;     // this wave's 32 keys: rows 32 (w & 1) .. of image w / 2
+      const bool edge = !keys_all_ok || qb + 64 > p.Lq || (p.causal && kw + 31 > qb) || qb + 63 >= band_end;
+      const int qlim = min(p.Lq, band_end) - qb;
+      constexpr int TPP = 2;
+#pragma unroll
+      for (int pass = 0; pass < 4 / TPP; ++pass) {
+        // the K fragments are re-read per pass (live only through its S products: 4 NKK registers fewer at the
+        // dV / dK peak, which is what keeps hd 96 at 256 registers without spills)
+        bf16x8 kf[2][NKK];
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int kk = 0; kk < NKK; ++kk) kf[j][kk] = *(const bf16x8*)(Kw + R::off(32 * (w & 1) + 16 * j + li, g + 4 * kk));
+        f32x4 s[2][TPP], dp[2][TPP];
+#pragma unroll
+        for (int th = 0; th < TPP; ++th) {
+          const int t = pass * TPP + th;
+          const f32x4 sl = *(const f32x4*)(nl + 16 * t + 4 * g) * -inv_scale;   // -lse / scale
+          const f32x4 dl = -*(const f32x4*)(nl + 64 + 16 * t + 4 * g);          // -delta
+          s[0][th] = sl; s[1][th] = sl;
+          dp[0][th] = dl; dp[1][th] = dl;
+          if (edge) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+              const int kmin = p.causal ? kw + 16 * j + li - qb : -0x40000000;
+              const unsigned kbad = key_ok[j] ? 0u : 1u;
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const int ql = 16 * t + 4 * g + r;
+                s[j][th][r] = (kbad | (unsigned)(ql >= qlim) | (unsigned)(ql < kmin)) ? -INFINITY : s[j][th][r];
+              }
+            }
+          }
+#pragma unroll
+          for (int k2 = 0; k2 < NKK; ++k2) {
+            const bf16x8 qa = *(const bf16x8*)(Qs + R::off(16 * t + li, g + 4 * k2));
+            const bf16x8 oa = *(const bf16x8*)(dOs + R::off(16 * t + li, g + 4 * k2));
+            s[0][th] = mfma16(qa, kf[0][k2], s[0][th]);
+            s[1][th] = mfma16(qa, kf[1][k2], s[1][th]);
+            dp[0][th] = mfma16(oa, vf[0][k2], dp[0][th]);
+            dp[1][th] = mfma16(oa, vf[1][k2], dp[1][th]);
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int th = 0; th < TPP; ++th)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float pr = __builtin_amdgcn_exp2f(s[j][th][r] * c);
+              s[j][th][r] = pr;
+              dp[j][th][r] = pr * dp[j][th][r];
+            }
+#pragma unroll
+        for (int k2 = 0; k2 < TPP / 2; ++k2) {
+          const int kk = pass * (TPP / 2) + k2;
+          const bf16x8 pf0 = pack8(s[0][2 * k2], s[0][2 * k2 + 1]), pf1 = pack8(s[1][2 * k2], s[1][2 * k2 + 1]);
+          const bf16x8 df0 = pack8(dp[0][2 * k2], dp[0][2 * k2 + 1]), df1 = pack8(dp[1][2 * k2], dp[1][2 * k2 + 1]);
+          // rows r0 = 32 kk + 4g + (li >> 2) and r0 + 16: the swizzles see row bits 0-3 only, so the address is the
+          // lane's row-(4g + (li >> 2)) address plus a constant (folded into the ds_read offset)
+          const int rq = 4 * g + (li >> 2);
+#pragma unroll
+          for (int u = 0; u < NT; ++u) {
+            const int uu = 4 * u + (li & 3);
+            const int pitch = 16 * u < 64 ? 128 : 64;
+            const int lo = R::uoff(rq, uu);
+            const int ro = 32 * kk * pitch;
+            const lds_char* po = lds_ptr(dOs) + lo + ro;
+            const lds_char* pq = lds_ptr(Qs) + lo + ro;
+            const bf16x8 ao = cat44(lds_read_tr3(po), lds_read_tr3(po + 16 * pitch));
+            dv[0][u] = mfma16(ao, pf0, dv[0][u]);
+            dv[1][u] = mfma16(ao, pf1, dv[1][u]);
+            const bf16x8 aq = cat44(lds_read_tr3(pq), lds_read_tr3(pq + 16 * pitch));
+            dk[0][u] = mfma16(aq, df0, dk[0][u]);
+            dk[1][u] = mfma16(aq, df1, dk[1][u]);
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int th = 0; th < TPP; ++th)
+            *(bf16x4*)(dSs + TS::uoff(32 * w + 16 * j + li, 4 * (pass * TPP + th) + g)) =
+                (bf16x4){f2bf(dp[j][th][0]), f2bf(dp[j][th][1]), f2bf(dp[j][th][2]), f2bf(dp[j][th][3])};
+      }
+    } else {
+      const bf16x4 z = {f2bf(0.f), f2bf(0.f), f2bf(0.f), f2bf(0.f)};
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) *(bf16x4*)(dSs + TS::uoff(32 * w + 16 * j + li, 4 * t + g)) = z;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();   // dS^T complete (a raw barrier: __syncthreads' vmcnt(0) would drain the DMA)
+    asm volatile("" ::: "memory");
+    // partial dQ[q = qb + 16 dq_q16 + li][d = 16 (dq_u0 + u) + 4g + r] over the block's keys (K fragment as the first
+    // MFMA operand: a lane holds 4 consecutive dims of one query)
+    f32x4 dq[DQ_NT];
+#pragma unroll
+    for (int u = 0; u < DQ_NT; ++u) dq[u] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    const int kvis = p.causal ? min(BWD8_KEYS, qb + 64 - k0) : min(BWD8_KEYS, p.Lk - k0);   // keys with dS != 0
+    // Addresses: row kr = 32 kk + 8g + (li >> 2) (and kr + 4) of the dS^T and K images. The swizzles depend on row
+    // bits 0-3 only, which do not move with kk, so a lane's address is its kk = 0 address plus a constant per kk
+    // (folded into the ds_read offset field): per-kk addresses computed in full were spilled (76 VGPRs at hd 96).
+    {
+      const int q4 = 8 * g + (li >> 2);
+      const int uq = 4 * dq_q16 + (li & 3);
+      const lds_char* sp0 = lds_ptr(dSs) + TS::uoff(q4, uq);
+      const lds_char* sp4 = lds_ptr(dSs) + TS::uoff(q4 + 4, uq);
+      const lds_char* kp0[DQ_NT];
+      const lds_char* kp4[DQ_NT];
+#pragma unroll
+      for (int u = 0; u < DQ_NT; ++u) {
+        const int uk = 4 * (dq_u0 + u) + (li & 3);
+        kp0[u] = lds_ptr(Ks) + R::uoff(q4, uk);
+        kp4[u] = lds_ptr(Ks) + R::uoff(q4 + 4, uk);
+      }
+#pragma unroll
+      for (int kk = 0; kk < BWD8_KEYS / 32; ++kk) {
+        if (32 * kk >= kvis) break;
+        const int so = kk * 32 * TS::PITCH;
+        const bf16x8 a = cat44(lds_read_tr3(sp0 + so), lds_read_tr3(sp4 + so));
+#pragma unroll
+        for (int u = 0; u < DQ_NT; ++u) {
+          // the fragment's part of the row image (dims < 64: 128-B rows; the 96-dim tail: 64-B rows) is wave-uniform
+          const int pitch = 16 * (dq_u0 + u) < 64 ? 128 : 64;
+          const int ko = (kk >> 1) * R::BYTES + (kk & 1) * 32 * pitch;
+          const bf16x8 bk = cat44(lds_read_tr3(kp0[u] + ko), lds_read_tr3(kp4[u] + ko));
+          dq[u] = mfma16(bk, a, dq[u]);
+        }
+      }
+    }
+    {
+      const bool qok = qb + 16 * dq_q16 + li < p.Lq;
+      const int qrow = (qb + 16 * dq_q16 + li) * (int)ldp + 4 * g;
+#pragma unroll
+      for (int u = 0; u < DQ_NT; ++u) {
+        const int d = 16 * (dq_u0 + u);
+        const int off = (qok && d + 4 * g < p.hd) ? (qrow + d) * 4 : 0x7FFFFFF0;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, dq[u]), prs, off, 0, 0);
+      }
+    }
+    // the next tile's DMA (issued before this tile's stores) has landed; the stores stay in flight
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DQ_STORES) : "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  }
+
+  // epilogue: dK (scaled, inverse rotary) and dV for key = kw + 16j + li, dims 16u + 4g + (0..3)
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int key = kw + 16 * j + li;
+    if (key >= p.Lk) continue;
+    bf16* DK = p.dk + b * p.bdk + (long long)key * p.sdk + (long long)h * p.hd;
+    bf16* DV = p.dv + b * p.bdv + (long long)key * p.sdv + (long long)h * p.hd;
+#pragma unroll
+    for (int u = 0; u < NT; ++u) {
+      const int d = 16 * u + 4 * g;
+      if (d >= p.hd) continue;
+      float x[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) x[r] = dk[j][u][r] * p.scale;
+      if (p.rot) {
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const int pair = (h * p.hd + d) / 2 + e;
+          const float2 cs = ((const float2*)p.rot)[(long long)key * (p.rot_d / 2) + pair];
+          const float a = x[2 * e], cc = x[2 * e + 1];
+          x[2 * e] = a * cs.x + cc * cs.y;
+          x[2 * e + 1] = -a * cs.y + cc * cs.x;
+        }
+      }
+      *(bf16x4*)(DK + d) = (bf16x4){f2bf(x[0]), f2bf(x[1]), f2bf(x[2]), f2bf(x[3])};
+      *(bf16x4*)(DV + d) = (bf16x4){f2bf(dv[j][u][0]), f2bf(dv[j][u][1]), f2bf(dv[j][u][2]), f2bf(dv[j][u][3])};
+    }
+  }
+}
+
+template <int HDC>
+__global__ __launch_bounds__(512, 1) void attn_bwd8_kernel(AP p) {
+  __shared__ __attribute__((aligned(16))) char smem[8 * RowImg<HDC>::BYTES + 4 * Tile<64>::BYTES + 4 * 64 * 4];
+  int kb, h, b;
+  xcd_block(kb, h, b, p.causal ? 2 : 0);
+  attn_bwd8_tile<HDC>(p, smem, kb, h, b);
+}
+
 // One key block per workgroup. (Pairing key blocks x and nkb - 1 - x per workgroup, to even out the causal
 // sweeps, measured slower: 219 -> 247 us at the C2 shape, 629 -> 771 us at L = 1024 -- half the workgroups and
 // two serial prologues per workgroup cost more than the imbalance.)
@@ -936,13 +1273,14 @@ __global__ __launch_bounds__(256) void attn_dq_reduce_kernel(AP p) {
   if (i >= rows * D4) return;
   const int row = i / D4, c4 = i - row * D4;      // row = b * Lq + q
   const int b = row / p.Lq, q = row - b * p.Lq;
-  const int nkb = (p.Lk + BWD_KEYS - 1) / BWD_KEYS;
+  const int KB = p.kblk;
+  const int nkb = (p.Lk + KB - 1) / KB;
   const long long plane = (long long)rows * D;
-  const int nk = p.causal ? min(nkb, q / BWD_KEYS + 1) : nkb;
+  const int nk = p.causal ? min(nkb, q / KB + 1) : nkb;
   // sliding window: key block k >= 1 wrote partials only for the query tiles it swept (see attn_bwd_kernel)
   int k1 = 1;
   if (p.window > 0)
-    while (k1 < nk && q >= (min(p.Lq, k1 * BWD_KEYS + BWD_KEYS - SBLK + SBLK * p.window) + 63) / 64 * 64) ++k1;
+    while (k1 < nk && q >= (min(p.Lq, k1 * KB + KB - SBLK + SBLK * p.window) + 63) / 64 * 64) ++k1;
   const float* src = p.dq_part + (long long)row * D + 4 * c4;
   f32x4 acc = *(const f32x4*)src;
   int k = k1;
@@ -1018,14 +1356,27 @@ SVAE_EXPORT int svae_attn_bwd(const svae_attn_desc* d, svae_stream_t stream) {
   if (d->hd % 4 || (d->dq_bf && d->ldq_bf % 4) || (!d->dq_bf && d->bdq % 4)) return SVAE_EINVAL;
   if (d->dq_bf && d->rot_tab && d->rot_d != d->H * d->hd) return SVAE_EINVAL;
   if ((long long)d->B * d->Lq * (d->H * d->hd / 4) > 0x7FFFFF00LL) return SVAE_EINVAL;   // (32-bit dQ-reduce index)
+  // (the 8-wave kernel's DMA offsets are 32-bit byte offsets from a sequence's row 0)
+  if (((long long)std::max(d->Lq, d->Lk) + 64) * std::max(std::max(d->sq, d->sk), d->sdo) * 2 > 0x7FFFFFF0LL) return SVAE_EINVAL;
   hipStream_t s = (hipStream_t)stream;
   const int rows = d->B * d->Lq * d->H;
   if (d->hd <= 64) hipLaunchKernelGGL(attn_delta_kernel<8>, dim3((rows + 31) / 32), dim3(256), 0, s, p);
   else hipLaunchKernelGGL(attn_delta_kernel<16>, dim3((rows + 15) / 16), dim3(256), 0, s, p);
-  dim3 grid((d->Lk + BWD_KEYS - 1) / BWD_KEYS, d->H, d->B);
-  if (d->hd <= 64) hipLaunchKernelGGL(attn_bwd_kernel<64>, grid, dim3(256), 0, s, p);
-  else if (d->hd <= 96) hipLaunchKernelGGL((attn_bwd_kernel<128, 96>), grid, dim3(256), 0, s, p);
-  else hipLaunchKernelGGL(attn_bwd_kernel<128>, grid, dim3(256), 0, s, p);
+  // hd <= 96: the 8-wave 256-key kernel; hd 128: the 4-wave 128-key one (its LDS rows do not fit the 8-wave layout).
+  // SVAE_ATTN_BWD8=0: the 4-wave kernels for every hd (A/B runs)
+  static const int bwd8_env = [] { const char* e = getenv("SVAE_ATTN_BWD8"); return e ? atoi(e) : 1; }();
+  if (bwd8_env && d->hd <= 96) {
+    p.kblk = BWD8_KEYS;
+    dim3 grid8((d->Lk + BWD8_KEYS - 1) / BWD8_KEYS, d->H, d->B);
+    if (d->hd <= 64) hipLaunchKernelGGL(attn_bwd8_kernel<64>, grid8, dim3(512), 0, s, p);
+    else hipLaunchKernelGGL(attn_bwd8_kernel<96>, grid8, dim3(512), 0, s, p);
+  } else {
+    p.kblk = BWD_KEYS;
+    dim3 grid((d->Lk + BWD_KEYS - 1) / BWD_KEYS, d->H, d->B);
+    if (d->hd <= 64) hipLaunchKernelGGL(attn_bwd_kernel<64>, grid, dim3(256), 0, s, p);
+    else if (d->hd <= 96) hipLaunchKernelGGL((attn_bwd_kernel<128, 96>), grid, dim3(256), 0, s, p);
+    else hipLaunchKernelGGL(attn_bwd_kernel<128>, grid, dim3(256), 0, s, p);
+  }
   const long long work = (long long)d->B * d->Lq * (d->H * d->hd / 4);
   hipLaunchKernelGGL(attn_dq_reduce_kernel, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, s, p);
   SVAE_LAUNCH_CHECK();

@@ -34,6 +34,23 @@ __device__ __forceinline__ short4v lds_read_tr(const void* lds_addr) {
       (__attribute__((address_space(3))) short4v*)(uintptr_t)(lds_addr));
 }
 
+// The lane id recomputed where it is used (volatile: never hoisted or shared): per-lane DMA offsets derived from it
+// stay cheap to rematerialise instead of being computed once at kernel entry and spilled around the loop (a spill
+// reload's compiler-inserted vmcnt(0) drains the hand-counted DMA).
+__device__ __forceinline__ int lane_id_fresh() {
+  int l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return l;
+}
+
+// The same read from an address-space-3 pointer: base + compile-time offset folds into the instruction's offset field
+// (through the generic-pointer form the compiler materialised every offset in a VGPR of its own).
+typedef __attribute__((address_space(3))) char lds_char;
+__device__ __forceinline__ const lds_char* lds_ptr(const void* p) { return (const lds_char*)(uintptr_t)p; }
+__device__ __forceinline__ short4v lds_read_tr3(const lds_char* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4v*)p);
+}
+
 // LDS-DMA of 16 B per lane (buffer_load_dwordx4 ... lds) into lds_base + 16 * lane, from rsrc + voff (bytes;
 // out-of-range offsets land as zeros). Issued through inline asm on purpose: the compiler's wait-count pass
 // would otherwise treat every later ds_read_b64_tr_b16 as a possible reader of the DMA destination and put a

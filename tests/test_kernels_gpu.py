@@ -413,6 +413,9 @@ def _attn_ref(q, k, v, pad, causal, scale):
     (2, 8, 64, 64, 16, False, False, False),
     (2, 2, 512, 512, 64, True, True, False),
     (1, 2, 300, 520, 64, False, True, False),
+    (1, 2, 1024, 1024, 96, True, True, False),     # C4 decoder head dim: 4 key blocks of 256, ragged padding
+    (2, 2, 600, 600, 96, True, False, False),      # hd 96, last key block partial (600 = 2 x 256 + 88)
+    (2, 4, 64, 520, 64, False, True, True),        # learned queries over 3 key blocks (the encoder's first layer)
 ])
 def test_attention_fwd_bwd(B, H, Lq, Lk, hd, causal, padded, learned):
     torch.manual_seed(Lq * 7 + hd)
