@@ -98,6 +98,15 @@ int svae_gemm_pair(const svae_gemm_desc* d0, const svae_gemm_desc* d1, svae_stre
  * Backward: dx = dres + LN'(dy) (dres may be NULL), written f32 to dx and (optionally) bf16 to dx_bf;
  * per-block partial (dw, db) sums go to part[nblk][2][D] (reduce with svae_colsum). Rows with
  * (row % zero_mod == 0) get dx = 0 when zero_mod > 0 (position-0 overwrite, transformer_vae.py:89-90). */
+/* Residual add + dropout + LayerNorm forward (transformer_layer.py:49-50, :58-61 and the following LayerNorm, :47 / :56),
+ * one pass: v = x[r] + dropout(y[r]) (x f32 [rows][D] or NULL; y bf16 [rows][ldy] -- the projection's output -- or
+ * NULL; y_dtype 0 = f32, 1 = bf16; dropout with the counter RNG of SVAE_EPI_DROPOUT_RESID: seed, index (r * D + c) / 4),
+ * or v = zrows[r / zmod]
+ * where zrows != NULL and r % zmod == 0 (the z splice, transformer_vae.py:89-90); xo f32 = v (may be NULL);
+ * h bf16 = LayerNorm(v) * w + b with mean / rstd, or h = bf16(v) when w == b == NULL. D % 8 == 0, D <= 1024. */
+int svae_resid_ln_fwd(const float* x, const void* y, int32_t y_dtype, int64_t ldy, float drop_p, uint64_t seed,
+                      const float* zrows, int32_t zmod, const float* w, const float* b, float* xo, void* h, float* mean,
+                      float* rstd, int32_t rows, int32_t D, svae_stream_t stream);
 int svae_layernorm_fwd(const void* x, int32_t x_dtype, const float* w, const float* b, void* y,
                        float* mean, float* rstd, int32_t rows, int32_t D, svae_stream_t stream);
 int svae_layernorm_bwd(const void* dy, const void* x, int32_t x_dtype, const float* w, const float* mean,

@@ -148,7 +148,6 @@ __device__ __forceinline__ void wait_vmcnt(int n) {
 // end: a tail of idle CUs; list-scheduling model of the C2 decoder shape: backward makespan 29 -> 24 block-tiles,
 // forward 21 -> 17; measured at C2: forward 59.3 -> 52.6 us, backward + delta + dQ reduce 202 -> 182 us).
 __device__ __forceinline__ void xcd_block(int& x, int& y, int& z, int lpt = 0) {
-#ifndef SVAE_ATTN_NO_XCD
   const int gx = gridDim.x, gy = gridDim.y;
   const int n = gx * gy * gridDim.z;
   const int lin = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
@@ -172,9 +171,6 @@ __device__ __forceinline__ void xcd_block(int& x, int& y, int& z, int lpt = 0) {
   x = l % gx;
   y = (l / gx) % gy;
   z = l / (gx * gy);
-#else
-  x = blockIdx.x; y = blockIdx.y; z = blockIdx.z;
-#endif
 }
 
 #ifdef SVAE_STAMPS
@@ -187,9 +183,7 @@ __device__ unsigned long long svae_attn_stamps[1024][6];
 #define ATTN_STAMP(k, v) ((void)0)
 #endif
 
-#ifndef ATTN_NS
-#define ATTN_NS 2   // (3 stages with the XCD order: 70.7 vs 67.5 us)
-#endif
+constexpr int ATTN_NS = 2;   // K/V ring stages (3 stages with the XCD order: 70.7 vs 67.5 us)
 
 
 // One 128-query tile of one (batch, head). smem: the K/V ring + key-padding ring of the kernel. HDP: the LDS row

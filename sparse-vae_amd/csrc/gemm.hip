@@ -594,19 +594,6 @@ __global__ __launch_bounds__(256, 3) void gemm_glds_kernel(GP p) {
 // f32 through the (then idle) LDS and handed to the shared vectorised epilogue, one 128-column half per
 // 256 threads.
 constexpr int G3_T = 256 * 64 * 2;   // 32 KiB per operand K-tile
-#ifndef SVAE_G3_PRIO
-#define SVAE_G3_PRIO 0
-#endif
-#ifndef SVAE_G3_RS_EARLY
-#define SVAE_G3_RS_EARLY 0   // A/B: bias-gradient row sums between quadrants 1|2 and 3|4 instead of after 2 and 4
-#endif
-#if SVAE_G3_PRIO
-#define G3_PRIO_HI() __builtin_amdgcn_s_setprio(1)
-#define G3_PRIO_LO() __builtin_amdgcn_s_setprio(0)
-#else
-#define G3_PRIO_HI() ((void)0)
-#define G3_PRIO_LO() ((void)0)
-#endif
 constexpr int G3_STAGE = 2 * G3_T;
 
 // Per-lane DMA source offsets of one operand's K-tile, hoisted out of the K loop: only the tile base (a
@@ -722,9 +709,6 @@ __device__ __forceinline__ void g3_epilogue(const GP& p, char* smem, const f32x4
 // waves through the side area into the 128-column partials ce_rows_kernel expects; the label logit is written
 // by the lane holding it.
 constexpr float G3_LOG2E = 1.4426950408889634f;
-#ifndef SVAE_P_NT
-#define SVAE_P_NT 0   // P-head stores: cached (A/B: -DSVAE_P_NT=1 nontemporal)
-#endif
 
 __device__ __forceinline__ unsigned pack_bf16x2(float a, float b) {
   typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
@@ -869,7 +853,7 @@ __device__ __forceinline__ void g3_reg_epilogue(const GP& p, const f32x4 (&acc)[
                 x2[h][e + 1] = x[1];
                 se2 += x;
               }
-            store_pair_bf16<SVAE_P_NT != 0>(crow, 32 * jp, row_ok ? nleft : 0, x2[0], x2[1], g);
+            store_pair_bf16(crow, 32 * jp, row_ok ? nleft : 0, x2[0], x2[1], g);   // cached stores
           }
         };
         if (__builtin_amdgcn_readfirstlane((int)(n0 + wc * 64 + 64 > p.N))) body(BoolC<true>{});
@@ -1276,29 +1260,18 @@ __device__ __forceinline__ void gemm256_run(const GP& p, int blk, int nwg) {
       for (int j = 0; j < 2; ++j)
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) b1[j][ks] = g3_bfrag<BT>(lb, wc * 64 + 32 + j * 16, ks, lane);
-      G3_PRIO_HI();
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int j = 0; j < 2; ++j) acc[i][j] = mfma16(b0[j][ks], a0[i][ks], acc[i][j]);
-      G3_PRIO_LO();
-#if SVAE_G3_RS_EARLY
-      if constexpr (AT) {   // the row sums between two quadrants, under the MFMAs already in the pipe
-        if (do_rs) {
-          if (wc == 0) rowsum2(a0[0], a0[1]);
-          else if (wc == 1) rowsum2(a0[2], a0[3]);
-        }
-      }
-#endif
       if constexpr (!AT) {   // (AT: transposed A reads need the registers; load after the a0 quadrants)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int ks = 0; ks < 2; ++ks) a1[i][ks] = g3_afrag<AT>(la, wr * 128 + 64 + i * 16, ks, lane);
       }
-      G3_PRIO_HI();
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
@@ -1306,18 +1279,14 @@ __device__ __forceinline__ void gemm256_run(const GP& p, int blk, int nwg) {
 #pragma unroll
           for (int j = 0; j < 2; ++j) acc[i][2 + j] = mfma16(b1[j][ks], a0[i][ks], acc[i][2 + j]);
       if constexpr (AT) {
-        G3_PRIO_LO();
-#if !SVAE_G3_RS_EARLY
         if (do_rs) {
           if (wc == 0) rowsum2(a0[0], a0[1]);
           else if (wc == 1) rowsum2(a0[2], a0[3]);
         }
-#endif
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int ks = 0; ks < 2; ++ks) a1[i][ks] = g3_afrag<AT>(la, wr * 128 + 64 + i * 16, ks, lane);
-        G3_PRIO_HI();
       }
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
@@ -1325,28 +1294,17 @@ __device__ __forceinline__ void gemm256_run(const GP& p, int blk, int nwg) {
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int j = 0; j < 2; ++j) acc[4 + i][2 + j] = mfma16(b1[j][ks], a1[i][ks], acc[4 + i][2 + j]);
-#if SVAE_G3_RS_EARLY
-      if constexpr (AT) {
-        if (do_rs) {
-          if (wc == 2) rowsum2(a1[0], a1[1]);
-          else if (wc == 3) rowsum2(a1[2], a1[3]);
-        }
-      }
-#endif
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int j = 0; j < 2; ++j) acc[4 + i][j] = mfma16(b0[j][ks], a1[i][ks], acc[4 + i][j]);
-      G3_PRIO_LO();
       if constexpr (AT) {
-#if !SVAE_G3_RS_EARLY
         if (do_rs) {
           if (wc == 2) rowsum2(a1[0], a1[1]);
           else if (wc == 3) rowsum2(a1[2], a1[3]);
         }
-#endif
       }
     }
     G3_STAMP(1);

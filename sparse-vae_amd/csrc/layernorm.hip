@@ -112,6 +112,122 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, co
   if (lane == 0) { mean_out[row] = mean; rstd_out[row] = rstd; }
 }
 
+// Residual add + dropout + LayerNorm, fused (the TransformerLayer's "x = x + y" followed by the next LayerNorm,
+// transformer_layer.py:49-50 / :56 and :58-61 + the next layer's :47): one wave per row, 8 consecutive columns per lane.
+//   v = x[r] + dropout(y[r])          (x may be NULL: no residual; y f32 or bf16, the projection GEMM's output; dropout with the
+//                                      counter RNG of the GEMM epilogues: index (r * D + c) / 4, keep u >= p, scale 1/(1-p))
+//   v = zrows[r / zmod]  when zrows and r % zmod == 0   (the z splice of transformer_vae.py:89-90)
+//   xo[r] = v (f32, when xo); h[r] = LN(v) * w + b (bf16) and mean / rstd when w, else h[r] = bf16(v).
+// Moves 14 B per element with an f32 y (x, y in; xo, h out): the residual add and the dropout leave the GEMM epilogue (which ran with
+// no MFMA beside it: the f32 + residual epilogue cost 2x a bf16 store at the C2 FFN2 shape) for this HBM-bound pass.
+template <int NR, typename TY>
+__global__ __launch_bounds__(256) void resid_ln_fwd_kernel(const float* __restrict__ x, const TY* __restrict__ y,
+                                                           long long ldy, float drop_p, unsigned long long seed,
+                                                           const float* __restrict__ zrows, int zmod,
+                                                           const float* __restrict__ w, const float* __restrict__ b,
+                                                           float* __restrict__ xo, bf16* __restrict__ h,
+                                                           float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                           int rows, int D) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const bool zr = zrows && row % zmod == 0;      // wave-uniform
+  const float sc = drop_p > 0.f ? 1.0f / (1.0f - drop_p) : 1.0f;
+  f32x4 v[NR][2];
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < NR; ++j) {
+    const int c = (lane + 64 * j) * 8;
+    const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+    v[j][0] = z4;
+    v[j][1] = z4;
+    if (c < D) {
+      if (zr) {
+        const float* zp = zrows + (long long)(row / zmod) * D + c;
+        v[j][0] = *(const f32x4*)zp;
+        v[j][1] = *(const f32x4*)(zp + 4);
+      } else {
+        if (x) {
+          v[j][0] = *(const f32x4*)(x + (long long)row * D + c);
+          v[j][1] = *(const f32x4*)(x + (long long)row * D + c + 4);
+        }
+        if (y) {
+          float yy[8];
+          if constexpr (sizeof(TY) == 2) {
+            const bf16x8 t = *(const bf16x8*)(y + (long long)row * ldy + c);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) yy[e] = (float)t[e];
+          } else {
+            const f32x4 t0 = *(const f32x4*)(y + (long long)row * ldy + c), t1 = *(const f32x4*)(y + (long long)row * ldy + c + 4);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) { yy[e] = t0[e]; yy[4 + e] = t1[e]; }
+          }
+          float u[8] = {1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f};
+          if (drop_p > 0.f) {
+            float u0[4], u1[4];
+            rand_uniform4(seed, ((unsigned long long)row * D + c) >> 2, u0);
+            rand_uniform4(seed, ((unsigned long long)row * D + c + 4) >> 2, u1);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) { u[e] = u0[e]; u[4 + e] = u1[e]; }
+          }
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float t = yy[e];
+            const float d = drop_p > 0.f ? (u[e] >= drop_p ? t * sc : 0.f) : t;
+            v[j][e >> 2][e & 3] += d;
+          }
+        }
+      }
+      s += (v[j][0][0] + v[j][0][1]) + (v[j][0][2] + v[j][0][3]) + (v[j][1][0] + v[j][1][1]) + (v[j][1][2] + v[j][1][3]);
+      if (xo) {
+        *(f32x4*)(xo + (long long)row * D + c) = v[j][0];
+        *(f32x4*)(xo + (long long)row * D + c + 4) = v[j][1];
+      }
+    }
+  }
+  if (!w) {                                      // no LayerNorm: the bf16 copy of v
+#pragma unroll
+    for (int j = 0; j < NR; ++j) {
+      const int c = (lane + 64 * j) * 8;
+      if (c < D) {
+        bf16x8 o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = f2bf(v[j][e >> 2][e & 3]);
+        *(bf16x8*)(h + (long long)row * D + c) = o;
+      }
+    }
+    return;
+  }
+  const float mean = wave_sum(s) / D;
+  float sq = 0.f;
+#pragma unroll
+  for (int j = 0; j < NR; ++j) {
+    const int c = (lane + 64 * j) * 8;
+    if (c < D) {
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { const float t = v[j][hh][e] - mean; sq += t * t; }
+    }
+  }
+  const float rstd = rsqrtf(wave_sum(sq) / D + 1e-5f);
+#pragma unroll
+  for (int j = 0; j < NR; ++j) {
+    const int c = (lane + 64 * j) * 8;
+    if (c < D) {
+      bf16x8 o;
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        const f32x4 ww = *(const f32x4*)(w + c + 4 * hh), bb = *(const f32x4*)(b + c + 4 * hh);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[4 * hh + e] = f2bf((v[j][hh][e] - mean) * rstd * ww[e] + bb[e]);
+      }
+      *(bf16x8*)(h + (long long)row * D + c) = o;
+    }
+  }
+  if (lane == 0) { mean_out[row] = mean; rstd_out[row] = rstd; }
+}
+
 template <typename T, int MAXV>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16* __restrict__ dy, const T* __restrict__ x,
                                                      const float* __restrict__ w, const float* __restrict__ mean_in,
@@ -258,6 +374,29 @@ SVAE_EXPORT int svae_layernorm_fwd(const void* x, int32_t x_dtype, const float* 
   else if (D <= 768) SVAE_LN_FWD(3);
   else SVAE_LN_FWD(5);
 #undef SVAE_LN_FWD
+  SVAE_LAUNCH_CHECK();
+  return SVAE_OK;
+}
+
+SVAE_EXPORT int svae_resid_ln_fwd(const float* x, const void* y, int32_t y_dtype, int64_t ldy, float drop_p,
+                                  uint64_t seed, const float* zrows, int32_t zmod, const float* w, const float* b,
+                                  float* xo, void* h, float* mean, float* rstd, int32_t rows, int32_t D,
+                                  svae_stream_t stream) {
+  if (!h || rows <= 0 || D <= 0 || D % 8 || D > 1024 || (!x && !y && !zrows) || (y_dtype != 0 && y_dtype != 1))
+    return SVAE_EINVAL;
+  if ((w == nullptr) != (b == nullptr) || (w && (!mean || !rstd)) || (zrows && zmod <= 0)) return SVAE_EINVAL;
+  if (drop_p < 0.f || drop_p >= 1.f || (y && ldy % 8) || (((uintptr_t)y | (uintptr_t)h) & 15)) return SVAE_EINVAL;
+  dim3 grid((rows + 3) / 4);
+  hipStream_t s = (hipStream_t)stream;
+#define SVAE_RLN(NR, TY)                                                                                          \
+  hipLaunchKernelGGL((resid_ln_fwd_kernel<NR, TY>), grid, dim3(256), 0, s, x, (const TY*)y, (long long)ldy, drop_p, \
+                     (unsigned long long)seed, zrows, zmod, w, b, xo, (bf16*)h, mean, rstd, rows, D)
+  if (D <= 512) {
+    if (y_dtype == 0) SVAE_RLN(1, float); else SVAE_RLN(1, bf16);
+  } else {
+    if (y_dtype == 0) SVAE_RLN(2, float); else SVAE_RLN(2, bf16);
+  }
+#undef SVAE_RLN
   SVAE_LAUNCH_CHECK();
   return SVAE_OK;
 }

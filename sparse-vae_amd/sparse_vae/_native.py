@@ -62,6 +62,8 @@ class AttnDesc(ctypes.Structure):
 _SIGS = {
     'svae_gemm': [ctypes.POINTER(GemmDesc), c_void_p],
     'svae_gemm_pair': [ctypes.POINTER(GemmDesc), ctypes.POINTER(GemmDesc), c_void_p],
+    'svae_resid_ln_fwd': [c_void_p, c_void_p, c_int32, c_int64, c_float, c_uint64, c_void_p, c_int32, c_void_p,
+                          c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p],
     'svae_layernorm_fwd': [c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32,
                            c_void_p],
     'svae_layernorm_bwd': [c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

@@ -238,6 +238,9 @@ class VAEEngine:
         # the two dW GEMMs of the FFN, and the attention output projection's with the Q/K/V projection's, run as one
         # paired launch each (kernels.linear_dw_pair); SVAE_DW_PAIR=0 launches them one by one (A/B runs)
         self.dw_pair = os.environ.get('SVAE_DW_PAIR', '1') != '0'
+        # decoder residual adds in the fused residual + dropout + LayerNorm pass (layer_fwd's fuse); SVAE_FUSE_LN=0: the
+        # projections' f32 residual epilogues and separate LayerNorms (A/B runs)
+        self.fuse_ln = os.environ.get('SVAE_FUSE_LN', '1') != '0'
         self.side = None
         if flat.device.type == 'cuda' and os.environ.get('SVAE_DW_STREAM', '0') != '0':
             self.side = torch.cuda.Stream(device=flat.device)
@@ -315,16 +318,28 @@ class VAEEngine:
 
     # ------------------------------------------------------------------ one transformer layer
     def layer_fwd(self, pre, x, B, Sx, L, pad, *, learned=0, cross=False, causal=False, ctx=None, heads, hd,
-                  drop_p=0.0, seed=0, tag, out=None, window=0):
+                  drop_p=0.0, seed=0, tag, out=None, window=0, fuse=False, h_in=None, next_ln=None, out_bf=None):
         """TransformerLayer.forward (transformer_layer.py:44-61) on x f32 [B*Sx, d]. Returns the f32 output
-        [B*Lq, d] and the saved state for layer_bwd. window > 0: sliding-window self-attention."""
+        [B*Lq, d] and the saved state for layer_bwd. window > 0: sliding-window self-attention.
+
+        fuse (no cross-attention): the two residual adds run in the fused residual + dropout + LayerNorm pass
+        (svae_resid_ln_fwd) instead of the projection GEMMs' f32 epilogues -- the out-projection writes bf16 and the
+        pass makes x1 = x + y and LayerNorm_f(x1); the FFN output is added (with its dropout) by the same pass fused
+        with the NEXT layer's attention LayerNorm: next_ln = (LayerNorm name, z rows [B, d] f32, L, next tag) -- the z
+        splice's rows are taken from the z rows -- which leaves (h, (x, mean, rstd)) in st['next_h'] for the next
+        layer's h_in; without next_ln (the last layer) only the bf16 copy of the output is written, into out_bf (the
+        head's input)."""
         d, ws, P = self.d, self.ws, self.P
         rows_x = B * Sx
         rot = self.rot(max(Sx, L), window)
         st = {'pre': pre, 'B': B, 'Sx': Sx, 'L': L, 'learned': learned, 'cross': cross, 'causal': causal,
               'heads': heads, 'hd': hd, 'drop_p': drop_p, 'seed': seed, 'x': x, 'tag': tag, 'window': window}
         a = pre + 'attention.'
-        h, st['ln_a'] = self._ln_fwd(pre + 'attn_layer_norm', x, rows_x, tag + '.ln_a')
+        fuse = fuse and not cross
+        if h_in is not None:
+            h, st['ln_a'] = h_in
+        else:
+            h, st['ln_a'] = self._ln_fwd(pre + 'attn_layer_norm', x, rows_x, tag + '.ln_a')
         st['h'] = h
         pad_k = pad if Sx == L else None          # PaddedTensor getter: mask iff key length == L
         if learned:
@@ -355,8 +370,20 @@ class VAEEngine:
         st.update(O=O, O32=O32, lse=lse, Lq=Lq, pad_k=pad_k)
         resid = Lq == Sx                           # transformer_layer.py:49
         x1 = ws.get(tag + '.x1', (rows_q, d), f32)
-        K.gemm(O, P.w(a + 'output_linear.weight'), x1, rows_q, d, d, epi=EPI_F32, bias=P.f(a + 'output_linear.bias'),
-               resid=x if resid else None, ldr=d)
+        if fuse:
+            # (the projection output stays f32: rounded to bf16 before the residual add it moved the C5-shape bottleneck
+            # key gradient -- a cancellation residual -- past its 2 % parity bar)
+            ya = ws.get('fuse.y', (rows_q, d), f32)
+            K.gemm(O, P.w(a + 'output_linear.weight'), ya, rows_q, d, d, epi=EPI_F32, bias=P.f(a + 'output_linear.bias'))
+            nm = pre + 'ffn_layer_norm'
+            h2 = ws.get(tag + '.ln_f.y', (rows_q, d))
+            mf, rf = ws.get(tag + '.ln_f.mean', (rows_q,), f32), ws.get(tag + '.ln_f.rstd', (rows_q,), f32)
+            K.resid_ln_fwd(x if resid else None, ya, h2, rows_q, d, w=P.f(nm + '.weight'), b=P.f(nm + '.bias'), mean=mf,
+                           rstd=rf, xo=x1)
+            st['ln_f'] = (x1, mf, rf)
+        else:
+            K.gemm(O, P.w(a + 'output_linear.weight'), x1, rows_q, d, d, epi=EPI_F32,
+                   bias=P.f(a + 'output_linear.bias'), resid=x if resid else None, ldr=d)
         st['resid'] = resid
         st['x1'] = x1
         xc = x1
@@ -383,14 +410,30 @@ class VAEEngine:
                    bias=P.f(c + 'output_linear.bias'), resid=x1, ldr=d)
             st.update(cx=cx, hq=hq, qc=qc, kvc=kvc, Oc=Oc, lsec=lsec, x2=x2, pad_ctx=pad)
             xc = x2
-        h2, st['ln_f'] = self._ln_fwd(pre + 'ffn_layer_norm', xc, rows_q, tag + '.ln_f')
+        if not fuse:
+            h2, st['ln_f'] = self._ln_fwd(pre + 'ffn_layer_norm', xc, rows_q, tag + '.ln_f')
         gprime = ws.get(tag + '.gprime', (rows_q, 4 * d))   # gelu'(pre-activation), saved by the epilogue
         f = ws.get(tag + '.f', (rows_q, 4 * d))
         K.gemm(h2, P.w(pre + 'ffn.0.weight'), f, rows_q, 4 * d, d, epi=EPI_GELU, bias=P.f(pre + 'ffn.0.bias'),
                aux=gprime, ldaux=4 * d)
-        out = ws.get(tag + '.out', (rows_q, d), f32) if out is None else out
-        K.gemm(f, P.w(pre + 'ffn.2.weight'), out, rows_q, d, 4 * d, epi=EPI_DROPOUT_RESID, resid=xc, ldr=d,
-               drop_p=drop_p, seed=seed)
+        if fuse:
+            yf = ws.get('fuse.y', (rows_q, d), f32)
+            K.gemm(f, P.w(pre + 'ffn.2.weight'), yf, rows_q, d, 4 * d, epi=EPI_F32)
+            if next_ln is not None:
+                nm, zrows, zmod, ntag = next_ln
+                out = ws.get(tag + '.out', (rows_q, d), f32) if out is None else out
+                hn = ws.get(ntag + '.ln_a.y', (rows_q, d))
+                mn, rn = ws.get(ntag + '.ln_a.mean', (rows_q,), f32), ws.get(ntag + '.ln_a.rstd', (rows_q,), f32)
+                K.resid_ln_fwd(xc, yf, hn, rows_q, d, w=P.f(nm + '.weight'), b=P.f(nm + '.bias'), mean=mn, rstd=rn,
+                               xo=out, drop_p=drop_p, seed=seed, zrows=zrows, zmod=zmod)
+                st['next_h'] = (hn, (out, mn, rn))
+            else:
+                assert out_bf is not None, 'the last fused layer writes the bf16 copy of its output'
+                K.resid_ln_fwd(xc, yf, out_bf, rows_q, d, xo=out, drop_p=drop_p, seed=seed)
+        else:
+            out = ws.get(tag + '.out', (rows_q, d), f32) if out is None else out
+            K.gemm(f, P.w(pre + 'ffn.2.weight'), out, rows_q, d, 4 * d, epi=EPI_DROPOUT_RESID, resid=xc, ldr=d,
+                   drop_p=drop_p, seed=seed)
         st.update(h2=h2, gprime=gprime, f=f, xc=xc, rows_q=rows_q)
         return out, st
 
@@ -543,11 +586,9 @@ class VAEEngine:
         sv.update(enc_bf=enc_bf, stats=stats, z_bf=zb, eps=eps_buf)
 
         # ---- decoder (transformer_vae.py:85-93), position 0 replaced by z_projections[i](z) every layer
-        xs, sv['dec_layers'] = self._decode(x_emb, zb, padm, B, L, dropout, seed, x_ready=True)
+        xf, sv['dec_layers'] = self._decode(x_emb, zb, padm, B, L, dropout, seed, x_ready=True)
 
         # ---- output head + cross entropy (transformer_language_model.py:55-63, language_model.py:161-170)
-        xf = ws.get('xf_bf', (T, d))
-        K.cast_bf16(xs, xf)
         gp0 = ws.get('h0_gprime', (T, d))
         h0 = ws.get('h0', (T, d))
         K.gemm(xf, P.w('output_layer.0.weight'), h0, T, d, d, epi=EPI_GELU, bias=P.f('output_layer.0.bias'),
@@ -705,8 +746,8 @@ class VAEEngine:
                 zf.view(ng, nb, Z).copy_(z[g0:g1, b0:b1])
                 zb = ws.get('z_bf', (B, Z))
                 K.cast_bf16(zf, zb)
-                xs, _ = self._decode(xe, zb, padm, B, L, 0.0, 0)
-                hh = self._head_hidden(xs, T)
+                xf, _ = self._decode(xe, zb, padm, B, L, 0.0, 0)
+                hh = self._head_hidden(xf, T)
                 part = ws.get('ce.part', (T, ntile, 2), f32)
                 lab_logit = ws.get('ce.label_logit', (T,), f32)
                 K.gemm(hh, P.w('input_layer.0.weight'), None, T, V, d, epi=EPI_CE_STATS,
@@ -716,12 +757,10 @@ class VAEEngine:
                 out[g0:g1, b0:b1].copy_(res.view(ng, nb))
         return out
 
-    def _head_hidden(self, xs, T):
+    def _head_hidden(self, xf, T):
         """output_layer[:3] (transformer_language_model.py:55-61): LayerNorm(GELU(Linear(x))) as the bf16
-        operand of the tied vocabulary GEMM."""
+        operand of the tied vocabulary GEMM, from the decoder's bf16 output xf."""
         d, ws, P = self.d, self.ws, self.P
-        xf = ws.get('xf_bf', (T, d))
-        K.cast_bf16(xs, xf)
         gp0 = ws.get('h0_gprime', (T, d))
         h0 = ws.get('h0', (T, d))
         K.gemm(xf, P.w('output_layer.0.weight'), h0, T, d, d, epi=EPI_GELU, bias=P.f('output_layer.0.bias'),
@@ -730,23 +769,47 @@ class VAEEngine:
         return hh
 
     def _decode(self, x_emb, zb, padm, B, L, dropout, seed, x_ready=False):
+        """The decoder stack of reconstruct (transformer_vae.py:85-93). Returns the bf16 copy of the last layer's
+        output [T, d] (the head's input; its f32 is not needed by any pass) and the layers' saved state.
+        Position 0 of every layer's input is z_projections[i](z): for layer 0 written into the embedding copy, for
+        the later layers into a [B, d] buffer the fused residual + LayerNorm pass of the layer below takes those rows
+        from (SVAE_FUSE_LN=0: the round-2 path, f32 GEMM epilogues + separate LayerNorms, for A/B runs)."""
         hp, d, ws, P = self.hp, self.d, self.ws, self.P
         T, Z = B * L, hp.latent_depth
         if self.window and L % 32:
             raise ValueError(f'sparse decoder attention needs seq_len % 32 == 0 (SparseAttention block_size 32, '
                              f'sparse_attention.py:81), got {L}')
+        fuse = self.fuse_ln
         xs = ws.get('x_dec0', (T, d), f32)
         if not x_ready:   # (the training forward's embedding gather wrote it already)
             xs.copy_(x_emb)
+        xf = ws.get('xf_bf', (T, d))
         dec = []
+        h_in = None
+        K.gemm(zb, P.w('z_projections.0.weight'), xs, B, d, Z, ldc=L * d, epi=EPI_F32, bias=P.f('z_projections.0.bias'))
         for i in range(hp.num_layers):
-            K.gemm(zb, P.w(f'z_projections.{i}.weight'), xs, B, d, Z, ldc=L * d, epi=EPI_F32,
-                   bias=P.f(f'z_projections.{i}.bias'))
+            last = i + 1 == hp.num_layers
+            if fuse:
+                nxt = None
+                if not last:
+                    zrows = ws.get('zrows', (B, d), f32)
+                    K.gemm(zb, P.w(f'z_projections.{i + 1}.weight'), zrows, B, d, Z, epi=EPI_F32,
+                           bias=P.f(f'z_projections.{i + 1}.bias'))
+                    nxt = (f'decoder_layers.{i + 1}.attn_layer_norm', zrows, L, f'd{i + 1}')
+                out = None if last else ws.get(f'x_dec{i + 1}', (T, d), f32)
+            else:
+                if i > 0:
+                    K.gemm(zb, P.w(f'z_projections.{i}.weight'), xs, B, d, Z, ldc=L * d, epi=EPI_F32,
+                           bias=P.f(f'z_projections.{i}.bias'))
+                nxt, out = None, ws.get(f'x_dec{i + 1}', (T, d), f32)
             xs, st = self.layer_fwd(f'decoder_layers.{i}.', xs, B, L, L, padm, causal=True, heads=self.H,
-                                    hd=self.hd, drop_p=dropout, seed=_mix_seed(seed, i), tag=f'd{i}',
-                                    out=ws.get(f'x_dec{i + 1}', (T, d), f32), window=self.window)
+                                    hd=self.hd, drop_p=dropout, seed=_mix_seed(seed, i), tag=f'd{i}', out=out,
+                                    window=self.window, fuse=fuse, h_in=h_in, next_ln=nxt, out_bf=xf if last else None)
+            h_in = st.pop('next_h', None)
             dec.append(st)
-        return xs, dec
+        if not fuse:
+            K.cast_bf16(xs, xf)
+        return xf, dec
 
     def reconstruct_f32(self, x_emb, z, pad=None):
         """reconstruct() in the fp32 kernel mode (f32-input MFMA GEMMs, f32 attention / LayerNorm): logits
@@ -801,9 +864,7 @@ class VAEEngine:
             padm.copy_(pad)
         zb = ws.get('z_bf', (B, Z))
         K.cast_bf16(z, zb)
-        xs, _ = self._decode(x_emb.reshape(T, d), zb, padm, B, L, 0.0, 0)
-        xf = ws.get('xf_bf', (T, d))
-        K.cast_bf16(xs, xf)
+        xf, _ = self._decode(x_emb.reshape(T, d), zb, padm, B, L, 0.0, 0)
         gp0 = ws.get('h0_gprime', (T, d))
         h0 = ws.get('h0', (T, d))
         K.gemm(xf, P.w('output_layer.0.weight'), h0, T, d, d, epi=EPI_GELU, bias=P.f('output_layer.0.bias'),

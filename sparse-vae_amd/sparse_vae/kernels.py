@@ -148,6 +148,18 @@ def _slab_workspace(n, device):
     return t
 
 
+def resid_ln_fwd(x, y, h, rows, D, *, w=None, b=None, mean=None, rstd=None, xo=None, drop_p=0.0, seed=0, zrows=None,
+                 zmod=0):
+    """svae_resid_ln_fwd: v = x + dropout(y) (or zrows[r // zmod] on rows r % zmod == 0); xo = v; h = LN(v) (or bf16(v)
+    without w / b)."""
+    _dev(h, *(t for t in (x, y, xo, zrows, w, b, mean, rstd) if t is not None))
+    assert h.dtype == bf16 and (y is None or y.dtype in (bf16, f32)) and (x is None or x.dtype == f32)
+    check(lib.svae_resid_ln_fwd(ptr(x), ptr(y), 1 if y is not None and y.dtype == bf16 else 0,
+                                y.stride(0) if y is not None else 0, float(drop_p), int(seed) & (2 ** 64 - 1),
+                                ptr(zrows), int(zmod), ptr(w), ptr(b), ptr(xo), h.data_ptr(), ptr(mean), ptr(rstd), rows,
+                                D, stream()), 'svae_resid_ln_fwd')
+
+
 def layernorm_fwd(x, w, b, y, mean, rstd, rows, D):
     _dev(x, w, b, y, mean, rstd)
     check(lib.svae_layernorm_fwd(x.data_ptr(), 0 if x.dtype == f32 else 1, w.data_ptr(), b.data_ptr(), y.data_ptr(),

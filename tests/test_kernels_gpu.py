@@ -641,3 +641,44 @@ def test_transpose_blocks_exact():
     torch.cuda.synchronize()
     for o, r, c in blocks:
         assert torch.equal(dst[o:o + r * c].view(c, r), src[o:o + r * c].view(r, c).t())
+
+
+@pytest.mark.parametrize('D,p,with_x,with_z,with_ln,ydt', [(512, 0.1, True, True, True, 'f32'),
+                                                           (768, 0.0, True, False, True, 'f32'),
+                                                           (512, 0.3, True, False, False, 'bf16'),
+                                                           (256, 0.0, False, False, True, 'bf16'),
+                                                           (768, 0.25, True, True, True, 'bf16')])
+def test_resid_ln_fwd(D, p, with_x, with_z, with_ln, ydt):
+    """svae_resid_ln_fwd (the decoder's fused residual add + dropout + LayerNorm) against torch: v = x + dropout(y)
+    with the mask of the counter RNG (recovered from dropout_bwd_cast of ones, the same index (r * D + c) / 4), the z
+    rows on r % L == 0; xo bit-exact, LayerNorm 1e-2 rel in bf16, mean / rstd 1e-5."""
+    torch.manual_seed(D + int(10 * p))
+    L, B = 64, 6
+    rows = B * L
+    x = torch.randn(rows, D, device=dev) if with_x else None
+    y = torch.randn(rows, D, device=dev)
+    y = y.bfloat16() if ydt == 'bf16' else y
+    zr = torch.randn(B, D, device=dev) if with_z else None
+    w, b = 1 + 0.1 * torch.randn(D, device=dev), 0.1 * torch.randn(D, device=dev)
+    seed = 12345 + D
+    h = torch.empty(rows, D, device=dev, dtype=torch.bfloat16)
+    xo = torch.empty(rows, D, device=dev)
+    mean, rstd = torch.empty(rows, device=dev), torch.empty(rows, device=dev)
+    K.resid_ln_fwd(x, y, h, rows, D, w=w if with_ln else None, b=b if with_ln else None, mean=mean if with_ln else None,
+                   rstd=rstd if with_ln else None, xo=xo, drop_p=p, seed=seed, zrows=zr, zmod=L if with_z else 0)
+    keep = torch.empty(rows, D, device=dev, dtype=torch.bfloat16)
+    K.dropout_bwd_cast(torch.ones(rows, D, device=dev), keep, p, seed, rows, D)
+    yv = torch.where(keep.float() != 0, y.float() * (1.0 / (1.0 - p) if p > 0 else 1.0), torch.zeros_like(y.float()))
+    v = (x if with_x else 0) + yv
+    if with_z:
+        v = v.view(B, L, D).clone()
+        v[:, 0] = zr
+        v = v.view(rows, D)
+    assert torch.equal(xo, v)
+    if with_ln:
+        ref = torch.nn.functional.layer_norm(v, (D,), w, b, 1e-5)
+        assert _rel(h, ref) < 1e-2
+        torch.testing.assert_close(mean, v.mean(-1), rtol=1e-5, atol=1e-5)
+        torch.testing.assert_close(rstd, (v.var(-1, unbiased=False) + 1e-5).rsqrt(), rtol=1e-4, atol=1e-5)
+    else:
+        assert torch.equal(h, v.bfloat16())
