@@ -231,7 +231,7 @@ int svae_ce_grad(void* logits, int64_t ld, const float* lse, const float* chunk_
  * ce_prob_finalize: part f32 [ntile][rows] (the per-tile sums of P) -> lse = c + log sum, row_loss = lse - c,
  *   chunk_w, nll_out: the chunked mean of means of svae_ce_finalize.
  * ce_prob_bwd_prep: r_out, q_out [rows]; hh_out bf16 [rows][D] = r * hh; dbias[label] -= q (atomics; may be NULL).
- * The GEMM caps the exponent at 2^127 (a logit more than 88 nats above the label logit); ce_prob_finalize_fix
+ * The GEMM's exponent overflows to +inf for a logit more than 88 nats above the label logit; ce_prob_finalize_fix
  * finds every labelled row whose sum of P reaches 2^100 (or is not finite), lists it in sat_ws (int32 [1 + rows]:
  * count, then rows; the count stays readable after the call) and recomputes it exactly: the row's logits from hh, W
  * and bias, P[row] = exp(logit - max) (bf16, into P with leading dimension ldp), lse = max + log sum, row_loss =

@@ -60,6 +60,9 @@ struct Tile {
   static constexpr int BYTES = 64 * PITCH;
   __device__ static __forceinline__ int off(int r, int c) { return r * PITCH + ((c ^ (r & (NCH - 1))) << 4); }
   __device__ static __forceinline__ int uoff(int r, int u) { return off(r, u >> 1) + ((u & 1) << 3); }
+  // byte distance between rows r and r + 1 for 4-dim unit u; the swizzle sees row bits below log2(NCH) only, so
+  // uoff(r + 16 k, u) = uoff(r, u) + 16 k row_pitch(u) (k >= 0)
+  __device__ static constexpr int row_pitch(int) { return PITCH; }
 };
 
 // Load rows [row0, row0+64) of a token-major matrix (row stride ld, head column offset folded into g)
@@ -106,6 +109,85 @@ __device__ __forceinline__ void dma_rows(const bf16* g, long long ld, int row0, 
     dma16_lds(rsrc, lds + inst * 1024, ok ? (r * (int)ld + c * 8) * 2 : 0x7FFFFFF0);
   }
 }
+
+// RowImg<HDC>: 64 rows x HDC bf16. Dims 0-63: the Tile<64> image (128-B rows, chunk c ^ (r & 7)). HDC = 96: dims
+// 64-95 follow as [64 rows][4 chunks] (64-B rows) with chunk swizzle c ^ tail_swz(r): rows r, r + 4, r + 8, r + 12
+// share banks, so tail_swz takes 4 distinct values over bits 2-3 of r (the 16-row b128 reads) and differs in bit 1
+// between r and r + 4 and between r and r + 8 (the transposed reads of rows 4g + q and 8g + q): conflict-free.
+template <int HDC>
+struct RowImg {
+  static_assert(HDC == 64 || HDC == 96, "RowImg: 64 or 96 dims");
+  static constexpr int NCH = HDC / 8;               // 16-B chunks per row
+  static constexpr int BYTES = 64 * HDC * 2;        // 8 or 12 KiB
+  static constexpr int PIECES = BYTES / 1024;       // LDS-DMA wave-instructions per image
+  __device__ static __forceinline__ int tail_swz(int r) { return ((((r >> 2) ^ (r >> 3)) & 1) << 1) | ((r >> 2) & 1); }
+  // byte offset of (row r < 64, logical chunk c)
+  __device__ static __forceinline__ int off(int r, int c) {
+    if (HDC == 64 || c < 8) return r * 128 + ((c ^ (r & 7)) << 4);
+    return 8192 + r * 64 + (((c - 8) ^ tail_swz(r)) << 4);
+  }
+  // 8-B unit u (dims 4u .. 4u + 3) of row r
+  __device__ static __forceinline__ int uoff(int r, int u) { return off(r, u >> 1) + ((u & 1) << 3); }
+  // as Tile::row_pitch (the swizzles see row bits 0-3 only)
+  __device__ static constexpr int row_pitch(int u) { return (HDC == 64 || u < 16) ? 128 : 64; }
+  // the LDS slot of lane `lane` in DMA piece i: row r and logical chunk c it receives (swizzle undone)
+  __device__ static __forceinline__ void piece_src(int i, int lane, int& r, int& c) {
+    if (HDC == 64 || i < 8) {
+      r = 8 * i + (lane >> 3);
+      c = (lane & 7) ^ (r & 7);
+    } else {
+      r = 16 * (i - 8) + (lane >> 2);
+      c = ((lane & 3) ^ tail_swz(r)) + 8;
+    }
+  }
+};
+
+// LDS-DMA of piece i of the RowImg of rows [row0, row0 + 64) of a token-major matrix whose row 0 the descriptor
+// addresses (offsets stay below 2^31 bytes: checked by svae_attn_bwd); rows >= nrows and dims >= hd land as zeros
+// (out-of-range source offset)
+template <int HDC>
+__device__ __forceinline__ void dma_img_piece(const u32x4& rsrc, long long ld, int row0, int nrows, int hd, char* img,
+                                              int i, int lane) {
+  int r, c;
+  RowImg<HDC>::piece_src(i, lane, r, c);
+  const bool ok = row0 + r < nrows && c * 8 < hd;
+  dma16_lds(rsrc, img + i * 1024, ok ? ((row0 + r) * (int)ld + c * 8) * 2 : 0x7FFFFFF0);
+}
+
+// The forward's K / V tile layout: RowImg for hd <= 96 (64 or 96 dims per row: hd 96 no longer pays 128-wide rows, so
+// three workgroups fit a CU), Tile<128> for hd 128.
+template <int HDP, int HDC>
+struct FwdTile {
+  using type = Tile<HDP>;
+};
+template <>
+struct FwdTile<64, 64> {
+  using type = RowImg<64>;
+};
+template <>
+struct FwdTile<128, 96> {
+  using type = RowImg<96>;
+};
+// rows [row0, row0 + 64) of a token-major matrix (row 0 at g) into the LDS image; the 4 waves split the pieces
+template <int HDP>
+__device__ __forceinline__ void dma_tile(const Tile<HDP>*, const bf16* g, long long ld, int row0, int nrows, int hd,
+                                         char* lds, int w, int lane) {
+  dma_rows<HDP>(g, ld, row0, nrows, hd, lds, w, lane);
+}
+template <int HDC>
+__device__ __forceinline__ void dma_tile(const RowImg<HDC>*, const bf16* g, long long ld, int row0, int nrows, int hd,
+                                         char* lds, int w, int lane) {
+  constexpr int PW = RowImg<HDC>::PIECES / 4;
+  static_assert(PW * 4 == RowImg<HDC>::PIECES, "pieces split over the 4 waves");
+  const u32x4 rs = buffer_rsrc(g, 0x7FFFFFF0u);
+  const int ln = lane_id_fresh();   // (offsets recomputed here, not kept live across the key loop)
+#pragma unroll
+  for (int i = 0; i < PW; ++i) dma_img_piece<HDC>(rs, ld, row0, nrows, hd, lds, w * PW + i, ln);
+}
+template <int HDP>
+constexpr int tile_pieces(const Tile<HDP>*) { return 64 * Tile<HDP>::PITCH / 1024; }
+template <int HDC>
+constexpr int tile_pieces(const RowImg<HDC>*) { return RowImg<HDC>::PIECES; }
 
 __device__ __forceinline__ bf16x8 pack8(const f32x4& a, const f32x4& b) {
   return (bf16x8){f2bf(a[0]), f2bf(a[1]), f2bf(a[2]), f2bf(a[3]), f2bf(b[0]), f2bf(b[1]), f2bf(b[2]), f2bf(b[3])};
@@ -191,13 +273,13 @@ constexpr int ATTN_NS = 2;   // K/V ring stages (3 stages with the XCD order: 70
 // zero padding).
 template <int HDP, int HDC = HDP>
 __device__ __forceinline__ void attn_fwd_tile(const AP& p, char* smem, int bx, int h, int b) {
-  using T = Tile<HDP>;
+  using T = typename FwdTile<HDP, HDC>::type;
   constexpr int NKK = HDC / 32, NT = HDC / 16;
   // K/V ring: NS stages of (K, V) tiles filled NS - 1 key tiles ahead; the key-padding bytes ride along in an
   // [NS][64] ring. Measured at the C2 shape (hd 64): 2 stages at 3 blocks / CU (33 KB LDS, <= 170 VGPRs) beat
   // 3 or 4 stages at 2 blocks / CU (73.5 vs 78.4 / 92 us): blocks in flight, not prefetch depth, set the time.
   constexpr int NS = ATTN_NS;
-  constexpr int DMA_OPS = 2 * (64 * T::PITCH / 1024) / 4;   // buffer_load_lds per wave per (K, V) tile
+  constexpr int DMA_OPS = 2 * tile_pieces((const T*)nullptr) / 4;   // buffer_load_lds per wave per (K, V) tile
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, li = lane & 15;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: scalar branches, not exec masks
   const int q0 = bx * 128;
@@ -246,8 +328,8 @@ __device__ __forceinline__ void attn_fwd_tile(const AP& p, char* smem, int bx, i
   auto issue = [&](int it2) {
     const int kn = (it2 == 0 ? 0 : kt1 + it2 - 1) * 64;
     char* nb = smem + (it2 % NS) * 2 * T::BYTES;
-    dma_rows<HDP>(K, p.sk, kn, p.Lk, p.hd, nb, w, lane);
-    dma_rows<HDP>(V, p.sv, kn, p.Lk, p.hd, nb + T::BYTES, w, lane);
+    dma_tile((const T*)nullptr, K, p.sk, kn, p.Lk, p.hd, nb, w, lane);
+    dma_tile((const T*)nullptr, V, p.sv, kn, p.Lk, p.hd, nb + T::BYTES, w, lane);
     if (pad && w == 0) dma1_lds(prs, pm + (it2 % NS) * 64, kn + lane < p.Lk ? kn + lane : 0x7FFFFFF0);
   };
   if (!pad && tid < NS * 64) pm[tid] = 0;
@@ -353,11 +435,13 @@ __device__ __forceinline__ void attn_fwd_tile(const AP& p, char* smem, int bx, i
       for (int kk = 0; kk < 2; ++kk) {
         const bf16x8 pf0 = pack8(s[0][2 * kk], s[0][2 * kk + 1]);
         const bf16x8 pf1 = pack8(s[1][2 * kk], s[1][2 * kk + 1]);
-        const int r0 = 32 * kk + 4 * g + (li >> 2);
+        const int rq = 4 * g + (li >> 2);   // row 32 kk + rq: a constant offset from row rq (folded into the ds_read)
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
           const int u = 4 * t + (li & 3);
-          const bf16x8 vf = cat44(lds_read_tr(Vs + T::uoff(r0, u)), lds_read_tr(Vs + T::uoff(r0 + 16, u)));
+          const int pt = T::row_pitch(4 * t);
+          const lds_char* pv = lds_ptr(Vs) + T::uoff(rq, u) + 32 * kk * pt;
+          const bf16x8 vf = cat44(lds_read_tr3(pv), lds_read_tr3(pv + 16 * pt));
           o[0][t] = mfma16(vf, pf0, o[0][t]);
           o[1][t] = mfma16(vf, pf1, o[1][t]);
         }
@@ -398,8 +482,8 @@ __device__ __forceinline__ void attn_fwd_tile(const AP& p, char* smem, int bx, i
 // work, measured 68 -> 73 us at the C2 shape on two boxes out of three, scripts/attn_probe.py: half the workgroups
 // in flight cost more than the imbalance.)
 template <int HDP, int HDC = HDP>
-__global__ __launch_bounds__(256, HDP == 64 ? 3 : 2) void attn_fwd_kernel(AP p) {
-  __shared__ __attribute__((aligned(16))) char smem[ATTN_NS * 2 * Tile<HDP>::BYTES + ATTN_NS * 64 * 4];
+__global__ __launch_bounds__(256, HDC <= 96 ? 3 : 2) void attn_fwd_kernel(AP p) {
+  __shared__ __attribute__((aligned(16))) char smem[ATTN_NS * 2 * FwdTile<HDP, HDC>::type::BYTES + ATTN_NS * 64 * 4];
   int bx, h, b;
   xcd_block(bx, h, b, p.causal ? 1 : 0);
   attn_fwd_tile<HDP, HDC>(p, smem, bx, h, b);
@@ -915,48 +999,6 @@ __device__ __forceinline__ void attn_bwd_tile_wide(const AP& p, char* smem, int 
 // 4-wave kernel needed 128-wide LDS rows and 256-register waves). LDS rows of HDC = 64 or 96 dims (RowImg: 96 = a
 // 64-dim Tile plus a 32-dim tail image), so hd 96 keeps K, dS^T and double-buffered Q / dO in 129 KiB.
 //
-// RowImg<HDC>: 64 rows x HDC bf16. Dims 0-63: the Tile<64> image (128-B rows, chunk c ^ (r & 7)). HDC = 96: dims
-// 64-95 follow as [64 rows][4 chunks] (64-B rows) with chunk swizzle c ^ tail_swz(r): rows r, r + 4, r + 8, r + 12
-// share banks, so tail_swz takes 4 distinct values over bits 2-3 of r (the 16-row b128 reads) and differs in bit 1
-// between r and r + 4 and between r and r + 8 (the transposed reads of rows 4g + q and 8g + q): conflict-free.
-template <int HDC>
-struct RowImg {
-  static_assert(HDC == 64 || HDC == 96, "RowImg: 64 or 96 dims");
-  static constexpr int NCH = HDC / 8;               // 16-B chunks per row
-  static constexpr int BYTES = 64 * HDC * 2;        // 8 or 12 KiB
-  static constexpr int PIECES = BYTES / 1024;       // LDS-DMA wave-instructions per image
-  __device__ static __forceinline__ int tail_swz(int r) { return ((((r >> 2) ^ (r >> 3)) & 1) << 1) | ((r >> 2) & 1); }
-  // byte offset of (row r < 64, logical chunk c)
-  __device__ static __forceinline__ int off(int r, int c) {
-    if (HDC == 64 || c < 8) return r * 128 + ((c ^ (r & 7)) << 4);
-    return 8192 + r * 64 + (((c - 8) ^ tail_swz(r)) << 4);
-  }
-  // 8-B unit u (dims 4u .. 4u + 3) of row r
-  __device__ static __forceinline__ int uoff(int r, int u) { return off(r, u >> 1) + ((u & 1) << 3); }
-  // the LDS slot of lane `lane` in DMA piece i: row r and logical chunk c it receives (swizzle undone)
-  __device__ static __forceinline__ void piece_src(int i, int lane, int& r, int& c) {
-    if (HDC == 64 || i < 8) {
-      r = 8 * i + (lane >> 3);
-      c = (lane & 7) ^ (r & 7);
-    } else {
-      r = 16 * (i - 8) + (lane >> 2);
-      c = ((lane & 3) ^ tail_swz(r)) + 8;
-    }
-  }
-};
-
-// LDS-DMA of piece i of the RowImg of rows [row0, row0 + 64) of a token-major matrix whose row 0 the descriptor
-// addresses (offsets stay below 2^31 bytes: checked by svae_attn_bwd); rows >= nrows and dims >= hd land as zeros
-// (out-of-range source offset)
-template <int HDC>
-__device__ __forceinline__ void dma_img_piece(const u32x4& rsrc, long long ld, int row0, int nrows, int hd, char* img,
-                                              int i, int lane) {
-  int r, c;
-  RowImg<HDC>::piece_src(i, lane, r, c);
-  const bool ok = row0 + r < nrows && c * 8 < hd;
-  dma16_lds(rsrc, img + i * 1024, ok ? ((row0 + r) * (int)ld + c * 8) * 2 : 0x7FFFFFF0);
-}
-
 constexpr int BWD8_KEYS = 256;
 
 template <int HDC>

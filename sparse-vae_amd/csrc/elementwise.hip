@@ -204,8 +204,8 @@ __global__ __launch_bounds__(256) void ce_label_logit_kernel(const bf16* __restr
 // flight), the 8 slice sums combined in LDS in a fixed order. (One thread per row walking all 256 tiles: 512 waves
 // on the chip, 37.6 us at C2.)
 // A labelled row whose sum reaches 2^100 (a logit more than ~69 nats above the label logit, or a non-finite one) is
-// appended to sat[1..] (count in sat[0]) for ce_prob_fixup: the GEMM epilogue caps the exponent at 2^127, so such a
-// row's P and lse are recomputed with the row maximum as the offset instead of being silently clipped.
+// appended to sat[1..] (count in sat[0]) for ce_prob_fixup: the GEMM epilogue's exp2 overflows to +inf past 88 nats, so
+// such a row's P and lse are recomputed with the row maximum as the offset.
 __global__ __launch_bounds__(256) void ce_prob_rows_kernel(const float* __restrict__ part, int ntile,
                                                            const float* __restrict__ off, const int* __restrict__ labels,
                                                            int rows, float* __restrict__ lse, float* __restrict__ row_loss,

@@ -843,7 +843,9 @@ __device__ __forceinline__ void g3_reg_epilogue(const GP& p, const f32x4 (&acc)[
                 const f32x2 a2 = {acc[i][j][e], acc[i][j][e + 1]};
                 const f32x2 c2 = (f32x2){bl4[j][e], bl4[j][e + 1]} + noff;
                 const f32x2 t2 = a2 * sa2 + c2;
-                f32x2 x = {__builtin_amdgcn_exp2f(fminf(t2[0], 127.0f)), __builtin_amdgcn_exp2f(fminf(t2[1], 127.0f))};
+                // (no clamp: a logit more than 88 nats above the label logit gives +inf here, which svae_ce_prob_finalize_fix finds
+                // in the row's sum and recomputes exactly)
+                f32x2 x = {__builtin_amdgcn_exp2f(t2[0]), __builtin_amdgcn_exp2f(t2[1])};
                 if constexpr (decltype(rag)::value) {
                   const int n = n0 + wc * 64 + j * 16 + 4 * g + e;
                   if (n >= p.N) x[0] = 0.f;

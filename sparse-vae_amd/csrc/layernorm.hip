@@ -120,7 +120,9 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, co
 //   xo[r] = v (f32, when xo); h[r] = LN(v) * w + b (bf16) and mean / rstd when w, else h[r] = bf16(v).
 // Moves 14 B per element with an f32 y (x, y in; xo, h out): the residual add and the dropout leave the GEMM epilogue (which ran with
 // no MFMA beside it: the f32 + residual epilogue cost 2x a bf16 store at the C2 FFN2 shape) for this HBM-bound pass.
-template <int NR, typename TY>
+// CPL = columns per lane per run (8: one 16-B bf16 store per run, D % 512 == 0 fills every lane; 4: D = 768 as 3 runs of
+// 256 columns, every lane busy -- the 8-column layout left half the lanes idle in its second run), NR runs.
+template <int NR, int CPL, typename TY>
 __global__ __launch_bounds__(256) void resid_ln_fwd_kernel(const float* __restrict__ x, const TY* __restrict__ y,
                                                            long long ldy, float drop_p, unsigned long long seed,
                                                            const float* __restrict__ zrows, int zmod,
@@ -128,72 +130,88 @@ __global__ __launch_bounds__(256) void resid_ln_fwd_kernel(const float* __restri
                                                            float* __restrict__ xo, bf16* __restrict__ h,
                                                            float* __restrict__ mean_out, float* __restrict__ rstd_out,
                                                            int rows, int D) {
+  constexpr int NV = CPL / 4;                    // f32x4 per run
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
   const bool zr = zrows && row % zmod == 0;      // wave-uniform
   const float sc = drop_p > 0.f ? 1.0f / (1.0f - drop_p) : 1.0f;
-  f32x4 v[NR][2];
+  f32x4 v[NR][NV];
   float s = 0.f;
 #pragma unroll
   for (int j = 0; j < NR; ++j) {
-    const int c = (lane + 64 * j) * 8;
-    const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
-    v[j][0] = z4;
-    v[j][1] = z4;
+    const int c = (lane + 64 * j) * CPL;
+#pragma unroll
+    for (int q = 0; q < NV; ++q) v[j][q] = (f32x4){0.f, 0.f, 0.f, 0.f};
     if (c < D) {
       if (zr) {
         const float* zp = zrows + (long long)(row / zmod) * D + c;
-        v[j][0] = *(const f32x4*)zp;
-        v[j][1] = *(const f32x4*)(zp + 4);
+#pragma unroll
+        for (int q = 0; q < NV; ++q) v[j][q] = *(const f32x4*)(zp + 4 * q);
       } else {
         if (x) {
-          v[j][0] = *(const f32x4*)(x + (long long)row * D + c);
-          v[j][1] = *(const f32x4*)(x + (long long)row * D + c + 4);
+#pragma unroll
+          for (int q = 0; q < NV; ++q) v[j][q] = *(const f32x4*)(x + (long long)row * D + c + 4 * q);
         }
         if (y) {
-          float yy[8];
+          float yy[CPL];
           if constexpr (sizeof(TY) == 2) {
-            const bf16x8 t = *(const bf16x8*)(y + (long long)row * ldy + c);
+            if constexpr (CPL == 8) {
+              const bf16x8 t = *(const bf16x8*)(y + (long long)row * ldy + c);
 #pragma unroll
-            for (int e = 0; e < 8; ++e) yy[e] = (float)t[e];
+              for (int e = 0; e < 8; ++e) yy[e] = (float)t[e];
+            } else {
+              const bf16x4 t = *(const bf16x4*)(y + (long long)row * ldy + c);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) yy[e] = (float)t[e];
+            }
           } else {
-            const f32x4 t0 = *(const f32x4*)(y + (long long)row * ldy + c), t1 = *(const f32x4*)(y + (long long)row * ldy + c + 4);
 #pragma unroll
-            for (int e = 0; e < 4; ++e) { yy[e] = t0[e]; yy[4 + e] = t1[e]; }
-          }
-          float u[8] = {1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f};
-          if (drop_p > 0.f) {
-            float u0[4], u1[4];
-            rand_uniform4(seed, ((unsigned long long)row * D + c) >> 2, u0);
-            rand_uniform4(seed, ((unsigned long long)row * D + c + 4) >> 2, u1);
+            for (int q = 0; q < NV; ++q) {
+              const f32x4 t = *(const f32x4*)(y + (long long)row * ldy + c + 4 * q);
 #pragma unroll
-            for (int e = 0; e < 4; ++e) { u[e] = u0[e]; u[4 + e] = u1[e]; }
+              for (int e = 0; e < 4; ++e) yy[4 * q + e] = t[e];
+            }
           }
 #pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float t = yy[e];
-            const float d = drop_p > 0.f ? (u[e] >= drop_p ? t * sc : 0.f) : t;
-            v[j][e >> 2][e & 3] += d;
+          for (int q = 0; q < NV; ++q) {
+            float u[4] = {1.f, 1.f, 1.f, 1.f};
+            if (drop_p > 0.f) rand_uniform4(seed, ((unsigned long long)row * D + c + 4 * q) >> 2, u);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float t = yy[4 * q + e];
+              v[j][q][e] += drop_p > 0.f ? (u[e] >= drop_p ? t * sc : 0.f) : t;
+            }
           }
         }
       }
-      s += (v[j][0][0] + v[j][0][1]) + (v[j][0][2] + v[j][0][3]) + (v[j][1][0] + v[j][1][1]) + (v[j][1][2] + v[j][1][3]);
+#pragma unroll
+      for (int q = 0; q < NV; ++q) s += (v[j][q][0] + v[j][q][1]) + (v[j][q][2] + v[j][q][3]);
       if (xo) {
-        *(f32x4*)(xo + (long long)row * D + c) = v[j][0];
-        *(f32x4*)(xo + (long long)row * D + c + 4) = v[j][1];
+#pragma unroll
+        for (int q = 0; q < NV; ++q) *(f32x4*)(xo + (long long)row * D + c + 4 * q) = v[j][q];
       }
     }
   }
+  auto store_h = [&](int c, const float (&o)[CPL]) {
+    if constexpr (CPL == 8) {
+      bf16x8 t;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) t[e] = f2bf(o[e]);
+      *(bf16x8*)(h + (long long)row * D + c) = t;
+    } else {
+      *(bf16x4*)(h + (long long)row * D + c) = (bf16x4){f2bf(o[0]), f2bf(o[1]), f2bf(o[2]), f2bf(o[3])};
+    }
+  };
   if (!w) {                                      // no LayerNorm: the bf16 copy of v
 #pragma unroll
     for (int j = 0; j < NR; ++j) {
-      const int c = (lane + 64 * j) * 8;
+      const int c = (lane + 64 * j) * CPL;
       if (c < D) {
-        bf16x8 o;
+        float o[CPL];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] = f2bf(v[j][e >> 2][e & 3]);
-        *(bf16x8*)(h + (long long)row * D + c) = o;
+        for (int e = 0; e < CPL; ++e) o[e] = v[j][e >> 2][e & 3];
+        store_h(c, o);
       }
     }
     return;
@@ -202,27 +220,25 @@ __global__ __launch_bounds__(256) void resid_ln_fwd_kernel(const float* __restri
   float sq = 0.f;
 #pragma unroll
   for (int j = 0; j < NR; ++j) {
-    const int c = (lane + 64 * j) * 8;
+    const int c = (lane + 64 * j) * CPL;
     if (c < D) {
 #pragma unroll
-      for (int hh = 0; hh < 2; ++hh)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) { const float t = v[j][hh][e] - mean; sq += t * t; }
+      for (int e = 0; e < CPL; ++e) { const float t = v[j][e >> 2][e & 3] - mean; sq += t * t; }
     }
   }
   const float rstd = rsqrtf(wave_sum(sq) / D + 1e-5f);
 #pragma unroll
   for (int j = 0; j < NR; ++j) {
-    const int c = (lane + 64 * j) * 8;
+    const int c = (lane + 64 * j) * CPL;
     if (c < D) {
-      bf16x8 o;
+      float o[CPL];
 #pragma unroll
-      for (int hh = 0; hh < 2; ++hh) {
-        const f32x4 ww = *(const f32x4*)(w + c + 4 * hh), bb = *(const f32x4*)(b + c + 4 * hh);
+      for (int q = 0; q < NV; ++q) {
+        const f32x4 ww = *(const f32x4*)(w + c + 4 * q), bb = *(const f32x4*)(b + c + 4 * q);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) o[4 * hh + e] = f2bf((v[j][hh][e] - mean) * rstd * ww[e] + bb[e]);
+        for (int e = 0; e < 4; ++e) o[4 * q + e] = (v[j][q][e] - mean) * rstd * ww[e] + bb[e];
       }
-      *(bf16x8*)(h + (long long)row * D + c) = o;
+      store_h(c, o);
     }
   }
   if (lane == 0) { mean_out[row] = mean; rstd_out[row] = rstd; }
@@ -388,13 +404,15 @@ SVAE_EXPORT int svae_resid_ln_fwd(const float* x, const void* y, int32_t y_dtype
   if (drop_p < 0.f || drop_p >= 1.f || (y && ldy % 8) || (((uintptr_t)y | (uintptr_t)h) & 15)) return SVAE_EINVAL;
   dim3 grid((rows + 3) / 4);
   hipStream_t s = (hipStream_t)stream;
-#define SVAE_RLN(NR, TY)                                                                                          \
-  hipLaunchKernelGGL((resid_ln_fwd_kernel<NR, TY>), grid, dim3(256), 0, s, x, (const TY*)y, (long long)ldy, drop_p, \
-                     (unsigned long long)seed, zrows, zmod, w, b, xo, (bf16*)h, mean, rstd, rows, D)
+#define SVAE_RLN(NR, CPL, TY)                                                                                     \
+  hipLaunchKernelGGL((resid_ln_fwd_kernel<NR, CPL, TY>), grid, dim3(256), 0, s, x, (const TY*)y, (long long)ldy,     \
+                     drop_p, (unsigned long long)seed, zrows, zmod, w, b, xo, (bf16*)h, mean, rstd, rows, D)
   if (D <= 512) {
-    if (y_dtype == 0) SVAE_RLN(1, float); else SVAE_RLN(1, bf16);
+    if (y_dtype == 0) SVAE_RLN(1, 8, float); else SVAE_RLN(1, 8, bf16);
+  } else if (D <= 768) {
+    if (y_dtype == 0) SVAE_RLN(3, 4, float); else SVAE_RLN(3, 4, bf16);
   } else {
-    if (y_dtype == 0) SVAE_RLN(2, float); else SVAE_RLN(2, bf16);
+    if (y_dtype == 0) SVAE_RLN(2, 8, float); else SVAE_RLN(2, 8, bf16);
   }
 #undef SVAE_RLN
   SVAE_LAUNCH_CHECK();

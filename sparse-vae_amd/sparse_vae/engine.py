@@ -238,9 +238,11 @@ class VAEEngine:
         # the two dW GEMMs of the FFN, and the attention output projection's with the Q/K/V projection's, run as one
         # paired launch each (kernels.linear_dw_pair); SVAE_DW_PAIR=0 launches them one by one (A/B runs)
         self.dw_pair = os.environ.get('SVAE_DW_PAIR', '1') != '0'
-        # decoder residual adds in the fused residual + dropout + LayerNorm pass (layer_fwd's fuse); SVAE_FUSE_LN=0: the
-        # projections' f32 residual epilogues and separate LayerNorms (A/B runs)
-        self.fuse_ln = os.environ.get('SVAE_FUSE_LN', '1') != '0'
+        # decoder residual adds in a separate fused residual + dropout + LayerNorm pass (layer_fwd's fuse, SVAE_FUSE_LN=1)
+        # instead of the projections' f32 residual epilogues + LayerNorm passes. Off by default: measured at C2 it moves
+        # 36 B per element and layer against 28 (the projection output makes an f32 round trip), +0.125 ms of kernel
+        # time per step (profiles/r03f_*); at C4 +0.5-0.8 ms/step
+        self.fuse_ln = os.environ.get('SVAE_FUSE_LN', '0') != '0'
         self.side = None
         if flat.device.type == 'cuda' and os.environ.get('SVAE_DW_STREAM', '0') != '0':
             self.side = torch.cuda.Stream(device=flat.device)

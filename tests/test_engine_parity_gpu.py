@@ -52,10 +52,13 @@ def _grad_bars(worst, msg):
         assert abs(r - 1.0) < tol, f'{n}: norm ratio {r:.4f}\n' + msg
 
 
-@pytest.mark.parametrize('name,chunk_numel', [('tiny_pad', None), ('small6_pad', None), ('hd96', None),
-                                              ('c2shape', None), ('c4shape', None), ('c5shape', None),
-                                              ('c4shape', 2 ** 25), ('c4shape', 23_000_000)])
-def test_step_matches_oracle(name, chunk_numel, monkeypatch):
+@pytest.mark.parametrize('name,chunk_numel,fuse_ln', [('tiny_pad', None, False), ('small6_pad', None, False),
+                                                      ('hd96', None, False), ('c2shape', None, False),
+                                                      ('c4shape', None, False), ('c5shape', None, False),
+                                                      ('c4shape', 2 ** 25, False), ('c4shape', 23_000_000, False),
+                                                      ('small6_pad', None, True), ('c2shape', None, True),
+                                                      ('c5shape', None, True)])
+def test_step_matches_oracle(name, chunk_numel, fuse_ln, monkeypatch):
     """chunk_numel lowers robust_cross_entropy's 2**30 threshold (language_model.py:163) on both sides, so the full
     engine runs the chunked mean of means (c4shape: 2 chunks of 512 / 511 positions, and 3 of 341, the padded
     sequence's tail inside the last chunk) through ce_prob_finalize's chunk weights, the [CLS] / label-0 rows and
@@ -76,6 +79,7 @@ def test_step_matches_oracle(name, chunk_numel, monkeypatch):
         assert K.ce_chunking(B, L, hp.vocab_size, chunk_numel)[0] > 1
 
     flat, eng = _build(hp, params)
+    eng.fuse_ln = fuse_ln          # the decoder's separate fused residual + dropout + LayerNorm pass (SVAE_FUSE_LN)
     out = eng.forward(ids.cuda(), ntok.cuda(), eps=eps.cuda(), dropout=0.0, kl_weight=kw)
     flat.grad.zero_()
     eng.backward(torch.ones((), device='cuda'), kw)
@@ -97,7 +101,7 @@ def test_step_matches_oracle(name, chunk_numel, monkeypatch):
 
     worst = _grad_report(flat, p)
     msg = '\n'.join(f'{c:.5f} {r:.4f} {n}' for c, r, n in worst[:8])
-    print(f'[{name} {chunk_numel}] loss {loss:.6f} ref {ref["loss"].item():.6f} kl {kl:.6f} ref {ref["kl"].item():.6f}\n' + msg)
+    print(f'[{name} {chunk_numel} fuse_ln={fuse_ln}] loss {loss:.6f} ref {ref["loss"].item():.6f} kl {kl:.6f} ref {ref["kl"].item():.6f}\n' + msg)
     _grad_bars(worst, msg)
 
 
