@@ -733,6 +733,43 @@ __device__ __forceinline__ void store_pair_bf16(bf16* row_base, int colbase, int
   } else if (c < ncols_left) *(u32x2*)(row_base + c) = (u32x2){w[0], w[1]};
 }
 
+// Whole-line bf16 stores of one 16-row fragment row group straight from registers. After the permlane16 swap
+// (store_pair_bf16) lane (g, li) holds 8 consecutive columns of row li for each 32-column half jp: w0 (chunk cg) and
+// w1 (chunk cg + 4) of the wave's 64 columns, so a store instruction would cover 16 rows x 64 B (half lines). A DPP
+// row rotation by 8 swaps w1 between lanes li and li +- 8 (the bank mask keeps w0 in the other half): instruction
+// 0 then writes rows 0-7 and instruction 1 rows 8-15, each 8 whole 128-B lines. No LDS, 12 VALU per row group.
+// Nontemporal (NT) for the tensors read back only much later or by one streaming pass: the P-head's P (2 GiB at C2:
+// head forward 1225 -> 1185 us; whole lines cached 1246, half lines nontemporal wrote 3.0 GB instead of 2.15) and the
+// FFN's GELU' (its FFN-output GEMM, which reads the GELU output next, 110 -> 93 us: the MALL keeps the GELU output).
+template <bool NT>
+__device__ __forceinline__ void store_rows_bf16(bf16* C, long long ldc, int mrow0, int M, int ncol0, int N,
+                                                const f32x4 (&x)[4], int g, int li) {
+  u32x4 w[2];
+#pragma unroll
+  for (int jp = 0; jp < 2; ++jp) {
+    const f32x4 a = x[2 * jp], b = x[2 * jp + 1];
+    const auto s0 = __builtin_amdgcn_permlane16_swap(pack_bf16x2(a[0], a[1]), pack_bf16x2(b[0], b[1]), false, false);
+    const auto s1 = __builtin_amdgcn_permlane16_swap(pack_bf16x2(a[2], a[3]), pack_bf16x2(b[2], b[3]), false, false);
+    w[jp] = (u32x4){s0[0], s1[0], s0[1], s1[1]};
+  }
+  u32x4 h[2];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {   // row_ror:8 (dpp_ctrl 0x128); bank mask 0xC: lanes 8-15 of a row, 0x3: lanes 0-7
+    h[0][d] = __builtin_amdgcn_update_dpp(w[0][d], w[1][d], 0x128, 0xF, 0xC, false);
+    h[1][d] = __builtin_amdgcn_update_dpp(w[0][d], w[1][d], 0x128, 0xF, 0x3, false);
+  }
+  const int cg = ((g & 1) ? 2 : 0) + ((g & 2) ? 1 : 0), hi = li >> 3;
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh) {
+    const int m = mrow0 + 8 * hh + (li & 7), c = cg + 4 * (hi ^ hh), nleft = N - ncol0 - 8 * c;
+    bf16* dst = C + (long long)(m < M ? m : 0) * ldc + ncol0 + 8 * c;
+    if (m < M && nleft >= 8) {
+      if constexpr (NT) __builtin_nontemporal_store(h[hh], (u32x4*)dst);
+      else *(u32x4*)dst = h[hh];
+    } else if (m < M && nleft > 0) *(u32x2*)dst = (u32x2){h[hh][0], h[hh][1]};
+  }
+}
+
 template <bool B>
 struct BoolC {
   static constexpr bool value = B;
@@ -799,10 +836,7 @@ __device__ __forceinline__ void g3_reg_epilogue(const GP& p, const f32x4 (&acc)[
       }
     }
     {
-      // (the permlane swaps need every lane: the bounds are applied to the stores only)
-      const bool row_ok = m < p.M;
-      const int nleft = p.N - (n0 + wc * 64);
-      bf16* crow = (bf16*)p.C + cofs + (long long)(row_ok ? m : 0) * p.ldc + n0 + wc * 64;
+      // (the permlane swaps and DPP moves need every lane: the bounds are applied to the stores only)
       if constexpr (EPI == SVAE_EPI_GELU) {
         f32x4 gg[4], dg[4];
 #pragma unroll
@@ -816,12 +850,9 @@ __device__ __forceinline__ void g3_reg_epilogue(const GP& p, const f32x4 (&acc)[
             dg[j][e] = de[0];
             dg[j][e + 1] = de[1];
           }
-        bf16* arow = (bf16*)p.aux + (long long)(row_ok ? m : 0) * p.ldaux + n0 + wc * 64;
-#pragma unroll
-        for (int jp = 0; jp < 2; ++jp) {
-          store_pair_bf16(crow, 32 * jp, row_ok ? nleft : 0, gg[2 * jp], gg[2 * jp + 1], g);
-          store_pair_bf16(arow, 32 * jp, row_ok ? nleft : 0, dg[2 * jp], dg[2 * jp + 1], g);
-        }
+        store_rows_bf16<false>((bf16*)p.C + cofs, p.ldc, m0 + wr * 128 + i * 16, p.M, n0 + wc * 64, p.N, gg, g, li);
+        // GELU' (read only by the FFN backward): nontemporal
+        store_rows_bf16<true>((bf16*)p.aux, p.ldaux, m0 + wr * 128 + i * 16, p.M, n0 + wc * 64, p.N, dg, g, li);
       } else if constexpr (EPI == SVAE_EPI_CE_PROB) {
         // p = exp(logit - c_row) for rows with a target (0 elsewhere); the f32 values feed the per-tile sums below
         // exponent in packed f32 pairs: x = acc (alpha log2e) + (bias log2e - off), one v_pk_fma_f32 per two logits
@@ -832,14 +863,11 @@ __device__ __forceinline__ void g3_reg_epilogue(const GP& p, const f32x4 (&acc)[
         // the column bound is checked per element only on a wave whose 64 columns cross N (a scalar branch between
         // two copies: if-converted into the one loop it cost 4 VALU per element, as much as the exp's arithmetic)
         auto body = [&](auto rag) {
+          f32x4 xs[4];
 #pragma unroll
-          for (int jp = 0; jp < 2; ++jp) {   // P [T, V] bf16 (2 GiB at C2)
-            f32x4 x2[2];
-#pragma unroll
-            for (int h = 0; h < 2; ++h)
+          for (int j = 0; j < 4; ++j)
 #pragma unroll
               for (int e = 0; e < 4; e += 2) {
-                const int j = 2 * jp + h;
                 const f32x2 a2 = {acc[i][j][e], acc[i][j][e + 1]};
                 const f32x2 c2 = (f32x2){bl4[j][e], bl4[j][e + 1]} + noff;
                 const f32x2 t2 = a2 * sa2 + c2;
@@ -851,21 +879,21 @@ __device__ __forceinline__ void g3_reg_epilogue(const GP& p, const f32x4 (&acc)[
                   if (n >= p.N) x[0] = 0.f;
                   if (n + 1 >= p.N) x[1] = 0.f;
                 }
-                x2[h][e] = x[0];
-                x2[h][e + 1] = x[1];
+                xs[j][e] = x[0];
+                xs[j][e + 1] = x[1];
                 se2 += x;
               }
-            store_pair_bf16(crow, 32 * jp, row_ok ? nleft : 0, x2[0], x2[1], g);   // cached stores
-          }
+          // P [T, V] bf16 (2 GiB at C2): whole lines, nontemporal
+          store_rows_bf16<true>((bf16*)p.C + cofs, p.ldc, m0 + wr * 128 + i * 16, p.M, n0 + wc * 64, p.N, xs, g, li);
         };
         if (__builtin_amdgcn_readfirstlane((int)(n0 + wc * 64 + 64 > p.N))) body(BoolC<true>{});
         else body(BoolC<false>{});
         float se = sum_x16_x32(se2[0] + se2[1]);
         if (g == 0) sstat[rl * 4 + wc] = se;
       } else if (EPI != SVAE_EPI_CE_STATS || p.C) {   // CE statistics with C == nullptr: no logits stored
-#pragma unroll
-        for (int jp = 0; jp < 2; ++jp)   // vocab logits (2 GiB at C2): nontemporal, 1444 -> 1322 us
-          store_pair_bf16<EPI == SVAE_EPI_CE_STATS>(crow, 32 * jp, row_ok ? nleft : 0, v[2 * jp], v[2 * jp + 1], g);
+        // (vocab logits of the statistics head, 2 GiB at C2: nontemporal)
+        store_rows_bf16<EPI == SVAE_EPI_CE_STATS>((bf16*)p.C + cofs, p.ldc, m0 + wr * 128 + i * 16, p.M, n0 + wc * 64,
+                                                  p.N, v, g, li);
       }
     }
     if constexpr (EPI == SVAE_EPI_CE_STATS) {
