@@ -454,6 +454,32 @@ __device__ __forceinline__ void attn_fwd_tile(const AP& p, char* smem, int bx, i
   ATTN_STAMP(4, (unsigned long long)nvisit);
   ATTN_STAMP(5, (unsigned long long)bx);
 #endif
+  if ((HDC == 64 || HDC == 96) && p.hd == HDC) {
+    // whole-line stores (common.h): O's first 64 dims as 8 rows x 128 B per instruction (hd 96: the last 32 dims as
+    // before), its f32 copy nontemporal (read only by the backward's delta pass): 55 -> 51 us at the C2 decoder shape
+    constexpr int NP = HDC / 32;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const float lsum = sum_x16_x32(ls[j]);
+      const float inv = lsum > 0.f ? 1.0f / lsum : 0.f;
+      f32x4 v[2 * NP];
+#pragma unroll
+      for (int t = 0; t < 2 * NP; ++t) v[t] = o[j][t < NT ? t : 0] * inv;
+      bf16* O = p.o + b * p.bo + (long long)h * HDC;
+      store_rows_bf16<false>(O, p.so, qw + 16 * j, p.Lq, 0, 64, *(const f32x4(*)[4])v, g, li);
+      const int qrow = qw + 16 * j + li;
+      if (HDC == 96 && qrow < p.Lq) {
+#pragma unroll
+        for (int t = 4; t < 2 * NP; ++t) {
+          const int d = 16 * t + 4 * g;
+          *(bf16x4*)(O + (long long)qrow * p.so + d) = (bf16x4){f2bf(v[t][0]), f2bf(v[t][1]), f2bf(v[t][2]), f2bf(v[t][3])};
+        }
+      }
+      if (p.o32)
+        store_rows_f32<true, NP>(p.o32 + b * p.bo32 + (long long)h * HDC, p.so32, qw + 16 * j, p.Lq, 0, HDC, v, g, li);
+      if (g == 0 && qrow < p.Lq) p.lse[((long long)b * p.H + h) * p.Lq + qrow] = m[j] * p.scale + __logf(lsum);
+    }
+  } else {
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const float lsum = sum_x16_x32(ls[j]);
@@ -472,6 +498,7 @@ __device__ __forceinline__ void attn_fwd_tile(const AP& p, char* smem, int bx, i
       }
       if (g == 0) p.lse[((long long)b * p.H + h) * p.Lq + qrow] = m[j] * p.scale + __logf(lsum);
     }
+  }
   }
 #ifdef SVAE_STAMPS
   ATTN_STAMP(3, __builtin_amdgcn_s_memtime());

@@ -186,7 +186,6 @@ __device__ __forceinline__ void rand_uniform4(uint64_t seed, uint64_t q, float (
   u[3] = ((hi >> 16) + 0.5f) * s;
 }
 
-}  // namespace svae
 
 // Status codes returned by every C-ABI entry point.
 #define SVAE_OK 0
@@ -198,3 +197,82 @@ __device__ __forceinline__ void rand_uniform4(uint64_t seed, uint64_t q, float (
     hipError_t _e = hipGetLastError();                       \
     if (_e != hipSuccess) return SVAE_ELAUNCH;               \
   } while (0)
+
+__device__ __forceinline__ unsigned pack_bf16x2(float a, float b) {
+  typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(unsigned, (bf16x2v){f2bf(a), f2bf(b)});
+}
+
+// Whole-line bf16 stores of one 16-row fragment row group straight from registers. After the permlane16 swap
+// (gemm.hip's store_pair_bf16) lane (g, li) holds 8 consecutive columns of row li for each 32-column half jp: w0 (chunk cg) and
+// w1 (chunk cg + 4) of the wave's 64 columns, so a store instruction would cover 16 rows x 64 B (half lines). A DPP
+// row rotation by 8 swaps w1 between lanes li and li +- 8 (the bank mask keeps w0 in the other half): instruction
+// 0 then writes rows 0-7 and instruction 1 rows 8-15, each 8 whole 128-B lines. No LDS, 12 VALU per row group.
+// Nontemporal (NT) for the tensors read back only much later or by one streaming pass: the P-head's P (2 GiB at C2:
+// head forward 1225 -> 1185 us; whole lines cached 1246, half lines nontemporal wrote 3.0 GB instead of 2.15) and the
+// FFN's GELU' (its FFN-output GEMM, which reads the GELU output next, 110 -> 93 us: the MALL keeps the GELU output).
+// The DPP merge of two 8-column chunks per lane (w[0]: chunk cg, w[1]: chunk cg + 4 of row li) and the two stores.
+template <bool NT>
+__device__ __forceinline__ void store_rows_w16(bf16* C, long long ldc, int mrow0, int M, int ncol0, int N,
+                                               const u32x4 (&w)[2], int g, int li) {
+  u32x4 h[2];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {   // row_ror:8 (dpp_ctrl 0x128); bank mask 0xC: lanes 8-15 of a row, 0x3: lanes 0-7
+    h[0][d] = __builtin_amdgcn_update_dpp(w[0][d], w[1][d], 0x128, 0xF, 0xC, false);
+    h[1][d] = __builtin_amdgcn_update_dpp(w[0][d], w[1][d], 0x128, 0xF, 0x3, false);
+  }
+  const int cg = ((g & 1) ? 2 : 0) + ((g & 2) ? 1 : 0), hi = li >> 3;
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh) {
+    const int m = mrow0 + 8 * hh + (li & 7), c = cg + 4 * (hi ^ hh), nleft = N - ncol0 - 8 * c;
+    bf16* dst = C + (long long)(m < M ? m : 0) * ldc + ncol0 + 8 * c;
+    if (m < M && nleft >= 8) {
+      if constexpr (NT) __builtin_nontemporal_store(h[hh], (u32x4*)dst);
+      else *(u32x4*)dst = h[hh];
+    } else if (m < M && nleft > 0) *(u32x2*)dst = (u32x2){h[hh][0], h[hh][1]};
+  }
+}
+
+template <bool NT>
+__device__ __forceinline__ void store_rows_bf16(bf16* C, long long ldc, int mrow0, int M, int ncol0, int N,
+                                                const f32x4 (&x)[4], int g, int li) {
+  u32x4 w[2];
+#pragma unroll
+  for (int jp = 0; jp < 2; ++jp) {
+    const f32x4 a = x[2 * jp], b = x[2 * jp + 1];
+    const auto s0 = __builtin_amdgcn_permlane16_swap(pack_bf16x2(a[0], a[1]), pack_bf16x2(b[0], b[1]), false, false);
+    const auto s1 = __builtin_amdgcn_permlane16_swap(pack_bf16x2(a[2], a[3]), pack_bf16x2(b[2], b[3]), false, false);
+    w[jp] = (u32x4){s0[0], s1[0], s0[1], s1[1]};
+  }
+  store_rows_w16<NT>(C, ldc, mrow0, M, ncol0, N, w, g, li);
+}
+
+// f32 rows: lane (g, li) holds columns 16 j + 4 g .. + 3 of row li; fragments j = 2 jp, 2 jp + 1 are the two halves
+// of the 128-B line at columns 32 jp .. 32 jp + 31, merged the same way (chunk g and g + 4). N % 4 == 0. NPAIR
+// fragment pairs (64 columns: 2; an hd-96 attention row: 3).
+template <bool NT = false, int NPAIR = 2>
+__device__ __forceinline__ void store_rows_f32(float* C, long long ldc, int mrow0, int M, int ncol0, int N,
+                                               const f32x4 (&x)[2 * NPAIR], int g, int li) {
+  const int hi = li >> 3;
+#pragma unroll
+  for (int jp = 0; jp < NPAIR; ++jp) {
+    f32x4 h[2];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      h[0][d] = __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(x[2 * jp][d]), __float_as_int(x[2 * jp + 1][d]),
+                                                           0x128, 0xF, 0xC, false));
+      h[1][d] = __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(x[2 * jp][d]), __float_as_int(x[2 * jp + 1][d]),
+                                                           0x128, 0xF, 0x3, false));
+    }
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      const int m = mrow0 + 8 * hh + (li & 7), n = ncol0 + 32 * jp + 4 * (g + 4 * (hi ^ hh));
+      if (m < M && n < N) {
+        if constexpr (NT) __builtin_nontemporal_store(h[hh], (f32x4*)(C + (long long)m * ldc + n));
+        else *(f32x4*)(C + (long long)m * ldc + n) = h[hh];
+      }
+    }
+  }
+}
+
+}  // namespace svae

@@ -710,10 +710,6 @@ __device__ __forceinline__ void g3_epilogue(const GP& p, char* smem, const f32x4
 // by the lane holding it.
 constexpr float G3_LOG2E = 1.4426950408889634f;
 
-__device__ __forceinline__ unsigned pack_bf16x2(float a, float b) {
-  typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
-  return __builtin_bit_cast(unsigned, (bf16x2v){f2bf(a), f2bf(b)});
-}
 
 // Store the bf16 of two fragments' column groups x (cols 16ja + 4g..) and y (cols 16ja + 16 + 4g..) of one row
 // as 16-B vectors: a permlane16 swap gives lane group g 8 consecutive columns (g0: 0-7, g2: 8-15, g1: 16-23,
@@ -731,43 +727,6 @@ __device__ __forceinline__ void store_pair_bf16(bf16* row_base, int colbase, int
     if constexpr (NT) __builtin_nontemporal_store(w, (u32x4*)(row_base + c));
     else *(u32x4*)(row_base + c) = w;
   } else if (c < ncols_left) *(u32x2*)(row_base + c) = (u32x2){w[0], w[1]};
-}
-
-// Whole-line bf16 stores of one 16-row fragment row group straight from registers. After the permlane16 swap
-// (store_pair_bf16) lane (g, li) holds 8 consecutive columns of row li for each 32-column half jp: w0 (chunk cg) and
-// w1 (chunk cg + 4) of the wave's 64 columns, so a store instruction would cover 16 rows x 64 B (half lines). A DPP
-// row rotation by 8 swaps w1 between lanes li and li +- 8 (the bank mask keeps w0 in the other half): instruction
-// 0 then writes rows 0-7 and instruction 1 rows 8-15, each 8 whole 128-B lines. No LDS, 12 VALU per row group.
-// Nontemporal (NT) for the tensors read back only much later or by one streaming pass: the P-head's P (2 GiB at C2:
-// head forward 1225 -> 1185 us; whole lines cached 1246, half lines nontemporal wrote 3.0 GB instead of 2.15) and the
-// FFN's GELU' (its FFN-output GEMM, which reads the GELU output next, 110 -> 93 us: the MALL keeps the GELU output).
-template <bool NT>
-__device__ __forceinline__ void store_rows_bf16(bf16* C, long long ldc, int mrow0, int M, int ncol0, int N,
-                                                const f32x4 (&x)[4], int g, int li) {
-  u32x4 w[2];
-#pragma unroll
-  for (int jp = 0; jp < 2; ++jp) {
-    const f32x4 a = x[2 * jp], b = x[2 * jp + 1];
-    const auto s0 = __builtin_amdgcn_permlane16_swap(pack_bf16x2(a[0], a[1]), pack_bf16x2(b[0], b[1]), false, false);
-    const auto s1 = __builtin_amdgcn_permlane16_swap(pack_bf16x2(a[2], a[3]), pack_bf16x2(b[2], b[3]), false, false);
-    w[jp] = (u32x4){s0[0], s1[0], s0[1], s1[1]};
-  }
-  u32x4 h[2];
-#pragma unroll
-  for (int d = 0; d < 4; ++d) {   // row_ror:8 (dpp_ctrl 0x128); bank mask 0xC: lanes 8-15 of a row, 0x3: lanes 0-7
-    h[0][d] = __builtin_amdgcn_update_dpp(w[0][d], w[1][d], 0x128, 0xF, 0xC, false);
-    h[1][d] = __builtin_amdgcn_update_dpp(w[0][d], w[1][d], 0x128, 0xF, 0x3, false);
-  }
-  const int cg = ((g & 1) ? 2 : 0) + ((g & 2) ? 1 : 0), hi = li >> 3;
-#pragma unroll
-  for (int hh = 0; hh < 2; ++hh) {
-    const int m = mrow0 + 8 * hh + (li & 7), c = cg + 4 * (hi ^ hh), nleft = N - ncol0 - 8 * c;
-    bf16* dst = C + (long long)(m < M ? m : 0) * ldc + ncol0 + 8 * c;
-    if (m < M && nleft >= 8) {
-      if constexpr (NT) __builtin_nontemporal_store(h[hh], (u32x4*)dst);
-      else *(u32x4*)dst = h[hh];
-    } else if (m < M && nleft > 0) *(u32x2*)dst = (u32x2){h[hh][0], h[hh][1]};
-  }
 }
 
 template <bool B>
@@ -997,6 +956,7 @@ __device__ __forceinline__ void g3_rowscale_gather_epilogue(const GP& p, const f
                        pack_bf16x2(ra * w[2] - rb * (float)gv[2], ra * w[3] - rb * (float)gv[3]),
                        pack_bf16x2(ra * w[4] - rb * (float)gv[4], ra * w[5] - rb * (float)gv[5]),
                        pack_bf16x2(ra * w[6] - rb * (float)gv[6], ra * w[7] - rb * (float)gv[7])};
+      // (half lines: the whole-line merge cost the head dX a spill and ~8 us)
       const int n = nb + 32 * jp + cs;
       if (m < p.M && n + 8 <= p.N) *(u32x4*)((bf16*)p.C + (long long)m * p.ldc + n) = o;
       else if (m < p.M && n < p.N) *(u32x2*)((bf16*)p.C + (long long)m * p.ldc + n) = (u32x2){o[0], o[1]};
@@ -1012,8 +972,8 @@ __device__ __forceinline__ void g3_rowscale_gather_epilogue(const GP& p, const f
 // resid, and bf16 x GELU' (the FFN backward). The operand rows for fragment row i + 1 are loaded before row i's
 // stores are issued, so the compiler's counted waits never drain the stores (vmcnt retires in issue order).
 // (A two-row-ahead variant measured no faster in the step.)
-// f32 rows: one 16-B load / store per fragment (16 rows x 64 B per instruction); GELU': the permlane-swapped
-// 8-column layout of store_pair_bf16, with the matching 16-B aux loads.
+// f32 rows: one 16-B load per fragment (16 rows x 64 B per instruction), whole-line stores (store_rows_f32); GELU':
+// the permlane-swapped 8-column layout of store_pair_bf16, with the matching 16-B aux loads, whole-line stores.
 template <int EPI>
 __device__ __forceinline__ void g3_reg_epilogue_ld(const GP& p, const f32x4 (&acc)[8][4], const float* sbias, int m0,
                                                    int n0, int batch, int split, int wr, int wc, int lane) {
@@ -1039,7 +999,7 @@ __device__ __forceinline__ void g3_reg_epilogue_ld(const GP& p, const f32x4 (&ac
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       if (i + 1 < 8) ld_row(i + 1, nxt);
-      const int m = m0 + wr * 128 + i * 16 + li;
+      u32x4 o[2];
 #pragma unroll
       for (int jp = 0; jp < 2; ++jp) {
         const f32x4 x = p.alpha * acc[i][2 * jp] + b4[2 * jp], y = p.alpha * acc[i][2 * jp + 1] + b4[2 * jp + 1];
@@ -1051,12 +1011,10 @@ __device__ __forceinline__ void g3_reg_epilogue_ld(const GP& p, const f32x4 (&ac
           w[4 + e] = __uint_as_float(s[1]);
         }
         const bf16x8 a = __builtin_bit_cast(bf16x8, cur[jp]);
-        const u32x4 o = {pack_bf16x2(w[0] * (float)a[0], w[1] * (float)a[1]), pack_bf16x2(w[2] * (float)a[2], w[3] * (float)a[3]),
-                         pack_bf16x2(w[4] * (float)a[4], w[5] * (float)a[5]), pack_bf16x2(w[6] * (float)a[6], w[7] * (float)a[7])};
-        const int n = nb + 32 * jp + cs;
-        if (m < p.M && n + 8 <= p.N) *(u32x4*)((bf16*)p.C + cofs + (long long)m * p.ldc + n) = o;
-        else if (m < p.M && n < p.N) *(u32x2*)((bf16*)p.C + cofs + (long long)m * p.ldc + n) = (u32x2){o[0], o[1]};
+        o[jp] = (u32x4){pack_bf16x2(w[0] * (float)a[0], w[1] * (float)a[1]), pack_bf16x2(w[2] * (float)a[2], w[3] * (float)a[3]),
+                        pack_bf16x2(w[4] * (float)a[4], w[5] * (float)a[5]), pack_bf16x2(w[6] * (float)a[6], w[7] * (float)a[7])};
       }
+      store_rows_w16<false>((bf16*)p.C + cofs, p.ldc, m0 + wr * 128 + i * 16, p.M, nb, p.N, o, g, li);
       if (i + 1 < 8) {
         cur[0] = nxt[0];
         cur[1] = nxt[1];
@@ -1082,15 +1040,24 @@ __device__ __forceinline__ void g3_reg_epilogue_ld(const GP& p, const f32x4 (&ac
     for (int i = 0; i < 8; ++i) {
       if (i + 1 < 8) ld_row(i + 1, nxt);
       const int m = m0 + wr * 128 + i * 16 + li;
+      f32x4 x[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int n = nb + j * 16 + 4 * g;
-        f32x4 x = p.alpha * acc[i][j] + b4[j];
+        x[j] = p.alpha * acc[i][j] + b4[j];
         if constexpr (EPI == SVAE_EPI_DROPOUT_RESID) {
-          if (p.drop_p > 0.f) dropout4(p, x, m, n);
+          if (p.drop_p > 0.f) dropout4(p, x[j], m, n);
         }
-        x += cur[j];
-        if (m < p.M && n < p.N) *(f32x4*)((float*)p.C + cofs + (long long)m * p.ldc + n) = x;
+        x[j] += cur[j];
+      }
+      if constexpr (EPI == SVAE_EPI_F32_ACC) {   // (the head dW: the merge's registers cost spills, 1185 -> 1211 us)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int n = nb + j * 16 + 4 * g;
+          if (m < p.M && n < p.N) *(f32x4*)((float*)p.C + cofs + (long long)m * p.ldc + n) = x[j];
+        }
+      } else {
+        store_rows_f32((float*)p.C + cofs, p.ldc, m0 + wr * 128 + i * 16, p.M, nb, p.N, x, g, li);
       }
       if (i + 1 < 8) {
 #pragma unroll
