@@ -39,6 +39,7 @@ struct AP {
   float* dq_part; void* dq_bf; long long ldq_bf;
   int window;        // > 0: causal sliding window of `window` 32-key blocks plus key block 0 (SparseAttention)
   int kblk;          // backward: keys per dQ partial (the key block of the kernel that wrote dq_part)
+  int dq_direct;     // backward (attn_bwd8, causal): key block 0 stores the final dQ of queries < 256 itself
 };
 
 // Block-sparse sliding window of SparseAttention (sparse_attention.py:39-60, causal, block 32): query q sees
@@ -374,7 +375,22 @@ __device__ __forceinline__ void attn_fwd_tile(const AP& p, char* smem, int bx, i
         }
       }
       const bool pad_any = pad && __builtin_amdgcn_ballot_w64((pms[lane] & 0xFFu) != 0) != 0;
-      if (pad_any || kbase + 64 > p.Lk || (p.causal && kbase + 63 > qw) || (kbase + 63 >= SBLK && kbase < lo_w)) {
+      const bool band_edge = kbase + 63 >= SBLK && kbase < lo_w;
+      if (HDC == 64 && !pad_any && !band_edge && (kbase + 64 > p.Lk || (p.causal && kbase + 63 > qw))) {
+        // The causal diagonal / ragged end alone (the common edge tile): key kl = 16 sx + 4 g + r is visible iff
+        // kl < lim_j, i.e. 16 sx + r < lim_j - 4 g -- one compare against an inline constant and one select per score
+        // instead of ~5 VALU + 2 hazard nops (the general form below). hd 64 only: at hd 96 the second path raised the
+        // forward's spills from 1 to 17 VGPRs.
+        const int t0 = (p.causal ? min(p.Lk, qw + li + 1) : p.Lk) - kbase - 4 * g;
+        const int t1 = (p.causal ? min(p.Lk, qw + 16 + li + 1) : p.Lk) - kbase - 4 * g;
+#pragma unroll
+        for (int sx = 0; sx < 4; ++sx)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            s[0][sx][r] = 16 * sx + r < t0 ? s[0][sx][r] : -INFINITY;
+            s[1][sx][r] = 16 * sx + r < t1 ? s[1][sx][r] : -INFINITY;
+          }
+      } else if (pad_any || kbase + 64 > p.Lk || (p.causal && kbase + 63 > qw) || band_edge) {
         // Edge tile (wave-uniform branch). The per-key tests are branch-free: bitwise ORs of compares feeding one
         // select per score (short-circuit || compiled to an exec-mask branch per score, ~5 scalar instructions each).
         // This lane's keys are kl = 16 sx + 4 g + r; its key-padding bits come from 4 16-B LDS reads.
@@ -1028,6 +1044,15 @@ __device__ __forceinline__ void attn_bwd_tile_wide(const AP& p, char* smem, int 
 //
 constexpr int BWD8_KEYS = 256;
 
+#ifdef SVAE_STAMPS
+// diagnostic build only: per (hardware block < 1024, wave) cycle sums of the q-tile phases of attn_bwd8 --
+// [0] prologue (block start -> loop), [1] S / dP / dV / dK + dS^T writes, [2] wait at the dS^T barrier, [3] dQ MFMAs
+// + stores, [4] end-of-tile DMA wait + barrier, [5] epilogue (dK / dV stores, drained), [6] live q-tiles, [7] q-tiles
+__device__ unsigned long long svae_bwd8_stamps[1024][8][8];
+#define BWD8_T(v) unsigned long long v = __builtin_amdgcn_s_memtime()
+#define BWD8_ACC(k, a, b) (st_acc[k] += (b) - (a))
+#endif
+
 template <int HDC>
 __device__ __forceinline__ void attn_bwd8_tile(const AP& p, char* smem, int kb, int h, int b) {
   using R = RowImg<HDC>;
@@ -1047,6 +1072,10 @@ __device__ __forceinline__ void attn_bwd8_tile(const AP& p, char* smem, int kb, 
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, li = lane & 15;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int k0 = kb * BWD8_KEYS;
+#ifdef SVAE_STAMPS
+  unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  BWD8_T(t_start);
+#endif
   const bf16* Q = p.q + b * p.bq + (long long)h * p.hd;
   const bf16* K = p.k + b * p.bk + (long long)h * p.hd;
   const bf16* V = p.v + b * p.bv + (long long)h * p.hd;
@@ -1091,6 +1120,10 @@ __device__ __forceinline__ void attn_bwd8_tile(const AP& p, char* smem, int kb, 
   float* part = p.dq_part + ((long long)kb * p.B + b) * p.Lq * p.H * p.hd + (long long)h * p.hd;
   const long long ldp = (long long)p.H * p.hd;
   const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc((void*)part, 0, 0x7FFFFFF0, 0x00020000);
+  // final dQ of the direct tiles (see the dQ stores): row 0 of this (batch, head) in dq_bf (bf16) or dq (f32)
+  void* dbase = p.dq_bf ? (void*)((bf16*)p.dq_bf + (long long)b * p.Lq * p.ldq_bf + (long long)h * p.hd)
+                        : (void*)(p.dq + b * p.bdq + (long long)h * p.hd);
+  const __amdgpu_buffer_rsrc_t drs = __builtin_amdgcn_make_buffer_rsrc(dbase, 0, 0x7FFFFFF0, 0x00020000);
   // dQ partial of a query tile (64 queries x HDC dims): wave w owns queries 16 (w & 3) .. + 15 and dims
   // (w >> 2) HDC / 2 .. + HDC / 2 - 1, i.e. NT / 2 fragments, stored as NT / 2 16-B buffer stores per lane (a fixed
   // count: the end-of-tile wait leaves exactly those in flight)
@@ -1117,7 +1150,14 @@ __device__ __forceinline__ void attn_bwd8_tile(const AP& p, char* smem, int kb, 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
+#ifdef SVAE_STAMPS
+  { BWD8_T(t1); BWD8_ACC(0, t_start, t1); }
+#endif
   for (int qt = qt0; qt < nqt; ++qt) {
+#ifdef SVAE_STAMPS
+    BWD8_T(ta);
+    st_acc[7] += 1;
+#endif
     const int buf = (qt - qt0) & 1;
     const int qb = qt * 64;
     const char* Qs = QO + buf * 2 * R::BYTES;
@@ -1125,6 +1165,9 @@ __device__ __forceinline__ void attn_bwd8_tile(const AP& p, char* smem, int kb, 
     const float* nl = cst + buf * 128;
     if (qt + 1 < nqt) fetch(qb + 64, buf ^ 1);
     const bool live = (!p.causal || kw <= qb + 63) && qb < band_end && kw < p.Lk;
+#ifdef SVAE_STAMPS
+    if (live) st_acc[6] += 1;
+#endif
     if (live) {
       const char* Kw = Ks + (w >> 1) * R::BYTES;     // this wave's 32 keys: rows 32 (w & 1) .. of image w / 2
       const bool edge = !keys_all_ok || qb + 64 > p.Lq || (p.causal && kw + 31 > qb) || qb + 63 >= band_end;
@@ -1218,8 +1261,16 @@ __device__ __forceinline__ void attn_bwd8_tile(const AP& p, char* smem, int kb, 
         for (int t = 0; t < 4; ++t) *(bf16x4*)(dSs + TS::uoff(32 * w + 16 * j + li, 4 * t + g)) = z;
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#ifdef SVAE_STAMPS
+    BWD8_T(tb);
+    BWD8_ACC(1, ta, tb);
+#endif
     __builtin_amdgcn_s_barrier();   // dS^T complete (a raw barrier: __syncthreads' vmcnt(0) would drain the DMA)
     asm volatile("" ::: "memory");
+#ifdef SVAE_STAMPS
+    BWD8_T(tc);
+    BWD8_ACC(2, tb, tc);
+#endif
     // partial dQ[q = qb + 16 dq_q16 + li][d = 16 (dq_u0 + u) + 4g + r] over the block's keys (K fragment as the first
     // MFMA operand: a lane holds 4 consecutive dims of one query)
     f32x4 dq[DQ_NT];
@@ -1257,7 +1308,37 @@ __device__ __forceinline__ void attn_bwd8_tile(const AP& p, char* smem, int kb, 
         }
       }
     }
-    {
+    if (p.dq_direct && qb + 64 <= BWD8_KEYS) {
+      // causal, key block 0, queries < 256: this block holds every key these queries see, so dQ is final here
+      // (scale, inverse rotary, bf16 or f32 out) -- no partial plane, and attn_dq_reduce skips these rows. The same
+      // number of store instructions as the partial path (out-of-range offsets for masked lanes): the end-of-tile wait
+      // counts them.
+      const int q = qb + 16 * dq_q16 + li;
+      const bool qok = q < p.Lq;
+#pragma unroll
+      for (int u = 0; u < DQ_NT; ++u) {
+        const int d = 16 * (dq_u0 + u) + 4 * g;
+        const bool ok = qok && d < p.hd;
+        f32x4 v = dq[u] * p.scale;
+        if (p.dq_bf) {
+          if (p.rot) {
+            const f32x4 cs = ok ? *(const f32x4*)(p.rot + ((long long)q * (p.rot_d / 2) + (h * p.hd + d) / 2) * 2)
+                                : (f32x4){1.f, 0.f, 1.f, 0.f};
+            const float a0 = v[0], b0 = v[1], a1 = v[2], b1 = v[3];
+            v[0] = a0 * cs[0] + b0 * cs[1];
+            v[1] = -a0 * cs[1] + b0 * cs[0];
+            v[2] = a1 * cs[2] + b1 * cs[3];
+            v[3] = -a1 * cs[3] + b1 * cs[2];
+          }
+          const bf16x4 pk = {f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, pk), drs,
+                                                ok ? (q * (int)p.ldq_bf + d) * 2 : 0x7FFFFFF0, 0, 0);
+        } else {
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), drs, ok ? (q * (int)ldp + d) * 4 : 0x7FFFFFF0,
+                                                 0, 0);
+        }
+      }
+    } else {
       const bool qok = qb + 16 * dq_q16 + li < p.Lq;
       const int qrow = (qb + 16 * dq_q16 + li) * (int)ldp + 4 * g;
 #pragma unroll
@@ -1267,12 +1348,22 @@ __device__ __forceinline__ void attn_bwd8_tile(const AP& p, char* smem, int kb, 
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, dq[u]), prs, off, 0, 0);
       }
     }
+#ifdef SVAE_STAMPS
+    BWD8_T(td);
+    BWD8_ACC(3, tc, td);
+#endif
     // the next tile's DMA (issued before this tile's stores) has landed; the stores stay in flight
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DQ_STORES) : "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+#ifdef SVAE_STAMPS
+    { BWD8_T(te); BWD8_ACC(4, td, te); }
+#endif
   }
+#ifdef SVAE_STAMPS
+  BWD8_T(t_ep);
+#endif
 
   // epilogue: dK (scaled, inverse rotary) and dV for key = kw + 16j + li, dims 16u + 4g + (0..3)
 #pragma unroll
@@ -1302,6 +1393,18 @@ __device__ __forceinline__ void attn_bwd8_tile(const AP& p, char* smem, int kb, 
       *(bf16x4*)(DV + d) = (bf16x4){f2bf(dv[j][u][0]), f2bf(dv[j][u][1]), f2bf(dv[j][u][2]), f2bf(dv[j][u][3])};
     }
   }
+#ifdef SVAE_STAMPS
+  {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    BWD8_T(t_end);
+    BWD8_ACC(5, t_ep, t_end);
+    const int lin_id = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    unsigned long long x = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) x = lane == k ? st_acc[k] : x;   // (static indices: no scratch array)
+    if (lin_id < 1024 && lane < 8) svae_bwd8_stamps[lin_id][w][lane] = x;
+  }
+#endif
 }
 
 template <int HDC>
@@ -1340,6 +1443,7 @@ __global__ __launch_bounds__(256) void attn_dq_reduce_kernel(AP p) {
   const int nkb = (p.Lk + KB - 1) / KB;
   const long long plane = (long long)rows * D;
   const int nk = p.causal ? min(nkb, q / KB + 1) : nkb;
+  if (p.dq_direct && q < KB) return;   // written final by attn_bwd8 (causal: key block 0 is the only contributor)
   // sliding window: key block k >= 1 wrote partials only for the query tiles it swept (see attn_bwd_kernel)
   int k1 = 1;
   if (p.window > 0)
@@ -1389,6 +1493,8 @@ bool fill(const svae_attn_desc* d, AP& p) {
   p.o32 = d->o32; p.so32 = d->so32; p.bo32 = d->bo32;
   p.dq_part = d->dq_part; p.dq_bf = d->dq_bf; p.ldq_bf = d->ldq_bf;
   p.window = d->window;
+  p.kblk = BWD_KEYS;
+  p.dq_direct = 0;
   if (p.window < 0 || (p.window > 0 && !p.causal)) return false;
   if (p.o32 && ((p.so32 | p.bo32) % 4)) return false;
   return true;
@@ -1428,8 +1534,11 @@ SVAE_EXPORT int svae_attn_bwd(const svae_attn_desc* d, svae_stream_t stream) {
   // hd <= 96: the 8-wave 256-key kernel; hd 128: the 4-wave 128-key one (its LDS rows do not fit the 8-wave layout).
   // SVAE_ATTN_BWD8=0: the 4-wave kernels for every hd (A/B runs)
   static const int bwd8_env = [] { const char* e = getenv("SVAE_ATTN_BWD8"); return e ? atoi(e) : 1; }();
+  // SVAE_ATTN_DQ_DIRECT=0: every query tile through the partial planes (A/B runs)
+  static const int direct_env = [] { const char* e = getenv("SVAE_ATTN_DQ_DIRECT"); return e ? atoi(e) : 1; }();
   if (bwd8_env && d->hd <= 96) {
     p.kblk = BWD8_KEYS;
+    p.dq_direct = (d->causal && direct_env) ? 1 : 0;
     dim3 grid8((d->Lk + BWD8_KEYS - 1) / BWD8_KEYS, d->H, d->B);
     if (d->hd <= 64) hipLaunchKernelGGL(attn_bwd8_kernel<64>, grid8, dim3(512), 0, s, p);
     else hipLaunchKernelGGL(attn_bwd8_kernel<96>, grid8, dim3(512), 0, s, p);
@@ -1454,5 +1563,8 @@ SVAE_EXPORT int64_t svae_attn_dq_part_elems(int32_t B, int32_t H, int32_t Lq, in
 #ifdef SVAE_STAMPS
 extern "C" __attribute__((visibility("default"))) int svae_debug_attn_stamps(unsigned long long* host) {
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(svae_attn_stamps), sizeof(svae_attn_stamps)) == hipSuccess ? 0 : -1;
+}
+extern "C" __attribute__((visibility("default"))) int svae_debug_bwd8_stamps(unsigned long long* host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(svae_bwd8_stamps), sizeof(svae_bwd8_stamps)) == hipSuccess ? 0 : -1;
 }
 #endif

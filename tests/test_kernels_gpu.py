@@ -514,10 +514,14 @@ def test_attention_sliding_window_fwd_bwd(B, H, L, hd, window, padded):
     assert _rel(dv, unheads(vr.grad)) < 2e-2
 
 
-def test_attention_bwd_fused_dq_rotary():
-    """bf16 dQ from the partial-sum reduce with inverse rotary == f32 dQ followed by dq_finalize."""
+@pytest.mark.parametrize('B,H,L,hd', [
+    (2, 4, 256, 64),     # every query < 256: dQ written final by key block 0 (no partial planes)
+    (2, 2, 640, 96),     # queries < 256 direct, the rest through the partial planes and the reduce
+])
+def test_attention_bwd_fused_dq_rotary(B, H, L, hd):
+    """bf16 dQ with inverse rotary (from key block 0 directly, or from the partial-sum reduce) == f32 dQ followed by
+    dq_finalize."""
     torch.manual_seed(9)
-    B, H, L, hd = 2, 4, 256, 64
     d = H * hd
     qkv = torch.randn(B * L, 3 * d, device=dev).bfloat16()
     o = torch.empty(B * L, d, device=dev, dtype=torch.bfloat16)
