@@ -42,6 +42,7 @@ struct GP {
   int total3;        // gemm256: tiles x batch x splits (blocks loop over tiles with stride gridDim.x)
   int desync;        // gemm256 persistent: odd blocks start this many s_sleep(127) late (staggered epilogues)
   int relaxed;       // gemm256 persistent: allow the vmcnt(G3_EPI_STORES) first wait after interior epilogues
+  int dma_stagger;   // gemm256: the M-half-1 waves issue their next-K-tile DMA after their first MFMA quadrant
   long long slab;    // split-K slab mode: split s writes its partial tile at C + s * slab (0 = off)
 };
 
@@ -1202,8 +1203,11 @@ __device__ __forceinline__ void gemm256_run(const GP& p, int blk, int nwg) {
       const char* lb = la + G3_T;
       char* nxt = smem + ((g + 1) & 1) * G3_STAGE;
       const bool do_rs = AT && p.a_rowsum && T.bn < 2;
+      // p.dma_stagger: the two waves of a SIMD (wr 0 and 1, same wc) issue their pieces of the next K-tile at different
+      // times -- wr 0 here, wr 1 after its first MFMA quadrant -- so one wave's DMA issue runs beside the other's MFMAs
+      const bool late = EPI != G3_EPI_ACC_KW && p.dma_stagger && wr == 1 && kt + 1 < T.nk;   // (wave-uniform)
       if (kt + 1 < T.nk) {
-        g3_issue<AT, BT>(p, T.A, T.B, sa, sb, T.m0, T.n0, T.kbeg + (kt + 1) * 64, T.kend, nxt, wave);
+        if (!late) g3_issue<AT, BT>(p, T.A, T.B, sa, sb, T.m0, T.n0, T.kbeg + (kt + 1) * 64, T.kend, nxt, wave);
       } else if (has_next) {   // the next tile's first K-tile, in flight during this tile's epilogue
         const G3Tile TN = g3_tile(p, t3n);
         if (TN.nk > 0) {
@@ -1263,6 +1267,11 @@ __device__ __forceinline__ void gemm256_run(const GP& p, int blk, int nwg) {
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int j = 0; j < 2; ++j) acc[i][j] = mfma16(b0[j][ks], a0[i][ks], acc[i][j]);
+      if (late) {
+        __builtin_amdgcn_sched_barrier(0);
+        g3_issue<AT, BT>(p, T.A, T.B, sa, sb, T.m0, T.n0, T.kbeg + (kt + 1) * 64, T.kend, nxt, wave);
+        __builtin_amdgcn_sched_barrier(0);
+      }
       if constexpr (!AT) {   // (AT: transposed A reads need the registers; load after the a0 quadrants)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
@@ -1551,6 +1560,7 @@ static void fill_gp(const svae_gemm_desc* d, GP& p) {
   p.gather = (const bf16*)d->gather; p.ldg = d->ldg;
   p.epi = d->epi;
   p.slab = 0;
+  p.dma_stagger = 0;
 }
 
 SVAE_EXPORT int svae_gemm(const svae_gemm_desc* d, svae_stream_t stream) {
@@ -1634,6 +1644,9 @@ SVAE_EXPORT int svae_gemm(const svae_gemm_desc* d, svae_stream_t stream) {
     static const int relax_env = [] { const char* e = getenv("SVAE_GEMM_RELAX"); return e ? atoi(e) : 1; }();
     // (the CE-statistics epilogue without a logits store issues too few stores for the counted first wait)
     p.relaxed = relax_env && !(d->epi == SVAE_EPI_CE_STATS && !d->C);
+    // (SVAE_GEMM_STAGGER=0 for A/B: C2 step 12.89 / 12.99 -> 12.75 / 12.73 ms, head forward 1.12 -> 1.07 ms)
+    static const int stagger_env = [] { const char* e = getenv("SVAE_GEMM_STAGGER"); return e ? atoi(e) : 1; }();
+    p.dma_stagger = stagger_env;
     dim3 grid3((unsigned)nb3);
 #define SVAE_GEMM3_CASE(E)                                                                                   \
   case E:                                                                                                    \
@@ -1744,7 +1757,7 @@ SVAE_EXPORT int svae_gemm_pair(const svae_gemm_desc* d0, const svae_gemm_desc* d
     if (nb[i] > (1 << 24)) return SVAE_EINVAL;
     p.total3 = (int)nb[i];
     p.desync = 0;
-    p.relaxed = 1;
+    p.relaxed = 1;   // (p.dma_stagger stays 0: on the paired dW launches it measured 12.72 / 12.77 -> 12.79 / 12.93 ms)
   }
   q.nb0 = (int)((nb[0] + 7) / 8 * 8);   // block ranges start on an XCD boundary (block id % 8)
   hipStream_t s = (hipStream_t)stream;
