@@ -33,3 +33,19 @@ for M, N_, K_ in [(512, 512, 32768), (2048, 512, 32768), (1536, 512, 32768), (51
     t = timeit(lambda: K.linear_dw(dY, X, C, K_, M, N_, bgrad=bg))
     print(f'impl={os.environ.get("SVAE_GEMM_IMPL", "auto")} dW M={M} N={N_} K={K_} splits={K.auto_splits(M, N_, K_)} '
           f'{t:7.1f} us {2.0 * M * N_ * K_ / t / 1e6:7.1f} TF/s', flush=True)
+
+# the two paired launches of the step (FFN1 + FFN2 weight gradients; QKV + out-projection with their bias sums)
+T, d = 32768, 512
+h = torch.randn(T, d, device=dev).to(torch.bfloat16)
+dY2 = torch.randn(T, 2048, device=dev).to(torch.bfloat16)
+dq = torch.randn(T, 1536, device=dev).to(torch.bfloat16)
+Wg1, Wg2 = torch.zeros(2048, d, device=dev), torch.zeros(d, 2048, device=dev)
+Wq, Wo, bq, bo = torch.zeros(1536, d, device=dev), torch.zeros(d, d, device=dev), torch.zeros(1536, device=dev), \
+    torch.zeros(d, device=dev)
+t = timeit(lambda: K.linear_dw_pair((dY2, h, Wg1, T, 2048, d, None, None, None), (h, dY2, Wg2, T, d, 2048, None, None,
+                                                                                  None)))
+print(f'pair ffn1+ffn2 dW {t:7.1f} us {2.0 * 2 * 2048 * d * T / t / 1e6:7.1f} TF/s', flush=True)
+t = timeit(lambda: K.linear_dw_pair((dq, h, Wq, T, 1536, d, None, None, bq), (h, h, Wo, T, d, d, None, None, bo)))
+print(f'pair qkv+out dW (bias sums) {t:7.1f} us {2.0 * (1536 + 512) * d * T / t / 1e6:7.1f} TF/s', flush=True)
+t = timeit(lambda: K.linear_dw_pair((dq, h, Wq, T, 1536, d, None, None, None), (h, h, Wo, T, d, d, None, None, None)))
+print(f'pair qkv+out dW (no bias) {t:7.1f} us {2.0 * (1536 + 512) * d * T / t / 1e6:7.1f} TF/s', flush=True)

@@ -81,3 +81,35 @@ report('ffn1-dX gelu_bwd', lambda: K.gemm(h, W1, f, T, 2048, d, epi=N.EPI_GELU_B
 A8 = torch.randn(8192, 8192, device=dev).to(bf16)
 C8 = torch.empty(8192, 8192, device=dev, dtype=bf16)
 report('8K^3 bf16', lambda: K.gemm(A8, A8, C8, 8192, 8192, 8192, epi=N.EPI_BF16))
+
+# split-K weight-gradient pairs (one tile per block: the K loop covers the block's whole K slice) and the clock the
+# stamps count at (s_memtime cycles of block 0's tile against HIP-event time of the same launch)
+dY2 = torch.randn(T, 2048, device=dev).to(bf16)
+Wg1 = torch.zeros(2048, d, device=dev)
+Wg2 = torch.zeros(d, 2048, device=dev)
+ffn_pair = lambda: K.linear_dw_pair((dY2, h, Wg1, T, 2048, d, None, None, None),   # noqa: E731
+                                    (h, dY2, Wg2, T, d, 2048, None, None, None))
+report('ffn dW pair (64 K-tiles)', ffn_pair)
+dq = torch.randn(T, 1536, device=dev).to(bf16)
+Wq = torch.zeros(1536, d, device=dev)
+Wo2 = torch.zeros(d, d, device=dev)
+bq, bo = torch.zeros(1536, device=dev), torch.zeros(d, device=dev)
+qkv_pair = lambda: K.linear_dw_pair((dq, h, Wq, T, 1536, d, None, None, bq),   # noqa: E731
+                                    (h, h, Wo2, T, d, d, None, None, bo))
+report('qkv+out dW pair (32 K-tiles)', qkv_pair)
+for name, fn in (('ffn dW pair', ffn_pair), ('qkv+out dW pair', qkv_pair), ('8K^3', lambda: K.gemm(
+        A8, A8, C8, 8192, 8192, 8192, epi=N.EPI_BF16))):
+    N.lib.svae_debug_stamps_clear()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn()
+    torch.cuda.synchronize()
+    N.lib.svae_debug_stamps_clear()
+    e0.record()
+    fn()
+    e1.record()
+    torch.cuda.synchronize()
+    s = stamps()
+    nt = int((s[0, :, 0] > 0).sum())
+    span = int(s[:, nt - 1, 2].max() - s[:, 0, 0].min())
+    us = e0.elapsed_time(e1) * 1e3
+    print(f'{name:28s} launch {us:8.1f} us  blocks 0-7 span {span} cyc -> {span / us:7.0f} MHz lower bound', flush=True)
