@@ -97,6 +97,17 @@ bq, bo = torch.zeros(1536, device=dev), torch.zeros(d, device=dev)
 qkv_pair = lambda: K.linear_dw_pair((dq, h, Wq, T, 1536, d, None, None, bq),   # noqa: E731
                                     (h, h, Wo2, T, d, d, None, None, bo))
 report('qkv+out dW pair (32 K-tiles)', qkv_pair)
+# the transposed K-step alone: 8K^3 dY^T X layout, one FFN1 dW tile column without splits (16 blocks: no contention),
+# and the same GEMM split 16 ways (256 blocks)
+C8f = torch.zeros(8192, 8192, device=dev)
+report('8K^3 at bt f32_acc', lambda: K.gemm(A8, A8, C8f, 8192, 8192, 8192, a_t=True, b_t=True, epi=N.EPI_F32_ACC))
+dY4, h4 = dY2[:4096], h[:4096]
+report('ffn1 dW K=4096 16 blocks', lambda: K.gemm(dY4, h4, Wg1, 2048, d, 4096, a_t=True, b_t=True, lda=2048, ldb=d,
+                                                    ldc=d, epi=N.EPI_F32_ACC))
+report('ffn1 dW K=32768 split 16', lambda: K.linear_dw(dY2, h, Wg1, T, 2048, d))
+h8 = torch.randn(4096, 8192, device=dev).to(bf16)
+report('8K^2 x K=4096 at bt (256 blk)', lambda: K.gemm(h8, h8, C8f, 8192, 8192, 4096, a_t=True, b_t=True,
+                                                        epi=N.EPI_F32_ACC))
 for name, fn in (('ffn dW pair', ffn_pair), ('qkv+out dW pair', qkv_pair), ('8K^3', lambda: K.gemm(
         A8, A8, C8, 8192, 8192, 8192, epi=N.EPI_BF16))):
     N.lib.svae_debug_stamps_clear()
