@@ -40,7 +40,6 @@ struct GP {
   int tn2, tm2;      // 256-tile counts (gemm256)
   int group;         // L2 grouping: consecutive tiles walk `group` tile rows (M) before the next tile column
   int total3;        // gemm256: tiles x batch x splits (blocks loop over tiles with stride gridDim.x)
-  int desync;        // gemm256 persistent: odd blocks start this many s_sleep(127) late (staggered epilogues)
   int relaxed;       // gemm256 persistent: allow the vmcnt(G3_EPI_STORES) first wait after interior epilogues
   int dma_stagger;   // gemm256: the M-half-1 waves issue their next-K-tile DMA after their first MFMA quadrant
   long long slab;    // split-K slab mode: split s writes its partial tile at C + s * slab (0 = off)
@@ -1175,9 +1174,6 @@ __device__ __forceinline__ void gemm256_run(const GP& p, int blk, int nwg) {
   if (T.nk > 0) {
     g3_issue<AT, BT>(p, T.A, T.B, sa, sb, T.m0, T.n0, T.kbeg, T.kend, smem, wave);
   }
-  if (p.desync > 0 && (bid & 1)) {   // stagger the epilogues of neighbouring blocks (HBM write bursts)
-    for (int i = 0; i < p.desync; ++i) __builtin_amdgcn_s_sleep(127);
-  }
 
   bool relaxed = false;   // the previous tile was interior: its epilogue issued >= G3_EPI_STORES stores per wave
   int ntile = 0;
@@ -1631,7 +1627,6 @@ SVAE_EXPORT int svae_gemm(const svae_gemm_desc* d, svae_stream_t stream) {
     // persistent above one block per CU (1 block of 8 waves fits a CU): blocks walk their tiles and prefetch the
     // next tile's first K-tile under the current tile's epilogue. SVAE_GEMM_PERSIST=0 restores 1 block per tile.
     static const int persist_env = [] { const char* e = getenv("SVAE_GEMM_PERSIST"); return e ? atoi(e) : 1; }();
-    static const int desync_env = [] { const char* e = getenv("SVAE_GEMM_DESYNC"); return e ? atoi(e) : -1; }();
     static const int ncu = [] {
       int dev = 0, n = 0;
       if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
@@ -1640,7 +1635,6 @@ SVAE_EXPORT int svae_gemm(const svae_gemm_desc* d, svae_stream_t stream) {
     }();
     p.total3 = (int)blocks256;
     const long long nb3 = persist_env ? std::min<long long>(blocks256, ncu) : blocks256;
-    p.desync = (nb3 < blocks256 && desync_env > 0) ? desync_env : 0;   // measured: staggering does not pay
     static const int relax_env = [] { const char* e = getenv("SVAE_GEMM_RELAX"); return e ? atoi(e) : 1; }();
     // (the CE-statistics epilogue without a logits store issues too few stores for the counted first wait)
     p.relaxed = relax_env && !(d->epi == SVAE_EPI_CE_STATS && !d->C);
@@ -1756,7 +1750,6 @@ SVAE_EXPORT int svae_gemm_pair(const svae_gemm_desc* d0, const svae_gemm_desc* d
     nb[i] = (long long)p.tn2 * p.tm2 * d[i]->splits;
     if (nb[i] > (1 << 24)) return SVAE_EINVAL;
     p.total3 = (int)nb[i];
-    p.desync = 0;
     p.relaxed = 1;   // (p.dma_stagger stays 0: on the paired dW launches it measured 12.72 / 12.77 -> 12.79 / 12.93 ms)
   }
   q.nb0 = (int)((nb[0] + 7) / 8 * 8);   // block ranges start on an XCD boundary (block id % 8)
