@@ -4,6 +4,11 @@
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
+`--gpus N` (N > 1) without WORLD_SIZE in the environment: this process launches the N ranks itself (one child
+per GPU with the torchrun environment, as Lightning's Trainer(gpus=N) does for the reference, train.py:63-64, 94),
+never touching the GPU; it exits non-zero at once when fewer than N GPUs are visible. At N > 1 the line also
+carries `scaling_efficiency` against a same-run N=1 rate (all-reduce off, after the timed region).
+
 A step = TransformerVAE.training_step (forward) + loss.backward() (engine backward with the bucketed RCCL
 gradient all-reduce overlapped) + on_after_backward (grad norm, KL anneal) + RAdam.step (fused clip +
 update) + LambdaLR.step, on a synthetic batch resident in HBM. Weak scaling: every rank runs the per-GPU
@@ -20,6 +25,7 @@ import argparse
 import json
 import math
 import os
+import subprocess
 import sys
 import time
 
@@ -49,6 +55,12 @@ def flops_per_token(nl, d, L, V=V, N=NLAT):
         + (4 * d * d * N + 4 * N * d + 18 * d * d) / L
     f_fwd = nl * (24 * d * d + 4 * L * d) + 2 * d * d + 2 * d * V + f_enc
     return 3 * f_fwd
+
+
+def flops_per_token_causal(nl, d, L, V=V, N=NLAT):
+    """The causal-useful count: the dense count less the masked half of the decoder's causal
+    attention scores and P.V products, nl * 2 * L * d per token forward."""
+    return flops_per_token(nl, d, L, V, N) - 3 * nl * 2 * L * d
 
 
 def build(cfg, device):
@@ -165,6 +177,71 @@ def parity_check(cfg, device):
             'argmax_fp32_mode_agreement': (am_gpu == am_ref).float().mean().item()}
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def device_count_in_child(python=sys.executable):
+    """GPUs visible to a fresh process. Queried in a child so the launcher itself never initialises HIP (a
+    process that has must not fork ranks off)."""
+    r = subprocess.run([python, '-c', 'import torch; print(torch.cuda.device_count())'],
+                       capture_output=True, text=True, timeout=600)
+    try:
+        return int(r.stdout.strip().splitlines()[-1])
+    except (ValueError, IndexError):
+        return 0
+
+
+def rank_env(rank, world, port, base=None):
+    """The environment torch.distributed.run gives rank `rank` of a one-node job."""
+    env = dict(os.environ if base is None else base)
+    env.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world),
+               GROUP_RANK='0', MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    env.setdefault('HSA_ENABLE_IPC_MODE_LEGACY', '0')          # dmabuf IPC for RCCL (see the image notes)
+    return env
+
+
+def launch_ranks(world, child_argv, poll_s=0.2):
+    """`python bench.py --gpus N` (N > 1) with no WORLD_SIZE in the environment: the reference's route to N GPUs is
+    Lightning's `Trainer(gpus=N)` (train.py:63-64, 94), which spawns one DDP process per GPU. Do the same: start N
+    child processes of `child_argv` with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT set (one
+    per GPU, RCCL over xGMI), wait for all of them, and return the first non-zero exit code (0 when all
+    succeed). Rank 0 prints the JSON line on the inherited stdout; no other rank prints to stdout. If one rank
+    fails, the others are terminated (they would wait forever in a collective)."""
+    port = _free_port()
+    procs = [subprocess.Popen(child_argv, env=rank_env(r, world, port)) for r in range(world)]
+    rc = 0
+    try:
+        live = list(procs)
+        while live:
+            for p in list(live):
+                code = p.poll()
+                if code is None:
+                    continue
+                live.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code
+                    print(f'bench.py: rank {procs.index(p)} exited with {code}; stopping the other ranks',
+                          file=sys.stderr, flush=True)
+                    for q in live:
+                        q.terminate()
+            time.sleep(poll_s)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+                try:
+                    p.wait(timeout=20)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -175,7 +252,19 @@ def main():
     ap.add_argument('--no-parity', action='store_true')
     args = ap.parse_args()
 
+    if args.gpus > 1 and 'WORLD_SIZE' not in os.environ:
+        # launcher: this process never touches the GPU; it checks the device count in a child and starts one
+        # rank per GPU
+        n = device_count_in_child()
+        if n < args.gpus:
+            print(f'bench.py: --gpus {args.gpus} needs {args.gpus} visible GPUs, this node has {n}',
+                  file=sys.stderr, flush=True)
+            sys.exit(3)
+        sys.exit(launch_ranks(args.gpus, [sys.executable, '-u', os.path.abspath(__file__)] + sys.argv[1:]))
+
     world = int(os.environ.get('WORLD_SIZE', '1'))
+    if world != args.gpus:
+        print(f'bench.py: WORLD_SIZE={world} overrides --gpus {args.gpus}', file=sys.stderr, flush=True)
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
     torch.cuda.set_device(local)
@@ -215,7 +304,27 @@ def main():
     tokens = cfg['B'] * cfg['L'] * world * args.steps
     value = tokens / dt
     fpt = flops_per_token(cfg['layers'], cfg['d'], cfg['L'])
+    fpt_causal = flops_per_token_causal(cfg['layers'], cfg['d'], cfg['L'])
     loss = model.logged.get('train_nll')
+
+    scaling = None
+    if world > 1:
+        # same-run N = 1 figure: every rank re-runs the K steps with the data-parallel gradient all-reduce off
+        # (model._dp = None is exactly the single-GPU step); after the timed region, so it never enters `value`
+        dp, model._dp = model._dp, None
+        dist.barrier()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            step(model, opt, sched, batch)
+        torch.cuda.synchronize()
+        d1 = torch.tensor([time.perf_counter() - t1], device=device)
+        dist.all_reduce(d1, op=dist.ReduceOp.MAX)
+        model._dp = dp
+        single = cfg['B'] * cfg['L'] * args.steps / d1.item()
+        scaling = {'value': round(value / (world * single), 4), 'single_gpu_tokens_per_s': round(single, 1),
+                   'basis': f'same run: the {args.steps} steps re-timed on every rank with the gradient all-reduce '
+                            f'off (the N=1 step, max over ranks); efficiency = value / (N x that rate)'}
 
     if rank == 0:
         T = cfg['B'] * cfg['L']
@@ -240,6 +349,7 @@ def main():
                        'seq_len': cfg['L'], 'parallelism': f'dp{world}'},
             'model_tflops_per_gpu': round(value / world * fpt / 1e12, 1),
             'step_mfu': round(value / world * fpt / (PEAK_BF16_TFLOPS * 1e12), 4),
+            'step_mfu_causal': round(value / world * fpt_causal / (PEAK_BF16_TFLOPS * 1e12), 4),
             'roofline': {'kernel': ('gemm256_kernel<false,false,SVAE_EPI_CE_PROB> (vocab head, stores P = exp(logit - '
                                     'label logit) + per-tile sums)' if eng.head_mode == 'prob' else
                                     'gemm256_kernel<false,false,SVAE_EPI_CE_STATS> (vocab head + CE stats)'),
@@ -249,6 +359,8 @@ def main():
                          'traffic': traffic, 'launch_ms': round(head_ms, 4), 'flops_per_launch': head_flops},
             'final_train_nll': round(loss.item(), 5) if torch.is_tensor(loss) else None,
         }
+        if scaling is not None:
+            res['scaling_efficiency'] = scaling
         if world == 1 and not args.no_parity:
             try:
                 res['parity'] = parity_check(cfg, device)

@@ -582,7 +582,8 @@ __device__ __forceinline__ void attn_bwd_tile(const AP& p, char* smem, int kb, i
   char* QO = smem;                                  // [buf][Q, dO] tiles
   char* Ks = smem + 4 * T::BYTES;                   // 128 key rows
   char* dSs = smem + 6 * T::BYTES;                  // 128 key rows x 64 queries
-  float* cst = (float*)(smem + 6 * T::BYTES + 2 * TS::BYTES);   // [buf][lse, delta][64] (DMA'd with the tile)
+  float* cst = (float*)(smem + 6 * T::BYTES + 2 * TS::BYTES);   // [buf][wave][lse, delta][64] (DMA'd with the tile)
+  constexpr int NWB = 4;
 
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, li = lane & 15;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: scalar branches, not exec masks
@@ -635,14 +636,16 @@ __device__ __forceinline__ void attn_bwd_tile(const AP& p, char* smem, int kb, i
   // so the end-of-tile wait can leave exactly those in flight (vmcnt retires in issue order).
   constexpr int DQ_STORES = NT;
 
-  // the row constants (lse, delta) of a query tile ride along with its Q / dO DMA into cst[buf][lse | delta]
+  // the row constants (lse, delta) of a query tile ride along with its Q / dO DMA into cst[buf][wave][lse | delta]
   const u32x4 lser = buffer_rsrc(lse, (unsigned)p.Lq * 4u), der = buffer_rsrc(delta, (unsigned)p.Lq * 4u);
   auto fetch = [&](int qb, int buf) {
     dma_rows<HDP>(Q, p.sq, qb, p.Lq, p.hd, QO + buf * 2 * T::BYTES, w, lane);
     dma_rows<HDP>(dO, p.sdo, qb, p.Lq, p.hd, QO + buf * 2 * T::BYTES + T::BYTES, w, lane);
     const int qo = qb + lane < p.Lq ? (qb + lane) * 4 : 0x7FFFFFF0;
-    if (w == 0) dma4_lds(lser, cst + buf * 128, qo);
-    else if (w == 1) dma4_lds(der, cst + buf * 128 + 64, qo);
+    // every wave DMAs the tile's lse and delta rows into its OWN slot; it reads them only after its own
+    // end-of-tile vmcnt (+ the block barrier), so no wave depends on another wave's DMA count
+    dma4_lds(lser, cst + (buf * NWB + w) * 128, qo);
+    dma4_lds(der, cst + (buf * NWB + w) * 128 + 64, qo);
   };
   if (qt0 < nqt) fetch(qt0 * 64, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -653,7 +656,7 @@ __device__ __forceinline__ void attn_bwd_tile(const AP& p, char* smem, int kb, i
     const int qb = qt * 64;
     const char* Qs = QO + buf * 2 * T::BYTES;
     const char* dOs = Qs + T::BYTES;
-    const float* nl = cst + buf * 128;
+    const float* nl = cst + (buf * NWB + w) * 128;
     const bool more = qt + 1 < nqt;
     if (more) fetch(qb + 64, buf ^ 1);
     const bool live = (!p.causal || kw <= qb + 63) && qb < band_end;   // some key of this wave visible to some query
@@ -825,7 +828,8 @@ __device__ __forceinline__ void attn_bwd_tile_wide(const AP& p, char* smem, int 
   char* QO = smem;                                  // [buf][Q, dO] tiles
   char* Ks = smem + 4 * T::BYTES;                   // 128 key rows
   char* dSs = smem + 6 * T::BYTES;                  // 128 key rows x 64 queries
-  float* cst = (float*)(smem + 6 * T::BYTES + 2 * TS::BYTES);   // [buf][lse, delta][64] (DMA'd with the tile)
+  float* cst = (float*)(smem + 6 * T::BYTES + 2 * TS::BYTES);   // [buf][wave][lse, delta][64] (DMA'd with the tile)
+  constexpr int NWB = 4;
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, li = lane & 15;
   const int k0 = kb * BWD_KEYS;
@@ -877,14 +881,16 @@ __device__ __forceinline__ void attn_bwd_tile_wide(const AP& p, char* smem, int 
   // issue order); edge tiles wait for everything.
   constexpr int DQ_STORES = NT;
 
-  // the row constants (lse, delta) of a query tile ride along with its Q / dO DMA into cst[buf][lse | delta]
+  // the row constants (lse, delta) of a query tile ride along with its Q / dO DMA into cst[buf][wave][lse | delta]
   const u32x4 lser = buffer_rsrc(lse, (unsigned)p.Lq * 4u), der = buffer_rsrc(delta, (unsigned)p.Lq * 4u);
   auto fetch = [&](int qb, int buf) {
     dma_rows<HDP>(Q, p.sq, qb, p.Lq, p.hd, QO + buf * 2 * T::BYTES, w, lane);
     dma_rows<HDP>(dO, p.sdo, qb, p.Lq, p.hd, QO + buf * 2 * T::BYTES + T::BYTES, w, lane);
     const int qo = qb + lane < p.Lq ? (qb + lane) * 4 : 0x7FFFFFF0;
-    if (w == 0) dma4_lds(lser, cst + buf * 128, qo);
-    else if (w == 1) dma4_lds(der, cst + buf * 128 + 64, qo);
+    // every wave DMAs the tile's lse and delta rows into its OWN slot; it reads them only after its own
+    // end-of-tile vmcnt (+ the block barrier), so no wave depends on another wave's DMA count
+    dma4_lds(lser, cst + (buf * NWB + w) * 128, qo);
+    dma4_lds(der, cst + (buf * NWB + w) * 128 + 64, qo);
   };
   if (qt0 < nqt) fetch(qt0 * 64, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -895,7 +901,7 @@ __device__ __forceinline__ void attn_bwd_tile_wide(const AP& p, char* smem, int 
     const int qb = qt * 64;
     const char* Qs = QO + buf * 2 * T::BYTES;
     const char* dOs = Qs + T::BYTES;
-    const float* nl = cst + buf * 128;
+    const float* nl = cst + (buf * NWB + w) * 128;
     const bool more = qt + 1 < nqt;
     if (more) fetch(qb + 64, buf ^ 1);
     const bool live = (!p.causal || kw <= qb + 63) && qb < band_end;   // some key of this wave visible to some query
@@ -1063,7 +1069,8 @@ __device__ __forceinline__ void attn_bwd8_tile(const AP& p, char* smem, int kb, 
   char* QO = smem;
   char* Ks = smem + 4 * R::BYTES;
   char* dSs = Ks + 4 * R::BYTES;
-  float* cst = (float*)(dSs + 4 * TS::BYTES);
+  float* cst = (float*)(dSs + 4 * TS::BYTES);   // [buf][wave][lse, delta][64] (DMA'd with the tile)
+  constexpr int NWB = 8;
   // LDS-DMA pieces per wave: one query tile's Q + dO images, and the K tile
   constexpr int QO_PW = 2 * R::PIECES / NW;
   constexpr int K_PW = 4 * R::PIECES / NW;
@@ -1124,6 +1131,7 @@ __device__ __forceinline__ void attn_bwd8_tile(const AP& p, char* smem, int kb, 
   void* dbase = p.dq_bf ? (void*)((bf16*)p.dq_bf + (long long)b * p.Lq * p.ldq_bf + (long long)h * p.hd)
                         : (void*)(p.dq + b * p.bdq + (long long)h * p.hd);
   const __amdgpu_buffer_rsrc_t drs = __builtin_amdgcn_make_buffer_rsrc(dbase, 0, 0x7FFFFFF0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.rot, 0, 0x7FFFFFF0, 0x00020000);
   // dQ partial of a query tile (64 queries x HDC dims): wave w owns queries 16 (w & 3) .. + 15 and dims
   // (w >> 2) HDC / 2 .. + HDC / 2 - 1, i.e. NT / 2 fragments, stored as NT / 2 16-B buffer stores per lane (a fixed
   // count: the end-of-tile wait leaves exactly those in flight)
@@ -1143,8 +1151,10 @@ __device__ __forceinline__ void attn_bwd8_tile(const AP& p, char* smem, int kb, 
       else dma_img_piece<HDC>(ors, p.sdo, qb, p.Lq, p.hd, base + R::BYTES, pc - R::PIECES, ln);
     }
     const int qo = qb + lane < p.Lq ? (qb + lane) * 4 : 0x7FFFFFF0;
-    if (w == 0) dma4_lds(lser, cst + buf * 128, qo);
-    else if (w == 1) dma4_lds(der, cst + buf * 128 + 64, qo);
+    // every wave DMAs the tile's lse and delta rows into its OWN slot; it reads them only after its own
+    // end-of-tile vmcnt (+ the block barrier), so no wave depends on another wave's DMA count
+    dma4_lds(lser, cst + (buf * NWB + w) * 128, qo);
+    dma4_lds(der, cst + (buf * NWB + w) * 128 + 64, qo);
   };
   if (qt0 < nqt) fetch(qt0 * 64, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1162,7 +1172,7 @@ __device__ __forceinline__ void attn_bwd8_tile(const AP& p, char* smem, int kb, 
     const int qb = qt * 64;
     const char* Qs = QO + buf * 2 * R::BYTES;
     const char* dOs = Qs + R::BYTES;
-    const float* nl = cst + buf * 128;
+    const float* nl = cst + (buf * NWB + w) * 128;
     if (qt + 1 < nqt) fetch(qb + 64, buf ^ 1);
     const bool live = (!p.causal || kw <= qb + 63) && qb < band_end && kw < p.Lk;
 #ifdef SVAE_STAMPS
@@ -1313,17 +1323,22 @@ __device__ __forceinline__ void attn_bwd8_tile(const AP& p, char* smem, int kb, 
       // (scale, inverse rotary, bf16 or f32 out) -- no partial plane, and attn_dq_reduce skips these rows. The same
       // number of store instructions as the partial path (out-of-range offsets for masked lanes): the end-of-tile wait
       // counts them.
-      const int q = qb + 16 * dq_q16 + li;
+      // lane terms from a fresh v_mbcnt: offsets derived from the hoisted lane id were kept across the q-tile loop
+      // and spilled (hd 96), and each reload's vmcnt(0) would wait on the next tile's DMA
+      const int lf = lane_id_fresh();
+      const int q = qb + 16 * dq_q16 + (lf & 15);
       const bool qok = q < p.Lq;
 #pragma unroll
       for (int u = 0; u < DQ_NT; ++u) {
-        const int d = 16 * (dq_u0 + u) + 4 * g;
+        const int d = 16 * (dq_u0 + u) + 4 * (lf >> 4);
         const bool ok = qok && d < p.hd;
         f32x4 v = dq[u] * p.scale;
         if (p.dq_bf) {
           if (p.rot) {
-            const f32x4 cs = ok ? *(const f32x4*)(p.rot + ((long long)q * (p.rot_d / 2) + (h * p.hd + d) / 2) * 2)
-                                : (f32x4){1.f, 0.f, 1.f, 0.f};
+            // 32-bit buffer offsets (a masked lane's load returns 0 and its store is dropped): the 64-bit per-fragment
+            // addresses of a plain load were hoisted out of the q-tile loop and spilled (hd 96: 3 reloads per tile)
+            const f32x4 cs = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                rrs, ok ? (q * (p.rot_d / 2) + (h * p.hd + d) / 2) * 8 : 0x7FFFFFF0, 0, 0));
             const float a0 = v[0], b0 = v[1], a1 = v[2], b1 = v[3];
             v[0] = a0 * cs[0] + b0 * cs[1];
             v[1] = -a0 * cs[1] + b0 * cs[0];
@@ -1409,7 +1424,7 @@ __device__ __forceinline__ void attn_bwd8_tile(const AP& p, char* smem, int kb, 
 
 template <int HDC>
 __global__ __launch_bounds__(512, 1) void attn_bwd8_kernel(AP p) {
-  __shared__ __attribute__((aligned(16))) char smem[8 * RowImg<HDC>::BYTES + 4 * Tile<64>::BYTES + 4 * 64 * 4];
+  __shared__ __attribute__((aligned(16))) char smem[8 * RowImg<HDC>::BYTES + 4 * Tile<64>::BYTES + 2 * 8 * 128 * 4];
   int kb, h, b;
   xcd_block(kb, h, b, p.causal ? 2 : 0);
   attn_bwd8_tile<HDC>(p, smem, kb, h, b);
@@ -1420,7 +1435,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd8_kernel(AP p) {
 // two serial prologues per workgroup cost more than the imbalance.)
 template <int HDP, int HDC = HDP>
 __global__ __launch_bounds__(256, HDP == 64 ? 2 : 1) void attn_bwd_kernel(AP p) {
-  __shared__ __attribute__((aligned(16))) char smem[6 * Tile<HDP>::BYTES + 2 * Tile<64>::BYTES + 4 * 64 * 4];
+  __shared__ __attribute__((aligned(16))) char smem[6 * Tile<HDP>::BYTES + 2 * Tile<64>::BYTES + 2 * 4 * 128 * 4];
   int kb, h, b;
   xcd_block(kb, h, b, p.causal ? 2 : 0);
   if constexpr (HDP == 64) attn_bwd_tile<HDP>(p, smem, kb, h, b);

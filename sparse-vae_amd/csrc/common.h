@@ -57,6 +57,19 @@ __device__ __forceinline__ short4v lds_read_tr3(const lds_char* p) {
 // vmcnt(0) in front of it, draining the prefetched tiles of every ring that uses transposed LDS reads. The
 // callers wait for the DMA explicitly (counted s_waitcnt vmcnt + barrier) before reading a stage.
 // rsrc: the 4 descriptor words (base lo, base hi, num_records, flags), wave-uniform.
+//
+// The statement is self-contained in two ways hipcc cannot provide for inline asm (cdna_hip_programming.md §5.7):
+//  * wait states: a VALU write of an SGPR needs 5 wait states before a VMEM instruction reads it as descriptor.
+//    hipcc pads only its own instructions, and it does put such writes right in front of these statements (an
+//    SGPR-spill reload `v_readlane_b32 s19, v208, 33` of a descriptor word, a `v_readfirstlane` recomputing a
+//    base: 2-4 states before the load in attn_bwd8 / attn_bwd / the k-weighted gemm256, scripts/isa_audit.py).
+//    The buffer_load then reads the descriptor's OLD words: silently wrong source data whenever the register held
+//    something else before (the same descriptor re-loaded is harmless, which is why it hid). The string opens with
+//    enough states (keep copy 1 + s_nop 1 (2) + m0 write 1 + s_nop 0 (1) = 5) so no instruction placed in front
+//    of it can be inside the window.
+//  * m0: compiler-reserved ("m0" in the clobber list is not honoured, only warned about); the statement saves it
+//    and restores it after the issue (the DMA reads m0 at issue).
+// scripts/isa_audit.py checks both on the built ISA (tests/test_isa_audit.py).
 __device__ __forceinline__ u32x4 buffer_rsrc(const void* base, unsigned num_records) {
   const uint64_t a = (uint64_t)(uintptr_t)base;
   return (u32x4){(unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)a),
@@ -65,29 +78,35 @@ __device__ __forceinline__ u32x4 buffer_rsrc(const void* base, unsigned num_reco
 }
 __device__ __forceinline__ void dma16_lds(const u32x4& rsrc, const void* lds_base, int voff) {
   const int m = __builtin_amdgcn_readfirstlane((int)(unsigned)(uintptr_t)lds_base);
-  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
-               :
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_nop 1\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dwordx4 %2, %3, 0 offen lds\n\t"
+               "s_mov_b32 m0, %0"
+               : "=&s"(keep)
                : "s"(m), "v"(voff), "s"(rsrc)
-               : "memory");  // (m0 is reserved: the compiler sets it before each of its own uses)
+               : "memory");
 }
 
 // 4 B per lane (buffer_load_dword ... lds) into lds_base + 4 * lane, same conventions as dma16_lds.
 __device__ __forceinline__ void dma4_lds(const u32x4& rsrc, const void* lds_base, int voff) {
   const int m = __builtin_amdgcn_readfirstlane((int)(unsigned)(uintptr_t)lds_base);
-  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dword %1, %2, 0 offen lds"
-               :
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_nop 1\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dword %2, %3, 0 offen lds\n\t"
+               "s_mov_b32 m0, %0"
+               : "=&s"(keep)
                : "s"(m), "v"(voff), "s"(rsrc)
-               : "memory");  // (m0 is reserved: the compiler sets it before each of its own uses)
+               : "memory");
 }
 
 // 1 B per lane (buffer_load_ubyte ... lds) into a dword slot per lane (lds_base + 4 * lane; the byte is the low
 // 8 bits of the slot), same conventions as dma16_lds.
 __device__ __forceinline__ void dma1_lds(const u32x4& rsrc, const void* lds_base, int voff) {
   const int m = __builtin_amdgcn_readfirstlane((int)(unsigned)(uintptr_t)lds_base);
-  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_ubyte %1, %2, 0 offen lds"
-               :
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_nop 1\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_ubyte %2, %3, 0 offen lds\n\t"
+               "s_mov_b32 m0, %0"
+               : "=&s"(keep)
                : "s"(m), "v"(voff), "s"(rsrc)
-               : "memory");  // (m0 is reserved: the compiler sets it before each of its own uses)
+               : "memory");
 }
 
 __device__ __forceinline__ bf16x8 cat44(short4v lo, short4v hi) {

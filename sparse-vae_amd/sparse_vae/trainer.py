@@ -87,7 +87,7 @@ class Trainer:
         carries no val_* key."""
         dm = self.datamodule
         saved = dict(model.logged)
-        sums, count = {}, 0
+        sums, counts, count = {}, {}, 0
         try:
             for j, batch in enumerate(dm.val_dataloader()):
                 if self.limit_val_batches is not None and j >= int(self.limit_val_batches):
@@ -97,18 +97,28 @@ class Trainer:
                 for k, v in model.logged.items():
                     if k.startswith('val_'):
                         sums[k] = sums.get(k, 0.0) + float(_scalar(v))
+                        counts[k] = counts.get(k, 0) + 1
                 count += 1
         finally:
             model.logged.clear()
             model.logged.update(saved)
         if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-            keys = sorted(sums)
-            t = torch.tensor([sums[k] for k in keys] + [float(count)], dtype=torch.float64,
+            # the ranks may hold different key sets (`val_mc_mutual_info` only where some batch had > 1 sequence):
+            # agree on the union of the names first, then reduce one fixed-length vector of per-key sums and
+            # per-key batch counts (0 where this rank has no value)
+            names = [None] * dist.get_world_size()
+            dist.all_gather_object(names, sorted(sums))
+            keys = sorted(set().union(*names))
+            t = torch.tensor([sums.get(k, 0.0) for k in keys] + [float(counts.get(k, 0)) for k in keys]
+                             + [float(count)], dtype=torch.float64,
                              device=model.device if dist.get_backend() == 'nccl' else 'cpu')
             dist.all_reduce(t)
+            n = len(keys)
             sums = {k: float(t[i]) for i, k in enumerate(keys)}
+            counts = {k: int(round(float(t[n + i]))) for i, k in enumerate(keys)}
             count = int(round(float(t[-1])))
-        logs = {k: v / max(count, 1) for k, v in sums.items()}
+        # each key is the mean over the batches that logged it (Lightning's epoch-level mean of a logged value)
+        logs = {k: v / max(counts.get(k, 0), 1) for k, v in sums.items()}
         logs['step'] = self.global_step
         logs['val_batches'] = count
         self.val_history.append(logs)

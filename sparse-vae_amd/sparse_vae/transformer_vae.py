@@ -243,6 +243,9 @@ class TransformerVAE(ContinuousVAEHooks, LanguageModel):
         if ids.shape[0] > 1 and self.hparams.get('log_mutual_info', True):
             # transformer_vae.py:59-61: kl - marginal_kl(posterior), fused (engine.mutual_info)
             self.log(stage + '_mc_mutual_info', eng.mutual_info(out, eps=eps_marginal))
+        else:
+            # not logged for this batch: drop an earlier step's value so it is neither reported nor reduced again
+            self.logged.pop(stage + '_mc_mutual_info', None)
         if stage == 'train':
             loss = _StepFn.apply(self._anchor, self, out['loss'])
             return {'loss': loss, 'posterior': Normal(loc=mu.detach(), scale=scale.detach())}
@@ -320,22 +323,28 @@ class TransformerVAE(ContinuousVAEHooks, LanguageModel):
     def reduce_logged(self, keys=LOGGED_REDUCE_KEYS):
         """the logged scalars averaged over the data-parallel ranks for reporting (each rank's
         training step logs its local values, language_model.py:112, continuous_autoencoder.py:50,
-        transformer_vae.py:61). One all-reduce of the stacked scalars; on RCCL `wait()` only orders the caller's
-        stream after it (no host synchronisation), so the step does not stall until a value is read. Every rank
-        calls it at the same optimiser steps (the trainer does, once per optimiser step); the keys are the same
-        on every rank because every rank runs the same training_step code on the same batch shapes."""
+        transformer_vae.py:61). One all-reduce of a FIXED-length vector: for every key of `keys`, the value (0 where
+        this rank did not log it) and a presence count, so ranks whose batches log different key sets (a
+        1-sequence token-budget batch logs no `train_mc_mutual_info`) still issue identical collectives; a key
+        is the mean over the ranks that logged it, and is dropped where no rank did. On RCCL `wait()` only orders
+        the caller's stream after it (no host synchronisation). Every rank calls it at the same optimiser steps
+        (the trainer does, once per optimiser step)."""
         dp = self._dp
         if dp is None:
             return
-        names = [k for k in keys if k in self.logged]
-        if not names:
-            return
+        keys = tuple(keys)
+        zero = torch.zeros((), dtype=torch.float32, device=self.device)
         vals = torch.stack([torch.as_tensor(self.logged[k], dtype=torch.float32, device=self.device).reshape(())
-                            for k in names])
+                            if k in self.logged else zero for k in keys]
+                           + [torch.tensor(float(k in self.logged), device=self.device) for k in keys])
         dist.all_reduce(vals, op=dist.ReduceOp.SUM, group=dp['group'], async_op=True).wait()
-        vals = vals / dp['world']
-        for i, k in enumerate(names):
-            self.logged[k] = vals[i]
+        n = len(keys)
+        counts = vals[n:].tolist()
+        for i, k in enumerate(keys):
+            if counts[i] > 0:
+                self.logged[k] = vals[i] / counts[i]
+            else:
+                self.logged.pop(k, None)
 
     # ------------------------------------------------------------------ inference-side helpers
     @torch.no_grad()
