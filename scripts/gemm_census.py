@@ -1,7 +1,7 @@
-"""Per-GEMM census of the C2 training step: every libsvae GEMM launch of a few bench steps timed with HIP events
-on its stream, grouped by (M, N, K, layout, epilogue, splits).
+"""Per-GEMM census of a bench config's training step (default C2): every libsvae GEMM launch of a few bench steps
+timed with HIP events on its stream, grouped by (M, N, K, layout, epilogue, splits), with TF/s per shape.
 
-    python scripts/gemm_census.py [steps] > profiles/<round>_c2_gemm_census.txt
+    python scripts/gemm_census.py [steps] [config] > profiles/<round>_<config>_gemm_census.txt
 """
 import os
 import sys
@@ -20,9 +20,11 @@ EPI = ['bf16', 'f32', 'f32_acc', 'f32_atomic', 'gelu', 'gelu_bwd', 'drop_resid',
 
 def main():
     steps = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+    cfg = sys.argv[2] if len(sys.argv) > 2 else 'c2'
     dev = torch.device('cuda', 0)
     torch.cuda.set_device(0)
-    model, opt, sched, batch = bench.build(bench.CONFIGS['c2'], dev)
+    model, opt, sched, batch = bench.build(bench.CONFIGS[cfg], dev)
+    print(f'config {cfg}: {bench.CONFIGS[cfg]}')
     for _ in range(3):
         bench.step(model, opt, sched, batch)
     torch.cuda.synchronize()
@@ -62,7 +64,7 @@ def main():
         agg[key][0] += 1
         agg[key][1] += e0.elapsed_time(e1) * 1e3
     total = sum(v[1] for v in agg.values()) / steps
-    print(f'GEMM time {total / 1e3:.3f} ms/step (HIP events around each launch, {steps} steps, C2 bench step)')
+    print(f'GEMM time {total / 1e3:.3f} ms/step (HIP events around each launch, {steps} steps, {cfg} bench step)')
     for key, (n, us) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
         M, N_, K_, at, bt, epi, sp, rs, kwt = key
         per = us / n

@@ -25,6 +25,9 @@ fi
 if [[ $ST == *p* && $rc == 0 ]]; then
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/prof" -o run -- $PB > "$OUT/prof.log" 2>&1; rc=$?
   tail -1 "$OUT/prof.log"
+  # the per-step summary and the --stats table are small; the trace itself is dropped below (> 8 MB)
+  [ $rc == 0 ] && python3 scripts/prof_summary.py "$OUT/prof" > "$OUT/kernel_summary.txt" 2>&1
+  find "$OUT/prof" -name '*kernel_stats.csv' -exec cp {} "$OUT/kernel_stats.csv" \;
 fi
 if [[ $ST == *m* && $rc == 0 ]]; then
   timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$HEAD_RE" -f csv -d "$OUT/pmc_fetch" -o run -- $PB > "$OUT/pmc_fetch.log" 2>&1; rc=$?

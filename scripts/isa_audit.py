@@ -103,18 +103,32 @@ def spill_meta(path):
 
 
 def loop_scratch(body):
-    """Scratch (spill) instructions inside a loop: between a label and a later branch back to it."""
+    """Scratch (spill) instructions inside a loop (between a label and a later branch back to it), and how many of
+    those sit in an innermost loop that issues MFMAs (the K-tile / q-tile loops, where a reload's vmcnt(0) drains the
+    DMA ring)."""
     labels = {}
     for i, (kind, text) in enumerate(body):
         if kind == 'label':
-            labels[text.rstrip(':').split()[0]] = i
+            labels[text.split(':')[0].strip()] = i
     ranges = []
     for i, (kind, text) in enumerate(body):
         m = re.match(r'^s_c?branch\w*\s+(\.LBB\w+)', text) if kind == 'ins' else None
         if m and m.group(1) in labels and labels[m.group(1)] < i:
             ranges.append((labels[m.group(1)], i))
-    return sum(1 for i, (kind, text) in enumerate(body) if kind == 'ins' and text.startswith('scratch_')
-               and any(a <= i <= b for a, b in ranges))
+    mfma = [i for i, (kind, text) in enumerate(body) if kind == 'ins' and text.startswith('v_mfma')]
+    inloop = inner = 0
+    for i, (kind, text) in enumerate(body):
+        if kind != 'ins' or not text.startswith('scratch_'):
+            continue
+        enc = [(a, b) for a, b in ranges if a <= i <= b]
+        if not enc:
+            continue
+        inloop += 1
+        a, b = min(enc, key=lambda r: r[1] - r[0])      # the innermost loop holding this spill
+        # ... with MFMAs on both sides of the spill inside that loop: the spill sits in the MFMA stream of a K-tile /
+        # q-tile loop (an epilogue spill of a persistent tile loop has the loop's MFMAs only before it)
+        inner += any(a <= j < i for j in mfma) and any(i < j <= b for j in mfma)
+    return inloop, inner
 
 
 def audit_kernel(name, body):
@@ -194,12 +208,12 @@ def main():
             ndma = sum(1 for k, t in body if k == 'ins' and t.endswith(' lds'))
             if issues:
                 bad += len(issues)
-            inloop = loop_scratch(body)
+            inloop, inner = loop_scratch(body)
             report[name] = dict(dma=ndma, vgpr=vg, vgpr_spill=vsp, sgpr_spill=ssp, scratch=scratch,
-                                scratch_in_loops=inloop, hazards=len(issues))
+                                scratch_in_loops=inloop, scratch_in_mfma_loops=inner, hazards=len(issues))
             if issues or not args.quiet and (ndma or vsp > 0 or ssp > 0):
                 print(f'{os.path.basename(f)} {name}: {ndma} LDS-DMA, vgpr {vg}, spills v{vsp}/s{ssp}, '
-                      f'{scratch} scratch instructions ({inloop} inside loops)')
+                      f'{scratch} scratch instructions ({inloop} inside loops, {inner} in an MFMA loop)')
             for kind, i, text in issues:
                 print(f'    {kind} @{i}: {text}')
     print(f'{bad} hazard(s)')

@@ -241,6 +241,7 @@ __global__ __launch_bounds__(256) void ce_prob_rows_kernel(const float* __restri
 // logit = hh . W[col] + bias[col] over the whole vocabulary (bf16 operands, f32 accumulation, as the GEMM), m = the
 // row maximum; P[row] = exp(logit - m) (bf16), lse = m + log sum, row_loss = lse - c (c = the label logit, the old
 // offset), and the offset becomes m, so the backward's r = q exp(off - lse) stays consistent with the new P.
+constexpr int CE_FIX_MAX_ROWS = 1024;
 __global__ __launch_bounds__(256) void ce_prob_fixup_kernel(const int* __restrict__ sat, const bf16* __restrict__ hh,
                                                             long long ldh, const bf16* __restrict__ W, long long ldw,
                                                             const float* __restrict__ bias, bf16* __restrict__ P,
@@ -248,7 +249,11 @@ __global__ __launch_bounds__(256) void ce_prob_fixup_kernel(const int* __restric
                                                             float* __restrict__ lse, float* __restrict__ row_loss) {
   __shared__ float h[1024];
   __shared__ float red[4];
-  const int n = sat[0];
+  // bounded: at most CE_FIX_MAX_ROWS rows are recomputed (each costs 2 V D MACs on one block: ~0.3 ms at
+  // V = 32768, D = 512, so the cap bounds the fix-up at ~16 rounds of the 64-block grid, ~5 ms). A step that saturates
+  // more rows is diverging: the rows past the cap keep their overflowed P (an infinite loss surfaces it) and sat[0]
+  // still counts every flagged row (out['ce_saturated']).
+  const int n = min(sat[0], CE_FIX_MAX_ROWS);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   for (int i = blockIdx.x; i < n; i += gridDim.x) {
     const int row = sat[1 + i];

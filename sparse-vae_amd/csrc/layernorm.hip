@@ -402,6 +402,8 @@ SVAE_EXPORT int svae_resid_ln_fwd(const float* x, const void* y, int32_t y_dtype
     return SVAE_EINVAL;
   if ((w == nullptr) != (b == nullptr) || (w && (!mean || !rstd)) || (zrows && zmod <= 0)) return SVAE_EINVAL;
   if (drop_p < 0.f || drop_p >= 1.f || (y && ldy % 8) || (((uintptr_t)y | (uintptr_t)h) & 15)) return SVAE_EINVAL;
+  // x, xo, zrows, w, b are read / written as f32x4 rows of stride D: 16-byte aligned
+  if (((uintptr_t)x | (uintptr_t)xo | (uintptr_t)zrows | (uintptr_t)w | (uintptr_t)b) & 15) return SVAE_EINVAL;
   dim3 grid((rows + 3) / 4);
   hipStream_t s = (hipStream_t)stream;
 #define SVAE_RLN(NR, CPL, TY)                                                                                     \

@@ -154,6 +154,9 @@ def resid_ln_fwd(x, y, h, rows, D, *, w=None, b=None, mean=None, rstd=None, xo=N
     without w / b)."""
     _dev(h, *(t for t in (x, y, xo, zrows, w, b, mean, rstd) if t is not None))
     assert h.dtype == bf16 and (y is None or y.dtype in (bf16, f32)) and (x is None or x.dtype == f32)
+    # the kernel walks x / xo / zrows / h as dense rows of D elements (y has its own leading dimension)
+    for t in (x, xo, zrows, h, w, b):
+        assert t is None or t.is_contiguous(), 'resid_ln_fwd: x, xo, zrows, h, w, b must be contiguous'
     check(lib.svae_resid_ln_fwd(ptr(x), ptr(y), 1 if y is not None and y.dtype == bf16 else 0,
                                 y.stride(0) if y is not None else 0, float(drop_p), int(seed) & (2 ** 64 - 1),
                                 ptr(zrows), int(zmod), ptr(w), ptr(b), ptr(xo), h.data_ptr(), ptr(mean), ptr(rstd), rows,

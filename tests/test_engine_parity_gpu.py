@@ -158,6 +158,22 @@ def test_mutual_info_matches_oracle(name):
     assert abs(mi - float(g['mutual_info'])) < 2e-2 * max(1.0, abs(float(g['mutual_info']))), (mi, g['mutual_info'])
 
 
+def test_marginal_kl_public_api_matches_oracle():
+    """sparse_vae.marginal_kl (the reference's math_utils.marginal_kl signature: a Normal posterior) runs the fused
+    kernel pair; with the fixture's draws injected it matches the oracle's marginal_kl within 1e-4."""
+    from torch.distributions.normal import Normal
+    from sparse_vae import marginal_kl
+    g, hp, params, ids = setup('small6_pad')
+    eps10 = torch.from_numpy(g['eps10'])
+    B = eps10.shape[1]
+    gen = torch.Generator().manual_seed(4)
+    mu = torch.randn(B, 1, 64, generator=gen, dtype=torch.float64) * 0.5
+    scale = torch.rand(B, 1, 64, generator=gen, dtype=torch.float64) * 0.8 + 0.2
+    got = marginal_kl(Normal(mu.float().cuda(), scale.float().cuda()), 10, eps=eps10.cuda()).item()
+    want = oracle.marginal_kl(mu, scale, eps10.double()).item()
+    assert abs(got - want) < 1e-4 * max(1.0, abs(want)), (got, want)
+
+
 def test_mutual_info_in_kernel_draws():
     """eps=None draws the 10 x B x Z normals in-kernel (counter-based Box-Muller). The estimator's mean over 300
     seeds matches the mean over 300 torch.randn draws through the oracle within 6 standard errors."""
