@@ -256,7 +256,10 @@ def main():
         # launcher: this process never touches the GPU; it checks the device count in a child and starts one
         # rank per GPU
         n = device_count_in_child()
-        if n < args.gpus:
+        # SVAE_BENCH_SHARE_GPUS=1 (rehearsal only, never a bench number): ranks share the visible GPUs round-robin,
+        # so the N-rank launch path runs end to end on a 1-GPU box (with SVAE_DIST_BACKEND=gloo)
+        share = os.environ.get('SVAE_BENCH_SHARE_GPUS') == '1'
+        if n < args.gpus and not (share and n >= 1):
             print(f'bench.py: --gpus {args.gpus} needs {args.gpus} visible GPUs, this node has {n}',
                   file=sys.stderr, flush=True)
             sys.exit(3)
@@ -267,10 +270,17 @@ def main():
         print(f'bench.py: WORLD_SIZE={world} overrides --gpus {args.gpus}', file=sys.stderr, flush=True)
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
+    if os.environ.get('SVAE_BENCH_SHARE_GPUS') == '1':
+        local %= torch.cuda.device_count()
     torch.cuda.set_device(local)
     device = torch.device('cuda', local)
     if world > 1:
-        dist.init_process_group('nccl', device_id=device)
+        # 'nccl' is RCCL on ROCm (the product path); SVAE_DIST_BACKEND=gloo only for the shared-GPU rehearsal
+        backend = os.environ.get('SVAE_DIST_BACKEND', 'nccl')
+        if backend == 'nccl':
+            dist.init_process_group('nccl', device_id=device)
+        else:
+            dist.init_process_group(backend)
     cfg_name = args.config or 'c2'
     cfg = CONFIGS[cfg_name]
 
@@ -361,6 +371,9 @@ def main():
         }
         if scaling is not None:
             res['scaling_efficiency'] = scaling
+        if os.environ.get('SVAE_BENCH_SHARE_GPUS') == '1':
+            res['rehearsal'] = (f'NOT a measurement: {world} ranks share {torch.cuda.device_count()} GPU(s), backend '
+                                f'{os.environ.get("SVAE_DIST_BACKEND", "nccl")}')
         if world == 1 and not args.no_parity:
             try:
                 res['parity'] = parity_check(cfg, device)

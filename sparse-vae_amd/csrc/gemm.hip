@@ -1422,7 +1422,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GP p) {
 // reads that operand ("a" / "b" = the wave's first / second two pieces). Schedule (j = K-tile; a wait retires
 // pieces at the start of its R segment; a piece is read one phase after the wait that retires it -- the two wave
 // rows are a barrier apart -- and re-filled one phase after its last read, whose lgkmcnt(0) precedes the barrier):
-//   FF (forward):        R0: A0[j+2]  R1: B0[j+2]  R2: B1[j+2]  R3: A2[j+2]    waits 10 10 10 10
+//   FF (forward):        R0: A2[j+1]  R1: A0[j+2]  R2: B0[j+2]  R3: B1[j+2]    waits 8 8 8 8 (lgkmcnt after the barrier)
 //   FT (dX, b_t):        R0: Bb[j+1]  R1: A2[j+1]  R2: Ba[j+2]  R3: A0[j+2]    waits - 6 4 4
 //   TT (dW, a_t b_t):    R0: Ab[j+1]  R1: Bb[j+1]  R2: Ba[j+2]  R3: Aa[j+2]    waits - - 2 2
 // Every piece flies 2-5 phases. Pieces of K-tiles past a tile's last belong to the block's next tile (its first two
@@ -1434,11 +1434,14 @@ template <bool AT, bool BT>
 struct G8 {
   static constexpr int LAY = AT ? 2 : (BT ? 1 : 0);   // TT / FT / FF
   // wait count at the start of R_q (-1: none), and whether it spans the epilogue at a tile's first K-tile
-  static constexpr int W[4] = {LAY == 0 ? 10 : -1, LAY == 0 ? 10 : (LAY == 1 ? 6 : -1), LAY == 2 ? 2 : (LAY == 0 ? 10 : 4),
-                               LAY == 2 ? 2 : (LAY == 0 ? 10 : 4)};
-  static constexpr bool SPAN[4] = {LAY == 0, LAY <= 1, LAY <= 1, LAY == 0};
-  // FF: the waits of K-tile 1's phases 0 and 1 also span the epilogue (their pieces flew since K-tile nk - 2)
-  static constexpr bool SPAN1[4] = {LAY == 0, LAY == 0, false, false};
+  static constexpr int W[4] = {LAY == 0 ? 8 : -1, LAY == 0 ? 8 : (LAY == 1 ? 6 : -1), LAY == 2 ? 2 : (LAY == 0 ? 8 : 4),
+                               LAY == 2 ? 2 : (LAY == 0 ? 8 : 4)};
+  static constexpr bool SPAN[4] = {LAY <= 1, LAY <= 1, LAY <= 1, LAY == 0};
+  // FF: the wait of K-tile 1's phase 0 also spans the epilogue (its piece flew since K-tile nk - 1)
+  static constexpr bool SPAN1[4] = {LAY == 0, false, false, false};
+  // FF: fragment reads are waited for after the barrier that ends their R segment (a region is re-filled >= 2
+  // phases after its last read); FT / TT wait before it (re-filled 1 phase after)
+  static constexpr bool LGKM_LATE = LAY == 0;
 };
 
 // A K-contiguous operand piece (8 rows x 128 B of a 256-row K-tile) into dst + piece * 1024
@@ -1491,8 +1494,26 @@ __device__ __forceinline__ void gemm256_run8(const GP& p, int blk, int nwg) {
   const int pb1[2] = {pb0[0] + 4, pb0[1] + 4};
   const int pma[2] = {4 * wave, 4 * wave + 1}, pmb[2] = {4 * wave + 2, 4 * wave + 3};
   // 2 pieces of A / B of K-tile kt of tile X into `stage`
+  // K-contiguous pieces of interior K-tiles (all 256 rows inside, no K tail): the lane part of the source offset
+  // depends only on the piece's parity (the swizzle sees row bits 1-3) and is computed once; the piece's row offset
+  // goes in as the scalar soffset. Edge tiles and the K tail take the exact per-lane path (g8_issue_k).
+  int voffA[2], voffB[2];
+#pragma unroll
+  for (int par = 0; par < 2; ++par) {
+    const int rl = lane >> 3, c = (lane & 7) ^ ((par * 4 + (rl >> 1)) & 7);
+    voffA[par] = (rl * (int)p.lda + c * 8) * 2;
+    voffB[par] = (rl * (int)p.ldb + c * 8) * 2;
+  }
   auto issueA = [&](const G3Tile& X, int kt, char* stage, const int (&pc)[2]) {
     const int k0 = X.kbeg + kt * 64;
+    if constexpr (!AT) {
+      if (p.M - X.m0 >= 256 && X.kend - k0 >= 64) {
+        const u32x4 rs = buffer_rsrc(X.A + (long long)X.m0 * p.lda + k0, 0x7FFFFFF0u);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) dma16_lds_so(rs, stage + pc[i] * 1024, voffA[pc[i] & 1], pc[i] * 16 * (int)p.lda);
+        return;
+      }
+    }
     if constexpr (AT) {
       const bf16* base = X.A + (long long)k0 * p.lda + X.m0;
 #pragma unroll
@@ -1505,6 +1526,15 @@ __device__ __forceinline__ void gemm256_run8(const GP& p, int blk, int nwg) {
   };
   auto issueB = [&](const G3Tile& X, int kt, char* stage, const int (&pc)[2]) {
     const int k0 = X.kbeg + kt * 64;
+    if constexpr (!BT) {
+      if (p.N - X.n0 >= 256 && X.kend - k0 >= 64) {
+        const u32x4 rs = buffer_rsrc(X.B + (long long)X.n0 * p.ldb + k0, 0x7FFFFFF0u);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+          dma16_lds_so(rs, stage + G3_T + pc[i] * 1024, voffB[pc[i] & 1], pc[i] * 16 * (int)p.ldb);
+        return;
+      }
+    }
     if constexpr (BT) {
       const bf16* base = X.B + (long long)k0 * p.ldb + X.n0;
 #pragma unroll
@@ -1522,8 +1552,8 @@ __device__ __forceinline__ void gemm256_run8(const GP& p, int blk, int nwg) {
     char* s1 = smem + G3_STAGE;
     if constexpr (S::LAY == 0) {
       issueA(T, 0, s0, pa0); issueB(T, 0, s0, pb0); issueB(T, 0, s0, pb1); issueA(T, 0, s0, pa2);
-      issueA(T, 1, s1, pa0); issueB(T, 1, s1, pb0); issueB(T, 1, s1, pb1); issueA(T, 1, s1, pa2);
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      issueA(T, 1, s1, pa0); issueB(T, 1, s1, pb0); issueB(T, 1, s1, pb1);
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
     } else if constexpr (S::LAY == 1) {
       issueB(T, 0, s0, pma); issueA(T, 0, s0, pa0); issueB(T, 0, s0, pmb); issueA(T, 0, s0, pa2);
       issueB(T, 1, s1, pma); issueA(T, 1, s1, pa0);
@@ -1571,7 +1601,11 @@ __device__ __forceinline__ void gemm256_run8(const GP& p, int blk, int nwg) {
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) a0[i][ks] = g3_afrag<AT>(la, wr * 128 + i * 16, ks, lane);
     }
+    // every wave's a0 reads done before any wave's R0 issues the A0 pieces of K-tile 2 into the same region (without
+    // this barrier a wave that ran ahead overwrote rows its neighbours had not read yet: wrong 16-row groups in 1 of
+    // ~2 launches with two tiles per block)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
     if (wr == 1) __builtin_amdgcn_s_barrier();   // the stagger: wave row 1 runs one barrier behind
     __builtin_amdgcn_sched_barrier(0);
 
@@ -1591,16 +1625,17 @@ __device__ __forceinline__ void gemm256_run8(const GP& p, int blk, int nwg) {
         if (tail) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         else if ((span && S::SPAN[q]) || (span1 && S::SPAN1[q])) {
           if (S::W[q] == 4) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 + G3_EPI_STORES) : "memory");
-          else if (S::W[q] == 10) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(10 + G3_EPI_STORES) : "memory");
+          else if (S::W[q] == 8) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(8 + G3_EPI_STORES) : "memory");
           else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(6 + G3_EPI_STORES) : "memory");
-        } else if (S::W[q] == 10) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+        } else if (S::W[q] == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
         else if (S::W[q] == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
         else if (S::W[q] == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
         else if (S::W[q] == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
       };
       auto mfma_seg = [&]() {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if constexpr (!S::LGKM_LATE) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
+        if constexpr (S::LGKM_LATE) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
       };
       auto end_seg = [&]() {
@@ -1621,7 +1656,7 @@ __device__ __forceinline__ void gemm256_run8(const GP& p, int blk, int nwg) {
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) b0[j][ks] = g3_bfrag<BT>(lb, wc * 64 + j * 16, ks, lane);
       if constexpr (S::LAY == 0) {
-        if (ok2) issueA(X2, k2, s2, pa0);
+        if (ok1) issueA(X1, k1, s1, pa2);
       } else if (ok1) {
         if constexpr (S::LAY == 1) issueB(X1, k1, s1, pmb);
         else issueA(X1, k1, s1, pmb);
@@ -1643,7 +1678,7 @@ __device__ __forceinline__ void gemm256_run8(const GP& p, int blk, int nwg) {
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) b1[j][ks] = g3_bfrag<BT>(lb, wc * 64 + 32 + j * 16, ks, lane);
       if constexpr (S::LAY == 0) {
-        if (ok2) issueB(X2, k2, s2, pb0);
+        if (ok2) issueA(X2, k2, s2, pa0);
       } else if (ok1) {
         if constexpr (S::LAY == 1) issueA(X1, k1, s1, pa2);
         else issueB(X1, k1, s1, pmb);
@@ -1671,7 +1706,7 @@ __device__ __forceinline__ void gemm256_run8(const GP& p, int blk, int nwg) {
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) a1[i][ks] = g3_afrag<AT>(la, wr * 128 + 64 + i * 16, ks, lane);
       if constexpr (S::LAY == 0) {
-        if (ok2) issueB(X2, k2, s2, pb1);
+        if (ok2) issueB(X2, k2, s2, pb0);
       } else {
         if (ok2) issueB(X2, k2, s2, pma);
       }
@@ -1696,7 +1731,7 @@ __device__ __forceinline__ void gemm256_run8(const GP& p, int blk, int nwg) {
       if (ok2) {
         if constexpr (S::LAY == 2) issueA(X2, k2, s2, pma);
         else if constexpr (S::LAY == 1) issueA(X2, k2, s2, pa0);
-        else issueA(X2, k2, s2, pa2);
+        else issueB(X2, k2, s2, pb1);
       }
       mfma_seg();
       __builtin_amdgcn_s_setprio(1);
