@@ -86,19 +86,6 @@ __device__ __forceinline__ void dma16_lds(const u32x4& rsrc, const void* lds_bas
                : "memory");
 }
 
-// dma16_lds with a scalar byte offset added to every lane's voff (soffset; not part of the buffer range check, so
-// the caller keeps the whole access inside the buffer or uses dma16_lds).
-__device__ __forceinline__ void dma16_lds_so(const u32x4& rsrc, const void* lds_base, int voff, int soff) {
-  const int m = __builtin_amdgcn_readfirstlane((int)(unsigned)(uintptr_t)lds_base);
-  const int so = __builtin_amdgcn_readfirstlane(soff);
-  unsigned keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_nop 1\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dwordx4 %2, %3, %4 offen lds\n\t"
-               "s_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "s"(m), "v"(voff), "s"(rsrc), "s"(so)
-               : "memory");
-}
-
 // 4 B per lane (buffer_load_dword ... lds) into lds_base + 4 * lane, same conventions as dma16_lds.
 __device__ __forceinline__ void dma4_lds(const u32x4& rsrc, const void* lds_base, int voff) {
   const int m = __builtin_amdgcn_readfirstlane((int)(unsigned)(uintptr_t)lds_base);

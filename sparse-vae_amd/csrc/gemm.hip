@@ -1405,393 +1405,6 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(GP p) {
   gemm256_run<AT, BT, EPI>(p, blockIdx.x, gridDim.x);
 }
 
-// ===================================================================================================
-// gemm256 with the 8-phase K-loop. Same tile, LDS image, fragment reads and epilogues as gemm256_run; what changes
-// is the schedule inside a K-tile. A K-tile is 4 phases, one per C-quadrant Q0..Q3 of the wave's 128 x 64 output
-// (16 MFMAs each). A phase is two segments separated by raw barriers: R (a counted vmcnt wait, the LDS fragment
-// reads the next MFMA segment needs, 2 LDS-DMA pieces of a later K-tile, lgkmcnt(0)) and M (the 16 MFMAs). The
-// wave-row-1 waves run one barrier behind the wave-row-0 waves, so on every SIMD (one wave of each row) one wave's R
-// segment runs beside the other wave's MFMAs: the MFMA pipe does not wait for fragment reads or DMA issue
-// (cdna_hip_programming.md, "The 256² 8-phase template").
-//
-// Reads per phase: R0 b0 (B cols wc*64 + 0..31), R1 b1 (+32..63), R2 a1 (A rows wr*128 + 64..127), R3 a0 of the
-// NEXT K-tile (rows wr*128 + 0..63); Q0 = a0 x b0, Q1 = a0 x b1, Q2 = a1 x b1, Q3 = a1 x b0.
-// DMA pieces (1 KiB, 8 per wave per K-tile) go out grouped by the phase that first reads them. A K-contiguous
-// operand piece is 8 rows: A "A0" (a0 rows) / "A2" (a1 rows), B "B0" (b0 cols) / "B1" (b1 cols); an MN-contiguous
-// piece (a_t / b_t) holds 4 k-rows of a whole 128-wide half, so it is read from the first to the last phase that
-// reads that operand ("a" / "b" = the wave's first / second two pieces). Schedule (j = K-tile; a wait retires
-// pieces at the start of its R segment; a piece is read one phase after the wait that retires it -- the two wave
-// rows are a barrier apart -- and re-filled one phase after its last read, whose lgkmcnt(0) precedes the barrier):
-//   FF (forward):        R0: A2[j+1]  R1: A0[j+2]  R2: B0[j+2]  R3: B1[j+2]    waits 8 8 8 8 (lgkmcnt after the barrier)
-//   FT (dX, b_t):        R0: Bb[j+1]  R1: A2[j+1]  R2: Ba[j+2]  R3: A0[j+2]    waits - 6 4 4
-//   TT (dW, a_t b_t):    R0: Ab[j+1]  R1: Bb[j+1]  R2: Ba[j+2]  R3: Aa[j+2]    waits - - 2 2
-// Every piece flies 2-5 phases. Pieces of K-tiles past a tile's last belong to the block's next tile (its first two
-// K-tiles fly under this tile's epilogue); a wait that spans the epilogue (the first K-tile of a tile) adds the
-// epilogue's G3_EPI_STORES stores. The block's last two K-tiles wait vmcnt(0) (nothing follows). Bias row sums (a_t,
-// p.a_rowsum) run in R segments: the a0 groups in R2, the a1 groups in the next K-tile's R0. Requires >= 2 K-tiles
-// in every tile (host-checked) and a register epilogue.
-template <bool AT, bool BT>
-struct G8 {
-  static constexpr int LAY = AT ? 2 : (BT ? 1 : 0);   // TT / FT / FF
-  // wait count at the start of R_q (-1: none), and whether it spans the epilogue at a tile's first K-tile
-  static constexpr int W[4] = {LAY == 0 ? 8 : -1, LAY == 0 ? 8 : (LAY == 1 ? 6 : -1), LAY == 2 ? 2 : (LAY == 0 ? 8 : 4),
-                               LAY == 2 ? 2 : (LAY == 0 ? 8 : 4)};
-  static constexpr bool SPAN[4] = {LAY <= 1, LAY <= 1, LAY <= 1, LAY == 0};
-  // FF: the wait of K-tile 1's phase 0 also spans the epilogue (its piece flew since K-tile nk - 1)
-  static constexpr bool SPAN1[4] = {LAY == 0, false, false, false};
-  // FF: fragment reads are waited for after the barrier that ends their R segment (a region is re-filled >= 2
-  // phases after its last read); FT / TT wait before it (re-filled 1 phase after)
-  static constexpr bool LGKM_LATE = LAY == 0;
-};
-
-// A K-contiguous operand piece (8 rows x 128 B of a 256-row K-tile) into dst + piece * 1024
-__device__ __forceinline__ void g8_issue_k(const bf16* base, long long ld, int rows_left, int krem, int piece,
-                                           char* dst) {
-  const int lane = lane_id_fresh();
-  const int r = piece * 8 + (lane >> 3), c = (lane & 7) ^ ((r >> 1) & 7);
-  const int off = (r < rows_left && (krem >= 64 || c * 8 < krem)) ? (r * (int)ld + c * 8) * 2 : 0x7FFFFFF0;
-  dma16_lds(buffer_rsrc(base, 0x7FFFFFF0u), dst + piece * 1024, off);
-}
-// An MN-contiguous operand piece (4 k-rows x 256 B of one [64][128] half) into dst + piece * 1024
-__device__ __forceinline__ void g8_issue_mn(const bf16* base, long long ld, int cols_left, int krem, int piece,
-                                            char* dst) {
-  const int lane = lane_id_fresh();
-  const int half = piece >> 4;
-  const int kr = (piece & 15) * 4 + (lane >> 4);
-  const int sk = (kr & 3) | (((kr >> 3) & 1) << 2);
-  const int col = half * 128 + (((lane & 15) ^ (sk << 1)) * 8);
-  const int off = (col < cols_left && kr < krem) ? (kr * (int)ld + col) * 2 : 0x7FFFFFF0;
-  dma16_lds(buffer_rsrc(base, 0x7FFFFFF0u), dst + piece * 1024, off);
-}
-
-template <bool AT, bool BT, int EPI>
-__device__ __forceinline__ void gemm256_run8(const GP& p, int blk, int nwg) {
-  static_assert(EPI != SVAE_EPI_F32_ATOMIC && EPI != G3_EPI_ACC_KW, "register epilogues without k-weights only");
-  static_assert(g3_epi_vmem_ops<EPI>() >= G3_EPI_STORES, "the epilogue-spanning waits would not cover the DMA");
-  static_assert(!AT || BT, "a_t needs b_t here");
-  using S = G8<AT, BT>;
-  __shared__ __attribute__((aligned(16))) char smem[2 * G3_STAGE + 2048 + 8192];
-  float* sbias = (float*)(smem + 2 * G3_STAGE);
-  int* slabel = (int*)(smem + 2 * G3_STAGE + 1024);
-  float* sstat = (float*)(smem + 2 * G3_STAGE + 2048);
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wave >> 2, wc = wave & 3;
-  int bid = blk;
-  if (nwg >= 16) {
-    const int q = nwg / 8, r = nwg % 8, xcd = bid % 8, idx = bid / 8;
-    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
-  }
-  int t3 = bid;
-  if (t3 >= p.total3) return;
-  G3Tile T = g3_tile(p, t3);
-  // this wave's pieces. K-contiguous A: A0 / A2 (2 each); K-contiguous B: B0 / B1 (2 each); MN-contiguous: pieces
-  // 4 wave .. 4 wave + 3, the first two "a", the last two "b"
-  const int j0 = 2 * wave, j1 = 2 * wave + 1;
-  const int pa0[2] = {j0 < 8 ? j0 : j0 + 8, j1 < 8 ? j1 : j1 + 8};
-  const int pa2[2] = {pa0[0] + 8, pa0[1] + 8};
-  const int pb0[2] = {(j0 >> 2) * 8 + (j0 & 3), (j1 >> 2) * 8 + (j1 & 3)};
-  const int pb1[2] = {pb0[0] + 4, pb0[1] + 4};
-  const int pma[2] = {4 * wave, 4 * wave + 1}, pmb[2] = {4 * wave + 2, 4 * wave + 3};
-  // 2 pieces of A / B of K-tile kt of tile X into `stage`
-  // K-contiguous pieces of interior K-tiles (all 256 rows inside, no K tail): the lane part of the source offset
-  // depends only on the piece's parity (the swizzle sees row bits 1-3) and is computed once; the piece's row offset
-  // goes in as the scalar soffset. Edge tiles and the K tail take the exact per-lane path (g8_issue_k).
-  int voffA[2], voffB[2];
-#pragma unroll
-  for (int par = 0; par < 2; ++par) {
-    const int rl = lane >> 3, c = (lane & 7) ^ ((par * 4 + (rl >> 1)) & 7);
-    voffA[par] = (rl * (int)p.lda + c * 8) * 2;
-    voffB[par] = (rl * (int)p.ldb + c * 8) * 2;
-  }
-  auto issueA = [&](const G3Tile& X, int kt, char* stage, const int (&pc)[2]) {
-    const int k0 = X.kbeg + kt * 64;
-    if constexpr (!AT) {
-      if (p.M - X.m0 >= 256 && X.kend - k0 >= 64) {
-        const u32x4 rs = buffer_rsrc(X.A + (long long)X.m0 * p.lda + k0, 0x7FFFFFF0u);
-#pragma unroll
-        for (int i = 0; i < 2; ++i) dma16_lds_so(rs, stage + pc[i] * 1024, voffA[pc[i] & 1], pc[i] * 16 * (int)p.lda);
-        return;
-      }
-    }
-    if constexpr (AT) {
-      const bf16* base = X.A + (long long)k0 * p.lda + X.m0;
-#pragma unroll
-      for (int i = 0; i < 2; ++i) g8_issue_mn(base, p.lda, p.M - X.m0, X.kend - k0, pc[i], stage);
-    } else {
-      const bf16* base = X.A + (long long)X.m0 * p.lda + k0;
-#pragma unroll
-      for (int i = 0; i < 2; ++i) g8_issue_k(base, p.lda, p.M - X.m0, X.kend - k0, pc[i], stage);
-    }
-  };
-  auto issueB = [&](const G3Tile& X, int kt, char* stage, const int (&pc)[2]) {
-    const int k0 = X.kbeg + kt * 64;
-    if constexpr (!BT) {
-      if (p.N - X.n0 >= 256 && X.kend - k0 >= 64) {
-        const u32x4 rs = buffer_rsrc(X.B + (long long)X.n0 * p.ldb + k0, 0x7FFFFFF0u);
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-          dma16_lds_so(rs, stage + G3_T + pc[i] * 1024, voffB[pc[i] & 1], pc[i] * 16 * (int)p.ldb);
-        return;
-      }
-    }
-    if constexpr (BT) {
-      const bf16* base = X.B + (long long)k0 * p.ldb + X.n0;
-#pragma unroll
-      for (int i = 0; i < 2; ++i) g8_issue_mn(base, p.ldb, p.N - X.n0, X.kend - k0, pc[i], stage + G3_T);
-    } else {
-      const bf16* base = X.B + (long long)X.n0 * p.ldb + k0;
-#pragma unroll
-      for (int i = 0; i < 2; ++i) g8_issue_k(base, p.ldb, p.N - X.n0, X.kend - k0, pc[i], stage + G3_T);
-    }
-  };
-
-  int g = 0;   // K-tiles consumed by this block: K-tile g lives in stage g & 1
-  {  // prologue: K-tile 0 whole and the early pieces of K-tile 1 (what the steady state issues during K-tile -1)
-    char* s0 = smem;
-    char* s1 = smem + G3_STAGE;
-    if constexpr (S::LAY == 0) {
-      issueA(T, 0, s0, pa0); issueB(T, 0, s0, pb0); issueB(T, 0, s0, pb1); issueA(T, 0, s0, pa2);
-      issueA(T, 1, s1, pa0); issueB(T, 1, s1, pb0); issueB(T, 1, s1, pb1);
-      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    } else if constexpr (S::LAY == 1) {
-      issueB(T, 0, s0, pma); issueA(T, 0, s0, pa0); issueB(T, 0, s0, pmb); issueA(T, 0, s0, pa2);
-      issueB(T, 1, s1, pma); issueA(T, 1, s1, pa0);
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    } else {
-      issueB(T, 0, s0, pma); issueA(T, 0, s0, pma); issueA(T, 0, s0, pmb); issueB(T, 0, s0, pmb);
-      issueB(T, 1, s1, pma); issueA(T, 1, s1, pma);
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();
-  }
-  bool relaxed = false;
-  while (true) {
-    const int t3n = t3 + nwg;
-    const bool has_next = t3n < p.total3;
-    G3Tile TN = T;
-    if (has_next) TN = g3_tile(p, t3n);
-    const int nk = T.nk;
-    const bool do_rs = AT && p.a_rowsum && T.bn < 2;
-    const int ks0 = p.tn2 >= 2 ? T.bn : 0, ks1 = p.tn2 >= 2 ? T.bn + 1 : 2;
-    float rsum[4] = {0.f, 0.f, 0.f, 0.f};
-    // bias row sums sum_k A[m][k] from fragments in registers (rows 16 i + (l & 15), k = 32 ks + 8 (l >> 4) + 0..7);
-    // blocks bn = 0, 1 (the same A rows) split the k-steps
-    auto rowsum2 = [&](const bf16x8 (&x)[2], const bf16x8 (&y)[2]) {
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        if (ks < ks0 || ks >= ks1) continue;   // (block-uniform)
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          rsum[0] += (float)x[ks][e];
-          rsum[1] += (float)y[ks][e];
-        }
-      }
-    };
-    f32x4 acc[8][4];
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    bf16x8 a0[4][2], a1[4][2], b0[2][2], b1[2][2];
-    {  // a0 of K-tile 0 (landed: retired before the last barrier)
-      const char* la = smem + (g & 1) * G3_STAGE;
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) a0[i][ks] = g3_afrag<AT>(la, wr * 128 + i * 16, ks, lane);
-    }
-    // every wave's a0 reads done before any wave's R0 issues the A0 pieces of K-tile 2 into the same region (without
-    // this barrier a wave that ran ahead overwrote rows its neighbours had not read yet: wrong 16-row groups in 1 of
-    // ~2 launches with two tiles per block)
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if (wr == 1) __builtin_amdgcn_s_barrier();   // the stagger: wave row 1 runs one barrier behind
-    __builtin_amdgcn_sched_barrier(0);
-
-    for (int kt = 0; kt < nk; ++kt, ++g) {
-      const char* la = smem + (g & 1) * G3_STAGE;
-      const char* lb = la + G3_T;
-      char* s1 = smem + ((g + 1) & 1) * G3_STAGE;   // stage of K-tile g + 1
-      char* s2 = smem + (g & 1) * G3_STAGE;         // stage of K-tile g + 2
-      const bool tail = !has_next && kt >= nk - 2;
-      const bool span = relaxed && kt == 0, span1 = relaxed && kt == 1;
-      // targets: K-tile kt + 1 and kt + 2 of this tile, else of the next tile (every tile has >= 2 K-tiles)
-      const bool ok1 = kt + 1 < nk || has_next, ok2 = kt + 2 < nk || has_next;
-      const G3Tile& X1 = kt + 1 < nk ? T : TN;
-      const G3Tile& X2 = kt + 2 < nk ? T : TN;
-      const int k1 = kt + 1 < nk ? kt + 1 : kt + 1 - nk, k2 = kt + 2 < nk ? kt + 2 : kt + 2 - nk;
-      auto wait = [&](int q) {
-        if (tail) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        else if ((span && S::SPAN[q]) || (span1 && S::SPAN1[q])) {
-          if (S::W[q] == 4) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 + G3_EPI_STORES) : "memory");
-          else if (S::W[q] == 8) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(8 + G3_EPI_STORES) : "memory");
-          else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(6 + G3_EPI_STORES) : "memory");
-        } else if (S::W[q] == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        else if (S::W[q] == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        else if (S::W[q] == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-        else if (S::W[q] == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-      };
-      auto mfma_seg = [&]() {
-        if constexpr (!S::LGKM_LATE) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        if constexpr (S::LGKM_LATE) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
-      };
-      auto end_seg = [&]() {
-        __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_sched_barrier(0);
-      };
-      // ---- phase 0: R0 reads b0, M0 = Q0 (a0 x b0)
-      wait(0);
-      if constexpr (AT) {   // the a1 row sums of the previous K-tile (its a1 lives until this K-tile's R2)
-        if (do_rs && kt > 0) {
-          if (wc == 2) rowsum2(a1[0], a1[1]);
-          else if (wc == 3) rowsum2(a1[2], a1[3]);
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) b0[j][ks] = g3_bfrag<BT>(lb, wc * 64 + j * 16, ks, lane);
-      if constexpr (S::LAY == 0) {
-        if (ok1) issueA(X1, k1, s1, pa2);
-      } else if (ok1) {
-        if constexpr (S::LAY == 1) issueB(X1, k1, s1, pmb);
-        else issueA(X1, k1, s1, pmb);
-      }
-      mfma_seg();
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j) acc[i][j] = mfma16(b0[j][ks], a0[i][ks], acc[i][j]);
-      __builtin_amdgcn_s_setprio(0);
-      end_seg();
-      // ---- phase 1: R1 reads b1, M1 = Q1 (a0 x b1)
-      wait(1);
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) b1[j][ks] = g3_bfrag<BT>(lb, wc * 64 + 32 + j * 16, ks, lane);
-      if constexpr (S::LAY == 0) {
-        if (ok2) issueA(X2, k2, s2, pa0);
-      } else if (ok1) {
-        if constexpr (S::LAY == 1) issueA(X1, k1, s1, pa2);
-        else issueB(X1, k1, s1, pmb);
-      }
-      mfma_seg();
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j) acc[i][2 + j] = mfma16(b1[j][ks], a0[i][ks], acc[i][2 + j]);
-      __builtin_amdgcn_s_setprio(0);
-      end_seg();
-      // ---- phase 2: R2 reads a1, M2 = Q2 (a1 x b1)
-      wait(2);
-      if constexpr (AT) {   // the a0 row sums (a0 is re-read in R3)
-        if (do_rs) {
-          if (wc == 0) rowsum2(a0[0], a0[1]);
-          else if (wc == 1) rowsum2(a0[2], a0[3]);
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) a1[i][ks] = g3_afrag<AT>(la, wr * 128 + 64 + i * 16, ks, lane);
-      if constexpr (S::LAY == 0) {
-        if (ok2) issueB(X2, k2, s2, pb0);
-      } else {
-        if (ok2) issueB(X2, k2, s2, pma);
-      }
-      mfma_seg();
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j) acc[4 + i][2 + j] = mfma16(b1[j][ks], a1[i][ks], acc[4 + i][2 + j]);
-      __builtin_amdgcn_s_setprio(0);
-      end_seg();
-      // ---- phase 3: R3 reads a0 of K-tile g + 1 (not after the tile's last K-tile), M3 = Q3 (a1 x b0)
-      wait(3);
-      if (kt + 1 < nk) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int ks = 0; ks < 2; ++ks) a0[i][ks] = g3_afrag<AT>(s1, wr * 128 + i * 16, ks, lane);
-      }
-      if (ok2) {
-        if constexpr (S::LAY == 2) issueA(X2, k2, s2, pma);
-        else if constexpr (S::LAY == 1) issueA(X2, k2, s2, pa0);
-        else issueB(X2, k2, s2, pb1);
-      }
-      mfma_seg();
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j) acc[4 + i][j] = mfma16(b0[j][ks], a1[i][ks], acc[4 + i][j]);
-      __builtin_amdgcn_s_setprio(0);
-      end_seg();
-    }
-    if (wr == 0) __builtin_amdgcn_s_barrier();   // undo the stagger: both rows leave the loop together
-    if constexpr (AT) {   // the last K-tile's a1 row sums
-      if (do_rs) {
-        if (wc == 2) rowsum2(a1[0], a1[1]);
-        else if (wc == 3) rowsum2(a1[2], a1[3]);
-      }
-    }
-    // epilogue operands into the side area (the previous epilogue's reads of it finished before this tile's loop)
-    if (tid < 256) {
-      const int n = T.n0 + tid, m = T.m0 + tid;
-      sbias[tid] = (p.bias && n < p.N) ? p.bias[n] : 0.f;
-      if (EPI == SVAE_EPI_CE_STATS || EPI == SVAE_EPI_CE_PROB || EPI == SVAE_EPI_ROWSCALE_GATHER)
-        slabel[tid] = m < p.M ? p.labels[m] : 0;
-      if (EPI == SVAE_EPI_CE_PROB) sstat[1024 + tid] = (m < p.M && p.labels[m] != 0) ? p.row_a[m] : INFINITY;
-      if (EPI == SVAE_EPI_ROWSCALE_GATHER) sstat[1024 + tid] = m < p.M ? p.row_a[m] : 0.f;
-      if (EPI == SVAE_EPI_ROWSCALE_GATHER) sstat[1280 + tid] = m < p.M ? p.row_b[m] : 0.f;
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if constexpr (AT) {
-      if (do_rs) {
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const float t = sum_x16_x32(rsum[h]);
-          const int m = T.m0 + wr * 128 + (2 * wc + h) * 16 + (lane & 15);
-          if ((lane >> 4) == 0 && m < p.M) atomicAdd(p.a_rowsum + m, t);
-        }
-      }
-    }
-    if constexpr (EPI == SVAE_EPI_BF16 || EPI == SVAE_EPI_GELU || EPI == SVAE_EPI_CE_STATS ||
-                  EPI == SVAE_EPI_ROTARY_BF16 || EPI == SVAE_EPI_CE_PROB)
-      g3_reg_epilogue<EPI>(p, acc, sbias, slabel, sstat, T.m0, T.n0, T.bn, T.batch, T.split, wr, wc, tid, lane);
-    else if constexpr (EPI == SVAE_EPI_ROWSCALE_GATHER)
-      g3_rowscale_gather_epilogue(p, acc, slabel, sstat + 1024, sstat + 1280, T.m0, T.n0, wr, wc, lane);
-    else
-      g3_reg_epilogue_ld<EPI>(p, acc, sbias, T.m0, T.n0, T.batch, T.split, wr, wc, lane);
-    relaxed = p.relaxed && T.m0 + 256 <= p.M && T.n0 + 256 <= p.N;
-    if (!has_next) break;
-    t3 = t3n;
-    T = TN;
-  }
-}
-
-template <bool AT, bool BT, int EPI>
-__global__ __launch_bounds__(512, 1) void gemm256_8ph_kernel(GP p) {
-  gemm256_run8<AT, BT, EPI>(p, blockIdx.x, gridDim.x);
-}
-
 // Two independent GEMMs in one launch (the weight gradients of two layers of one transformer block, split-K slab
 // mode): blocks [0, nb0) run p[0], the rest p[1]. Each GEMM then needs only half the split-K slices to fill the
 // chip, which halves its slab bytes (written by the epilogue, read by slab_reduce) and shares one launch's
@@ -1806,14 +1419,6 @@ __global__ __launch_bounds__(512, 1) void gemm256_pair_kernel(GP2 q) {
   const int b = blockIdx.x;
   if (b < q.nb0) gemm256_run<AT, BT, EPI>(q.p[0], b, q.nb0);
   else gemm256_run<AT, BT, EPI>(q.p[1], b - q.nb0, (int)gridDim.x - q.nb0);
-}
-
-// the paired weight-gradient launch on the 8-phase K-loop
-template <int EPI>
-__global__ __launch_bounds__(512, 1) void gemm256_pair8_kernel(GP2 q) {
-  const int b = blockIdx.x;
-  if (b < q.nb0) gemm256_run8<true, true, EPI>(q.p[0], b, q.nb0);
-  else gemm256_run8<true, true, EPI>(q.p[1], b - q.nb0, (int)gridDim.x - q.nb0);
 }
 
 // ===================================================================================================
@@ -1991,17 +1596,6 @@ static void fill_gp(const svae_gemm_desc* d, GP& p) {
   p.dma_stagger = 0;
 }
 
-// The 8-phase gemm256 (gemm256_run8) applies: SVAE_GEMM8 set, a register epilogue (not the staged split-K atomics,
-// not the k-weighted row sums), a_t only with b_t (the weight-gradient layout), and every tile >= 2 K-tiles (its
-// prefetch reaches two K-tiles ahead). p: the launch parameters (kchunk, splits) after fill_gp.
-static bool g8_ok(const svae_gemm_desc* d, int epi_run, const GP& p) {
-  static const int g8_env = [] { const char* e = getenv("SVAE_GEMM8"); return e ? atoi(e) : 0; }();
-  if (!g8_env || epi_run == SVAE_EPI_F32_ATOMIC || epi_run == G3_EPI_ACC_KW) return false;
-  if (d->a_t && !d->b_t) return false;
-  const long long last = (long long)d->K - (long long)(p.splits - 1) * p.kchunk;   // the last split's K range
-  return p.kchunk >= 128 && last >= 128;
-}
-
 SVAE_EXPORT int svae_gemm(const svae_gemm_desc* d, svae_stream_t stream) {
   if (const int rc = validate_desc(d)) return rc;
   const bool epi_new = d->epi == SVAE_EPI_CE_PROB || d->epi == SVAE_EPI_ROWSCALE_GATHER;
@@ -2085,36 +1679,6 @@ SVAE_EXPORT int svae_gemm(const svae_gemm_desc* d, svae_stream_t stream) {
     static const int stagger_env = [] { const char* e = getenv("SVAE_GEMM_STAGGER"); return e ? atoi(e) : 1; }();
     p.dma_stagger = stagger_env;
     dim3 grid3((unsigned)nb3);
-    // the 8-phase K-loop (gemm256_run8): a register epilogue, every tile >= 2 K-tiles, a_t only with b_t, no k-weights
-    if (g8_ok(d, epi_run, p)) {
-#define SVAE_GEMM8_CASE(E)                                                                                   \
-  case E:                                                                                                    \
-    if (d->a_t) hipLaunchKernelGGL((gemm256_8ph_kernel<true, true, E>), grid3, dim3(512), 0, s, p);          \
-    else if (d->b_t) hipLaunchKernelGGL((gemm256_8ph_kernel<false, true, E>), grid3, dim3(512), 0, s, p);    \
-    else hipLaunchKernelGGL((gemm256_8ph_kernel<false, false, E>), grid3, dim3(512), 0, s, p);               \
-    break;
-      switch (epi_run) {
-        SVAE_GEMM8_CASE(SVAE_EPI_BF16)
-        SVAE_GEMM8_CASE(SVAE_EPI_F32)
-        SVAE_GEMM8_CASE(SVAE_EPI_F32_ACC)
-        SVAE_GEMM8_CASE(SVAE_EPI_GELU)
-        SVAE_GEMM8_CASE(SVAE_EPI_GELU_BWD)
-        SVAE_GEMM8_CASE(SVAE_EPI_DROPOUT_RESID)
-        SVAE_GEMM8_CASE(SVAE_EPI_ROTARY_BF16)
-        SVAE_GEMM8_CASE(SVAE_EPI_CE_STATS)
-        case SVAE_EPI_ROWSCALE_GATHER:
-          if (d->b_t) hipLaunchKernelGGL((gemm256_8ph_kernel<false, true, SVAE_EPI_ROWSCALE_GATHER>), grid3, dim3(512), 0, s, p);
-          else hipLaunchKernelGGL((gemm256_8ph_kernel<false, false, SVAE_EPI_ROWSCALE_GATHER>), grid3, dim3(512), 0, s, p);
-          break;
-        case SVAE_EPI_CE_PROB:
-          hipLaunchKernelGGL((gemm256_8ph_kernel<false, false, SVAE_EPI_CE_PROB>), grid3, dim3(512), 0, s, p);
-          break;
-        default: return SVAE_EINVAL;
-      }
-#undef SVAE_GEMM8_CASE
-      SVAE_LAUNCH_CHECK();
-      return slab ? launch_slab_reduce(d, s) : SVAE_OK;
-    }
 #define SVAE_GEMM3_CASE(E)                                                                                   \
   case E:                                                                                                    \
     if (d->a_t && !d->b_t) {                                                                                 \
@@ -2227,11 +1791,8 @@ SVAE_EXPORT int svae_gemm_pair(const svae_gemm_desc* d0, const svae_gemm_desc* d
   }
   q.nb0 = (int)((nb[0] + 7) / 8 * 8);   // block ranges start on an XCD boundary (block id % 8)
   hipStream_t s = (hipStream_t)stream;
-  if (g8_ok(d0, SVAE_EPI_F32, q.p[0]) && g8_ok(d1, SVAE_EPI_F32, q.p[1]))
-    hipLaunchKernelGGL((gemm256_pair8_kernel<SVAE_EPI_F32>), dim3((unsigned)(q.nb0 + nb[1])), dim3(512), 0, s, q);
-  else
-    hipLaunchKernelGGL((gemm256_pair_kernel<true, true, SVAE_EPI_F32>), dim3((unsigned)(q.nb0 + nb[1])), dim3(512), 0,
-                       s, q);
+  hipLaunchKernelGGL((gemm256_pair_kernel<true, true, SVAE_EPI_F32>), dim3((unsigned)(q.nb0 + nb[1])), dim3(512), 0, s,
+                     q);
   SVAE_LAUNCH_CHECK();
   if (const int rc = launch_slab_reduce(d0, s)) return rc;
   return launch_slab_reduce(d1, s);
