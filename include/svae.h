@@ -81,6 +81,15 @@ typedef struct svae_gemm_desc {
   const float* row_b;       /* ROWSCALE_GATHER: [M] f32                                                  */
   const void* gather;       /* ROWSCALE_GATHER: bf16 rows [*][ldg], row labels[m] gathered; 16-B aligned */
   int64_t ldg;
+  /* optional with SVAE_EPI_BF16 (the attention output projection's dO GEMM under autograd, attention.py:51-105):
+   * also write the attention backward's row constants delta[(b * (N / delta_hd) + h) * delta_seq + q] = sum over
+   * the head's delta_hd columns of bf16(C)[m][h * delta_hd + c] * delta_o32[m * ld_o32 + h * delta_hd + c], m = b *
+   * delta_seq + q (delta_o32: the forward's f32 copy of O). delta is overwritten; svae_attn_bwd with delta_ready = 1
+   * then skips its own delta pass. splits 1, batch 1, a_t 0; N % delta_hd == 0, delta_hd % 16 == 0, M % delta_seq == 0. */
+  float* delta;
+  const float* delta_o32;
+  int64_t ld_o32;
+  int32_t delta_hd, delta_seq;
 } svae_gemm_desc;
 
 int svae_gemm(const svae_gemm_desc* d, svae_stream_t stream);
@@ -166,6 +175,9 @@ typedef struct svae_attn_desc {
      block_size 32, include_cls): query q sees key k <= q iff k < 32 or k / 32 >= q / 32 - (window - 1).
      0 = dense. */
   int32_t window;
+  /* backward: 1 = delta already holds rowsum(dO . O) (svae_gemm's delta epilogue on the dO GEMM): the delta pass is
+     skipped */
+  int32_t delta_ready;
 } svae_attn_desc;
 
 int svae_attn_fwd(const svae_attn_desc* d, svae_stream_t stream);

@@ -292,7 +292,8 @@ __device__ __forceinline__ void attn_fwd_tile(const AP& p, char* smem, int bx, i
   const bf16* K = p.k + b * p.bk + (long long)h * p.hd;
   const bf16* V = p.v + b * p.bv + (long long)h * p.hd;
   const unsigned char* pad = p.pad ? p.pad + (long long)b * p.Lk : nullptr;
-  // key-padding ring: one dword per key (LDS-DMA writes a dword slot per lane; the byte is its low 8 bits)
+  // key-padding ring: one dword per key (LDS-DMA writes a dword slot per lane; the byte is its low 8 bits), one ring
+  // per wave ([wave][NS][64]): every wave DMAs the bytes it reads itself (no wave reads another wave's DMA)
   unsigned* pm = (unsigned*)(smem + NS * 2 * T::BYTES);
 
   const int qw = q0 + 32 * w;
@@ -322,18 +323,19 @@ __device__ __forceinline__ void attn_fwd_tile(const AP& p, char* smem, int bx, i
   const int kt1 = max(1, band_lo(q0, p.window) / 64);
   const int nvisit = 1 + max(0, ntiles - kt1);
   const int lo_w = band_lo(qw, p.window);          // this wave's 32 queries share one 32-block
-  // vector-memory ops one tile issue adds per wave: the K and V pieces, and for wave 0 the key-padding bytes
-  // (DMA'd into the [NS][64] ring like the tiles: no register round trip, no compiler-visible load to wait for)
-  const int ops = DMA_OPS + ((pad && w == 0) ? 1 : 0);
+  // vector-memory ops one tile issue adds per wave: the K and V pieces, and the key-padding bytes (DMA'd into the
+  // wave's own [NS][64] ring like the tiles: no register round trip, no compiler-visible load to wait for)
+  const int ops = DMA_OPS + (pad ? 1 : 0);
   const u32x4 prs = buffer_rsrc(pad ? (const void*)pad : (const void*)p.q, pad ? (unsigned)p.Lk : 0u);
   auto issue = [&](int it2) {
     const int kn = (it2 == 0 ? 0 : kt1 + it2 - 1) * 64;
     char* nb = smem + (it2 % NS) * 2 * T::BYTES;
     dma_tile((const T*)nullptr, K, p.sk, kn, p.Lk, p.hd, nb, w, lane);
     dma_tile((const T*)nullptr, V, p.sv, kn, p.Lk, p.hd, nb + T::BYTES, w, lane);
-    if (pad && w == 0) dma1_lds(prs, pm + (it2 % NS) * 64, kn + lane < p.Lk ? kn + lane : 0x7FFFFFF0);
+    if (pad) dma1_lds(prs, pm + (w * NS + it2 % NS) * 64, kn + lane < p.Lk ? kn + lane : 0x7FFFFFF0);
   };
-  if (!pad && tid < NS * 64) pm[tid] = 0;
+  if (!pad)
+    for (int i = tid; i < 4 * NS * 64; i += 256) pm[i] = 0;
 #pragma unroll
   for (int s2 = 0; s2 < NS - 1; ++s2)
     if (s2 < nvisit) issue(s2);
@@ -350,7 +352,7 @@ __device__ __forceinline__ void attn_fwd_tile(const AP& p, char* smem, int bx, i
     const int st = it % NS;
     const char* Ks = smem + st * 2 * T::BYTES;
     const char* Vs = Ks + T::BYTES;
-    const unsigned* pms = pm + st * 64;
+    const unsigned* pms = pm + (w * NS + st) * 64;
     wait_vmcnt(min(NS - 2, nvisit - 1 - it) * ops);   // this wave's pieces of tile it have landed
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();   // everyone's have; stage (it - 1) % NS is free (a raw barrier: __syncthreads
@@ -526,7 +528,7 @@ __device__ __forceinline__ void attn_fwd_tile(const AP& p, char* smem, int bx, i
 // in flight cost more than the imbalance.)
 template <int HDP, int HDC = HDP>
 __global__ __launch_bounds__(256, HDC <= 96 ? 3 : 2) void attn_fwd_kernel(AP p) {
-  __shared__ __attribute__((aligned(16))) char smem[ATTN_NS * 2 * FwdTile<HDP, HDC>::type::BYTES + ATTN_NS * 64 * 4];
+  __shared__ __attribute__((aligned(16))) char smem[ATTN_NS * 2 * FwdTile<HDP, HDC>::type::BYTES + 4 * ATTN_NS * 64 * 4];
   int bx, h, b;
   xcd_block(bx, h, b, p.causal ? 1 : 0);
   attn_fwd_tile<HDP, HDC>(p, smem, bx, h, b);
@@ -1544,8 +1546,11 @@ SVAE_EXPORT int svae_attn_bwd(const svae_attn_desc* d, svae_stream_t stream) {
   if (((long long)std::max(d->Lq, d->Lk) + 64) * std::max(std::max(d->sq, d->sk), d->sdo) * 2 > 0x7FFFFFF0LL) return SVAE_EINVAL;
   hipStream_t s = (hipStream_t)stream;
   const int rows = d->B * d->Lq * d->H;
-  if (d->hd <= 64) hipLaunchKernelGGL(attn_delta_kernel<8>, dim3((rows + 31) / 32), dim3(256), 0, s, p);
-  else hipLaunchKernelGGL(attn_delta_kernel<16>, dim3((rows + 15) / 16), dim3(256), 0, s, p);
+  // delta_ready: the dO GEMM's epilogue already wrote delta (svae_gemm_desc.delta)
+  if (!d->delta_ready) {
+    if (d->hd <= 64) hipLaunchKernelGGL(attn_delta_kernel<8>, dim3((rows + 31) / 32), dim3(256), 0, s, p);
+    else hipLaunchKernelGGL(attn_delta_kernel<16>, dim3((rows + 15) / 16), dim3(256), 0, s, p);
+  }
   // hd <= 96: the 8-wave 256-key kernel; hd 128: the 4-wave 128-key one (its LDS rows do not fit the 8-wave layout).
   // SVAE_ATTN_BWD8=0: the 4-wave kernels for every hd (A/B runs)
   static const int bwd8_env = [] { const char* e = getenv("SVAE_ATTN_BWD8"); return e ? atoi(e) : 1; }();

@@ -43,6 +43,7 @@ struct GP {
   int relaxed;       // gemm256 persistent: allow the vmcnt(G3_EPI_STORES) first wait after interior epilogues
   int dma_stagger;   // gemm256: the M-half-1 waves issue their next-K-tile DMA after their first MFMA quadrant
   long long slab;    // split-K slab mode: split s writes its partial tile at C + s * slab (0 = off)
+  float* delta; const float* delta_o32; long long ld_o32; int delta_hd, delta_seq;   // see svae_gemm_desc.delta
 };
 
 // byte offset of (row, 16-B chunk c) in a K-contiguous [128][64] bf16 tile (128-B rows)
@@ -595,6 +596,8 @@ __global__ __launch_bounds__(256, 3) void gemm_glds_kernel(GP p) {
 // 256 threads.
 constexpr int G3_T = 256 * 64 * 2;   // 32 KiB per operand K-tile
 constexpr int G3_STAGE = 2 * G3_T;
+// internal instantiation: SVAE_EPI_BF16 that also writes the attention backward's delta (svae_gemm_desc.delta)
+constexpr int G3_EPI_BF16_DELTA = 65;
 
 // Per-lane DMA source offsets of one operand's K-tile, hoisted out of the K loop: only the tile base (a
 // scalar) moves with k0. off[i] already carries the M/N-bound (out-of-range -> OOB offset); the K tail
@@ -983,7 +986,55 @@ __device__ __forceinline__ void g3_reg_epilogue_ld(const GP& p, const f32x4 (&ac
   f32x4 b4[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) b4[j] = *(const f32x4*)(sbias + wc * 64 + j * 16 + 4 * g);
-  if constexpr (EPI == SVAE_EPI_GELU_BWD) {
+  if constexpr (EPI == G3_EPI_BF16_DELTA) {
+    // bf16 out, and per (row, head) the sum of bf16(C) * O32 over the head's columns (the attention backward's delta,
+    // attention.py:51-105). A wave's 64 columns hold at most two heads (hd 64 / 96 / 128, head bounds on 16-column
+    // fragments): one partial per head, reduced over the 4 lane groups, added by f32 atomics into the zeroed delta
+    // -- at most two contributions per (row, head) onto 0, so the order does not change the sum. The O32 rows of
+    // fragment row i + 1 are loaded before row i's stores (vmcnt retires in issue order).
+    const int H = p.N / p.delta_hd;
+    const int hA = nb / p.delta_hd;
+    auto ld_row = [&](int i, f32x4 (&r)[4]) {
+      const int m = m0 + wr * 128 + i * 16 + li;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = nb + j * 16 + 4 * g;
+        r[j] = (m < p.M && n < p.N) ? *(const f32x4*)(p.delta_o32 + (long long)m * p.ld_o32 + n)
+                                    : (f32x4){0.f, 0.f, 0.f, 0.f};
+      }
+    };
+    f32x4 cur[4], nxt[4];
+    ld_row(0, cur);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if (i + 1 < 8) ld_row(i + 1, nxt);
+      const int m = m0 + wr * 128 + i * 16 + li;
+      f32x4 x[4];
+      float sA = 0.f, sB = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        x[j] = p.alpha * acc[i][j] + b4[j];
+        float dj = 0.f;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) dj = fmaf((float)f2bf(x[j][e]), cur[j][e], dj);
+        if ((nb + 16 * j) / p.delta_hd == hA) sA += dj;
+        else sB += dj;
+      }
+      store_rows_bf16<false>((bf16*)p.C + cofs, p.ldc, m0 + wr * 128 + i * 16, p.M, nb, p.N, x, g, li);
+      sA = sum_x16_x32(sA);
+      sB = sum_x16_x32(sB);
+      if (g == 0 && m < p.M && nb < p.N) {
+        const int b = m / p.delta_seq, q = m - b * p.delta_seq;
+        atomicAdd(p.delta + ((long long)b * H + hA) * p.delta_seq + q, sA);
+        if ((nb + 63) / p.delta_hd != hA && hA + 1 < H) atomicAdd(p.delta + ((long long)b * H + hA + 1) * p.delta_seq + q, sB);
+      }
+      if (i + 1 < 8) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) cur[j] = nxt[j];
+      }
+    }
+    return;
+  } else if constexpr (EPI == SVAE_EPI_GELU_BWD) {
     const int cs = ((g & 1) ? 16 : 0) + ((g & 2) ? 8 : 0);   // column of this lane's 8 within a 32-column pair
     auto ld_row = [&](int i, u32x4 (&r)[2]) {
       const int m = m0 + wr * 128 + i * 16 + li;
@@ -1119,6 +1170,7 @@ template <int EPI>
 constexpr int g3_epi_vmem_ops() {
   switch (EPI) {
     case SVAE_EPI_BF16:
+    case G3_EPI_BF16_DELTA:
     case SVAE_EPI_ROTARY_BF16:
     case SVAE_EPI_CE_STATS:           // with C (the host clears p.relaxed when C == NULL: no logits stored)
     case SVAE_EPI_ROWSCALE_GATHER:
@@ -1378,7 +1430,7 @@ __device__ __forceinline__ void gemm256_run(const GP& p, int blk, int nwg) {
     else if constexpr (EPI == SVAE_EPI_ROWSCALE_GATHER)
       g3_rowscale_gather_epilogue(p, acc, slabel, sstat + 1024, sstat + 1280, T.m0, T.n0, wr, wc, lane);
     else if constexpr (EPI == SVAE_EPI_F32 || EPI == SVAE_EPI_F32_ACC || EPI == SVAE_EPI_DROPOUT_RESID ||
-                       EPI == SVAE_EPI_GELU_BWD)
+                       EPI == SVAE_EPI_GELU_BWD || EPI == G3_EPI_BF16_DELTA)
       g3_reg_epilogue_ld<EPI>(p, acc, sbias, T.m0, T.n0, T.batch, T.split, wr, wc, lane);
     else if constexpr (EPI == G3_EPI_ACC_KW)
       g3_reg_epilogue_ld<SVAE_EPI_F32_ACC>(p, acc, sbias, T.m0, T.n0, T.batch, T.split, wr, wc, lane);
@@ -1594,9 +1646,52 @@ static void fill_gp(const svae_gemm_desc* d, GP& p) {
   p.epi = d->epi;
   p.slab = 0;
   p.dma_stagger = 0;
+  p.delta = d->delta; p.delta_o32 = d->delta_o32; p.ld_o32 = d->ld_o32;
+  p.delta_hd = d->delta_hd; p.delta_seq = d->delta_seq;
 }
 
+// delta[(b * H + h) * seq + q] = sum_c bf16 C[m][h * hd + c] * o32[m][h * hd + c] (m = b * seq + q), one wave per
+// (row, head) -- svae_gemm's delta for the GEMMs that do not run the 256 x 256 kernel (its epilogue does it there)
+__global__ __launch_bounds__(256) void gemm_delta_kernel(const bf16* __restrict__ C, long long ldc,
+                                                         const float* __restrict__ o32, long long ldo, int M, int H,
+                                                         int hd, int seq, float* __restrict__ delta) {
+  const int gw = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (gw >= M * H) return;
+  const int m = gw / H, h = gw - m * H;
+  float s = 0.f;
+  for (int c = lane * 4; c < hd; c += 256) {
+    const bf16x4 a = *(const bf16x4*)(C + (long long)m * ldc + h * hd + c);
+    const f32x4 o = *(const f32x4*)(o32 + (long long)m * ldo + h * hd + c);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) s = fmaf((float)a[e], o[e], s);
+  }
+  s = wave_sum(s);
+  const int b = m / seq, q = m - b * seq;
+  if (lane == 0) delta[((long long)b * H + h) * seq + q] = s;
+}
+
+static int gemm_run(const svae_gemm_desc* d, svae_stream_t stream, bool* fused_delta);
+
 SVAE_EXPORT int svae_gemm(const svae_gemm_desc* d, svae_stream_t stream) {
+  if (!d || !d->delta) return gemm_run(d, stream, nullptr);
+  // the attention backward's delta alongside the dO GEMM (svae_gemm_desc.delta)
+  if (d->epi != SVAE_EPI_BF16 || d->splits != 1 || d->batch != 1 || d->a_t || !d->delta_o32 || !d->C ||
+      d->delta_hd <= 0 || d->delta_hd % 16 || d->N % d->delta_hd || d->delta_seq <= 0 || d->M % d->delta_seq ||
+      d->ld_o32 < d->N || d->ld_o32 % 4 || ((uintptr_t)d->delta_o32 & 15) || ((uintptr_t)d->C & 7))
+    return SVAE_EINVAL;
+  bool fused = false;
+  if (const int rc = gemm_run(d, stream, &fused)) return rc;
+  if (!fused) {
+    const int H = d->N / d->delta_hd;
+    hipLaunchKernelGGL(gemm_delta_kernel, dim3((unsigned)(((long long)d->M * H + 3) / 4)), dim3(256), 0,
+                       (hipStream_t)stream, (const bf16*)d->C, (long long)d->ldc, d->delta_o32, (long long)d->ld_o32,
+                       d->M, H, d->delta_hd, d->delta_seq, d->delta);
+    SVAE_LAUNCH_CHECK();
+  }
+  return SVAE_OK;
+}
+
+static int gemm_run(const svae_gemm_desc* d, svae_stream_t stream, bool* fused_delta) {
   if (const int rc = validate_desc(d)) return rc;
   const bool epi_new = d->epi == SVAE_EPI_CE_PROB || d->epi == SVAE_EPI_ROWSCALE_GATHER;
   GP p;
@@ -1679,6 +1774,13 @@ SVAE_EXPORT int svae_gemm(const svae_gemm_desc* d, svae_stream_t stream) {
     static const int stagger_env = [] { const char* e = getenv("SVAE_GEMM_STAGGER"); return e ? atoi(e) : 1; }();
     p.dma_stagger = stagger_env;
     dim3 grid3((unsigned)nb3);
+    // the delta epilogue (a wave's 64 columns hold at most two heads: hd >= 64) adds into a zeroed delta (svae_gemm)
+    if (fused_delta && epi_run == SVAE_EPI_BF16 && d->delta_hd >= 64) {
+      const long long n = (long long)d->M * (d->N / d->delta_hd);
+      if (hipMemsetAsync(d->delta, 0, n * sizeof(float), s) != hipSuccess) return SVAE_ELAUNCH;
+      epi_run = G3_EPI_BF16_DELTA;
+      *fused_delta = true;
+    }
 #define SVAE_GEMM3_CASE(E)                                                                                   \
   case E:                                                                                                    \
     if (d->a_t && !d->b_t) {                                                                                 \
@@ -1704,6 +1806,10 @@ SVAE_EXPORT int svae_gemm(const svae_gemm_desc* d, svae_stream_t stream) {
         break;
       case SVAE_EPI_CE_PROB:
         hipLaunchKernelGGL((gemm256_kernel<false, false, SVAE_EPI_CE_PROB>), grid3, dim3(512), 0, s, p);
+        break;
+      case G3_EPI_BF16_DELTA:
+        if (d->b_t) hipLaunchKernelGGL((gemm256_kernel<false, true, G3_EPI_BF16_DELTA>), grid3, dim3(512), 0, s, p);
+        else hipLaunchKernelGGL((gemm256_kernel<false, false, G3_EPI_BF16_DELTA>), grid3, dim3(512), 0, s, p);
         break;
       case SVAE_EPI_ROWSCALE_GATHER:
         if (d->b_t) hipLaunchKernelGGL((gemm256_kernel<false, true, SVAE_EPI_ROWSCALE_GATHER>), grid3, dim3(512), 0, s, p);

@@ -37,6 +37,7 @@ class GemmDesc(ctypes.Structure):
         ('labels', c_void_p), ('label_logit', c_void_p),
         ('a_rowsum', c_void_p),
         ('k_weight', c_void_p), ('row_a', c_void_p), ('row_b', c_void_p), ('gather', c_void_p), ('ldg', c_int64),
+        ('delta', c_void_p), ('delta_o32', c_void_p), ('ld_o32', c_int64), ('delta_hd', c_int32), ('delta_seq', c_int32),
     ]
 
 
@@ -56,6 +57,7 @@ class AttnDesc(ctypes.Structure):
         ('o32', c_void_p), ('so32', c_int64), ('bo32', c_int64),
         ('dq_part', c_void_p), ('dq_bf', c_void_p), ('ldq_bf', c_int64),
         ('window', c_int32),
+        ('delta_ready', c_int32),
     ]
 
 

@@ -22,13 +22,19 @@ def _dev(*ts):
 def gemm(A, B, C, M, N_, K, *, a_t=False, b_t=False, lda=None, ldb=None, ldc=None, epi=N.EPI_BF16, bias=None,
          resid=None, ldr=0, aux=None, ldaux=0, alpha=1.0, splits=1, drop_p=0.0, seed=0, rot=None, rot_cols=0,
          rot_d=0, rot_seq=0, labels=None, label_logit=None, batch=1, sA=0, sB=0, sC=0, a_rowsum=None, k_weight=None,
-         row_a=None, row_b=None, gather=None, ldg=0):
-    """C = epi(alpha * A . B) with A [M,K] (a_t: stored [K,M]) and B [K,N] (b_t: stored [K,N], else [N,K])."""
+         row_a=None, row_b=None, gather=None, ldg=0, delta=None, delta_o32=None, ld_o32=0, delta_hd=0, delta_seq=0):
+    """C = epi(alpha * A . B) with A [M,K] (a_t: stored [K,M]) and B [K,N] (b_t: stored [K,N], else [N,K]).
+    delta (BF16 epilogue): also the attention backward's delta = rowsum over each head of bf16(C) * delta_o32."""
     d = _fill_desc(_gemm_desc, A, B, C, M, N_, K, a_t=a_t, b_t=b_t, lda=lda, ldb=ldb, ldc=ldc, epi=epi, bias=bias,
                    resid=resid, ldr=ldr, aux=aux, ldaux=ldaux, alpha=alpha, splits=splits, drop_p=drop_p, seed=seed,
                    rot=rot, rot_cols=rot_cols, rot_d=rot_d, rot_seq=rot_seq, labels=labels, label_logit=label_logit,
                    batch=batch, sA=sA, sB=sB, sC=sC, a_rowsum=a_rowsum, k_weight=k_weight, row_a=row_a, row_b=row_b,
                    gather=gather, ldg=ldg)
+    if delta is not None:
+        _dev(delta, delta_o32)
+        assert delta.dtype == f32 and delta_o32.dtype == f32 and delta.numel() >= M * (N_ // delta_hd)
+    d.delta, d.delta_o32, d.ld_o32 = ptr(delta), ptr(delta_o32), ld_o32
+    d.delta_hd, d.delta_seq = delta_hd, delta_seq
     check(lib.svae_gemm(ctypes.byref(d), stream()), 'svae_gemm')
 
 
@@ -65,6 +71,7 @@ def _fill_desc(d, A, B, C, M, N_, K, *, a_t=False, b_t=False, lda=None, ldb=None
     d.k_weight = ptr(k_weight)
     d.row_a, d.row_b = ptr(row_a), ptr(row_b)
     d.gather, d.ldg = ptr(gather), ldg
+    d.delta, d.delta_o32, d.ld_o32, d.delta_hd, d.delta_seq = None, None, 0, 0, 0
     return d
 
 
@@ -202,7 +209,7 @@ _attn_desc = N.AttnDesc()
 def attention(q, k, v, o, lse, *, B, H, Lq, Lk, hd, sq, sk, sv, so, bq, bk, bv, bo, key_pad=None, causal=False,
               window=0, scale=None, backward=False, dout=None, sdo=0, bdo=0, delta=None, dq=None, bdq=0, dk=None, dv=None,
               sdk=0, sdv=0, bdk=0, bdv=0, rot=None, rot_d=0, o32=None, so32=0, bo32=0, dq_part=None, dq_bf=None,
-              ldq_bf=0):
+              ldq_bf=0, delta_ready=False):
     """Forward (o, lse[, o32]) or backward (dk, dv and dq: f32 `dq` or bf16 `dq_bf` with inverse rotary).
     dq_part: f32 workspace of attn_dq_part_elems(...) floats (allocated here when not given).
     window > 0 (causal): SparseAttention's sliding window of `window` 32-key blocks + the [CLS] block."""
@@ -213,6 +220,7 @@ def attention(q, k, v, o, lse, *, B, H, Lq, Lk, hd, sq, sk, sv, so, bq, bk, bv, 
     d.lse = lse.data_ptr()
     d.B, d.H, d.Lq, d.Lk, d.hd, d.causal = B, H, Lq, Lk, hd, int(causal)
     d.window = int(window)
+    d.delta_ready = int(bool(delta_ready))
     d.scale = hd ** -0.5 if scale is None else scale
     d.o32, d.so32, d.bo32 = ptr(o32), so32, bo32
     if backward:

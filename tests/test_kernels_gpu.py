@@ -686,3 +686,26 @@ def test_resid_ln_fwd(D, p, with_x, with_z, with_ln, ydt):
         torch.testing.assert_close(rstd, (v.var(-1, unbiased=False) + 1e-5).rsqrt(), rtol=1e-4, atol=1e-5)
     else:
         assert torch.equal(h, v.bfloat16())
+
+
+@pytest.mark.parametrize('M,Nn,Kk,hd,seq', [(24576, 512, 512, 64, 512),     # gemm256: the fused epilogue (hd 64)
+                                            (16384, 768, 768, 96, 1024),    # gemm256, hd 96: heads across waves
+                                            (4096, 512, 512, 64, 128),      # small grid: the separate delta kernel
+                                            (64, 128, 128, 16, 1)])         # skinny GEMM, hd 16
+def test_gemm_delta_epilogue(M, Nn, Kk, hd, seq):
+    """svae_gemm's delta (the attention backward's rowsum(dO . O) per head, written by the dO GEMM): C identical to
+    the plain BF16 GEMM, delta against torch on the bf16 C and the f32 O copy (summation order differs: 1e-5)."""
+    torch.manual_seed(M + hd)
+    A = torch.randn(M, Kk, device=dev).bfloat16()
+    W = (torch.randn(Nn, Kk, device=dev) * 0.05).bfloat16()
+    o32 = torch.randn(M, Nn, device=dev)
+    C0 = torch.empty(M, Nn, device=dev, dtype=torch.bfloat16)
+    K.gemm(A, W, C0, M, Nn, Kk, epi=N.EPI_BF16)
+    C = torch.empty_like(C0)
+    delta = torch.full((M * (Nn // hd),), 7.0, device=dev)
+    K.gemm(A, W, C, M, Nn, Kk, epi=N.EPI_BF16, delta=delta, delta_o32=o32, ld_o32=Nn, delta_hd=hd, delta_seq=seq)
+    torch.cuda.synchronize()
+    assert torch.equal(C, C0)
+    H = Nn // hd
+    ref = (C.float() * o32).view(M // seq, seq, H, hd).sum(-1).permute(0, 2, 1).reshape(-1)
+    torch.testing.assert_close(delta, ref, rtol=1e-5, atol=1e-4)
