@@ -42,6 +42,7 @@ def main():
         'rowsum': lambda: K.gemm(P, hh, dW, V, d, T, a_t=True, b_t=True, ldb=d, epi=N.EPI_F32_ACC, a_rowsum=rs),
         'k_weight': lambda: K.gemm(P, hh, dW, V, d, T, a_t=True, b_t=True, ldb=d, epi=N.EPI_F32_ACC, a_rowsum=rs,
                                    k_weight=kw),
+        'plain_s2': lambda: K.gemm(P, hh, dW, V, d, T, a_t=True, b_t=True, ldb=d, epi=N.EPI_F32_ATOMIC, splits=2),
     }
     for r in range(2):
         for name, fn in cases.items():

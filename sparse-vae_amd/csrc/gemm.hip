@@ -1150,6 +1150,7 @@ constexpr int G3_EPI_STORES = 16;
 // diagnostic build only (make STAMPS=1 -> libsvae_stamps.so): s_memtime at tile start / after the K loop / after
 // the epilogue, for blocks 0..7 and their first 96 tiles
 __device__ unsigned long long svae_stamps[8][96][3];
+__device__ unsigned long long svae_rt[1024][2];   // per block: entry, exit (s_memrealtime, 100 MHz)
 #define G3_STAMP(k) \
   do { if (blockIdx.x < 8 && tid == 0 && ntile < 96) svae_stamps[blockIdx.x][ntile][k] = __builtin_amdgcn_s_memtime(); } while (0)
 #else
@@ -1454,7 +1455,14 @@ __device__ __forceinline__ void gemm256_run(const GP& p, int blk, int nwg) {
 
 template <bool AT, bool BT, int EPI>
 __global__ __launch_bounds__(512, 1) void gemm256_kernel(GP p) {
+#ifdef SVAE_STAMPS
+  // (diagnostic) every block's entry and exit on the chip-wide 100 MHz clock: the launch's start skew and tail
+  if (threadIdx.x == 0 && blockIdx.x < 1024) svae_rt[blockIdx.x][0] = __builtin_amdgcn_s_memrealtime();
+#endif
   gemm256_run<AT, BT, EPI>(p, blockIdx.x, gridDim.x);
+#ifdef SVAE_STAMPS
+  if (threadIdx.x == 0 && blockIdx.x < 1024) svae_rt[blockIdx.x][1] = __builtin_amdgcn_s_memrealtime();
+#endif
 }
 
 // Two independent GEMMs in one launch (the weight gradients of two layers of one transformer block, split-K slab
@@ -1907,6 +1915,9 @@ SVAE_EXPORT int svae_gemm_pair(const svae_gemm_desc* d0, const svae_gemm_desc* d
 #ifdef SVAE_STAMPS
 extern "C" __attribute__((visibility("default"))) int svae_debug_stamps(unsigned long long* host) {
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(svae_stamps), sizeof(svae_stamps)) == hipSuccess ? 0 : -1;
+}
+extern "C" __attribute__((visibility("default"))) int svae_debug_rt(unsigned long long* host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(svae_rt), sizeof(svae_rt)) == hipSuccess ? 0 : -1;
 }
 extern "C" __attribute__((visibility("default"))) int svae_debug_stamps_clear() {
   static unsigned long long zeros[8 * 96 * 3];

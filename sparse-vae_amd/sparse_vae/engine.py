@@ -243,6 +243,10 @@ class VAEEngine:
         # 36 B per element and layer against 28 (the projection output makes an f32 round trip), +0.125 ms of kernel
         # time per step (profiles/r03f_*); at C4 +0.5-0.8 ms/step
         self.fuse_ln = os.environ.get('SVAE_FUSE_LN', '0') != '0'
+        # attention backward delta = rowsum(dO . O): SVAE_DELTA_FUSED=1 has the dO GEMM's epilogue write it (built and
+        # tested, measured no faster: C2 12.725 / 12.696 vs 12.648 / 12.681 ms, C4 neutral,
+        # profiles/r04j_delta_ab.log); default: the attention backward's own delta pass
+        self.delta_fused = os.environ.get('SVAE_DELTA_FUSED', '0') != '0'
         self.side = None
         if flat.device.type == 'cuda' and os.environ.get('SVAE_DW_STREAM', '0') != '0':
             self.side = torch.cuda.Stream(device=flat.device)
@@ -482,13 +486,13 @@ class VAEEngine:
             dOc = ws.get('b.dO', (rows_q, d))
             delta = ws.get('b.delta', (B, heads, Lq), f32)
             # the dO GEMM also writes delta = rowsum(dO . O) per head (its epilogue holds dO; no separate pass)
-            K.gemm(gxc, P.wT(c + 'output_linear.weight', d, d), dOc, rows_q, d, d, epi=EPI_BF16, delta=delta,
+            K.gemm(gxc, P.wT(c + 'output_linear.weight', d, d), dOc, rows_q, d, d, epi=EPI_BF16, delta=delta if self.delta_fused else None,
                    delta_o32=st['Oc32'], ld_o32=d, delta_hd=hd, delta_seq=Lq)
             dqc = ws.get('b.dqc', (rows_q, d))
             dkvc = ws.get('b.dkvc', (rows_c, 2 * d))
             K.attention(st['qc'], st['kvc'], st['kvc'][:, d:], st['Oc'], st['lsec'], B=B, H=heads, Lq=Lq, Lk=L,
                         hd=hd, sq=d, bq=Lq * d, sk=2 * d, sv=2 * d, bk=L * 2 * d, bv=L * 2 * d, so=d, bo=Lq * d,
-                        key_pad=st['pad_ctx'], causal=False, backward=True, delta_ready=True,
+                        key_pad=st['pad_ctx'], causal=False, backward=True, delta_ready=self.delta_fused,
                         dout=dOc, sdo=d, bdo=Lq * d, delta=delta, dq_bf=dqc, ldq_bf=d, dk=dkvc, dv=dkvc[:, d:],
                         sdk=2 * d, sdv=2 * d, bdk=L * 2 * d, bdv=L * 2 * d, rot=rot, rot_d=d, o32=st['Oc32'],
                         so32=d, bo32=Lq * d, dq_part=self._dq_part(B, heads, Lq, L, hd))
@@ -508,7 +512,7 @@ class VAEEngine:
         wo_dw = (gx1, st['O'], a + 'output_linear.weight', rows_q, d, d, None, None, a + 'output_linear.bias')
         dO = ws.get('b.dO', (rows_q, d))
         delta = ws.get('b.delta', (B, heads, Lq), f32)
-        K.gemm(gx1, P.wT(a + 'output_linear.weight', d, d), dO, rows_q, d, d, epi=EPI_BF16, delta=delta,
+        K.gemm(gx1, P.wT(a + 'output_linear.weight', d, d), dO, rows_q, d, d, epi=EPI_BF16, delta=delta if self.delta_fused else None,
                delta_o32=st['O32'], ld_o32=d, delta_hd=hd, delta_seq=Lq)
         if st['learned']:
             kv = st['kv']
@@ -517,7 +521,7 @@ class VAEEngine:
             K.attention(P.w(a + 'learned_queries').view(Lq, d), kv, kv[:, d:], st['O'], st['lse'], B=B, H=heads,
                         Lq=Lq, Lk=Sx, hd=hd, sq=d, bq=0, sk=2 * d, sv=2 * d, bk=Sx * 2 * d, bv=Sx * 2 * d, so=d,
                         bo=Lq * d, key_pad=st['pad_k'], causal=False, backward=True, dout=dO, sdo=d, bdo=Lq * d,
-                        delta=delta, delta_ready=True, dq=dq32, bdq=Lq * d, dk=dkv, dv=dkv[:, d:], sdk=2 * d, sdv=2 * d,
+                        delta=delta, delta_ready=self.delta_fused, dq=dq32, bdq=Lq * d, dk=dkv, dv=dkv[:, d:], sdk=2 * d, sdv=2 * d,
                         bdk=Sx * 2 * d, bdv=Sx * 2 * d, rot=rot, rot_d=d, o32=st['O32'], so32=d, bo32=Lq * d,
                         dq_part=self._dq_part(B, heads, Lq, Sx, hd))
             K.colsum(dq32, B, Lq * d, Lq * d, P.g(a + 'learned_queries').view(-1))
@@ -532,7 +536,7 @@ class VAEEngine:
                         sq=3 * d, bq=Sx * 3 * d, sk=3 * d, sv=3 * d, bk=Sx * 3 * d, bv=Sx * 3 * d, so=d, bo=Lq * d,
                         key_pad=st['pad_k'], causal=st['causal'], window=st['window'], backward=True, dout=dO,
                         sdo=d, bdo=Lq * d,
-                        delta=delta, delta_ready=True, dq_bf=dqkv, ldq_bf=3 * d, dk=dqkv[:, d:], dv=dqkv[:, 2 * d:], sdk=3 * d,
+                        delta=delta, delta_ready=self.delta_fused, dq_bf=dqkv, ldq_bf=3 * d, dk=dqkv[:, d:], dv=dqkv[:, 2 * d:], sdk=3 * d,
                         sdv=3 * d, bdk=Sx * 3 * d, bdv=Sx * 3 * d, rot=rot, rot_d=d, o32=st['O32'], so32=d,
                         bo32=Lq * d, dq_part=self._dq_part(B, heads, Lq, Sx, hd))
             self._dw_pair(wo_dw, (dqkv, st['h'], a + 'q_linear.weight', rows_x, 3 * d, d, None, None,

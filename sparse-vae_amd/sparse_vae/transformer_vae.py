@@ -248,7 +248,8 @@ class TransformerVAE(ContinuousVAEHooks, LanguageModel):
             self.logged.pop(stage + '_mc_mutual_info', None)
         if stage == 'train':
             loss = _StepFn.apply(self._anchor, self, out['loss'])
-            return {'loss': loss, 'posterior': Normal(loc=mu.detach(), scale=scale.detach())}
+            # (validate_args=False: the argument check reads the scale back to the host, a sync per step)
+            return {'loss': loss, 'posterior': Normal(loc=mu.detach(), scale=scale.detach(), validate_args=False)}
         if stage == 'val':
             self.log('val_loss', out['nll'] + out['kl'])
             if self.token_weights is not None:
