@@ -75,7 +75,8 @@ typedef struct svae_gemm_desc {
   const int32_t* labels;    /* CE_STATS: [M] target column per row (0 = ignored) */
   float* label_logit;       /* CE_STATS: [M] f32 out */
   float* a_rowsum;          /* a_t only, optional: a_rowsum[m] += sum_k A[m][k] (bias grad of a dW GEMM) */
-  /* optional with a_rowsum (a_t && b_t, splits 1): a_rowsum[m] += sum_k A[m][k] * k_weight[k]            */
+  /* optional with a_rowsum (a_t && b_t; splits 1 with F32_ACC, or split-K slab mode: F32_ATOMIC with aux):  */
+  /* a_rowsum[m] += sum_k A[m][k] * k_weight[k]                                                            */
   const float* k_weight;
   const float* row_a;       /* CE_PROB / ROWSCALE_GATHER: [M] f32 (see svae_epi)                        */
   const float* row_b;       /* ROWSCALE_GATHER: [M] f32                                                  */

@@ -36,6 +36,7 @@ def main():
     dW = torch.zeros(V, d, device=dev)
     rs = torch.zeros(V, device=dev)
     kw = torch.rand(T, device=dev)
+    slab = torch.empty(2 * V * d, device=dev)
     fl = 2.0 * T * d * V
     cases = {
         'plain': lambda: K.gemm(P, hh, dW, V, d, T, a_t=True, b_t=True, ldb=d, epi=N.EPI_F32_ACC),
@@ -43,6 +44,8 @@ def main():
         'k_weight': lambda: K.gemm(P, hh, dW, V, d, T, a_t=True, b_t=True, ldb=d, epi=N.EPI_F32_ACC, a_rowsum=rs,
                                    k_weight=kw),
         'plain_s2': lambda: K.gemm(P, hh, dW, V, d, T, a_t=True, b_t=True, ldb=d, epi=N.EPI_F32_ATOMIC, splits=2),
+        'kw_slab2': lambda: K.gemm(P, hh, dW, V, d, T, a_t=True, b_t=True, ldb=d, epi=N.EPI_F32_ATOMIC, splits=2,
+                                   aux=slab, a_rowsum=rs, k_weight=kw),
     }
     for r in range(2):
         for name, fn in cases.items():

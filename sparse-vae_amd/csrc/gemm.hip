@@ -1159,6 +1159,9 @@ __device__ unsigned long long svae_rt[1024][2];   // per block: entry, exit (s_m
 // internal instantiation: SVAE_EPI_F32_ACC whose fused bias-gradient row sums are weighted by k_weight (the
 // vocabulary head's dW, where the per-token weight r folds the softmax normalisation into the row sums)
 constexpr int G3_EPI_ACC_KW = 64;
+// internal: the split-K slab form of the same (each split stores its partial tile, slab_reduce adds them into C;
+// the k-weighted row sums of each split's K range go to a_rowsum by atomics as in every split-K row sum)
+constexpr int G3_EPI_F32_KW = 66;
 #ifndef SVAE_KW_FORM
 #define SVAE_KW_FORM 0
 #endif
@@ -1185,6 +1188,7 @@ constexpr int g3_epi_vmem_ops() {
     case SVAE_EPI_F32_ACC:
     case SVAE_EPI_DROPOUT_RESID:
     case G3_EPI_ACC_KW:
+    case G3_EPI_F32_KW:
       return 8 * 4;                   // 8 fragment rows x 4 16-B f32 stores
     case SVAE_EPI_F32_ATOMIC:
       return 4 * 32;                  // staged: 4 passes x 32 atomics per lane
@@ -1204,7 +1208,8 @@ __device__ __forceinline__ void gemm256_run(const GP& p, int blk, int nwg) {
   // [stage][wave] k-weight slots, each wave DMAs the weights of a K-tile into its OWN slot -- form 1: 64 dwords
   // (buffer_load_dword lds) after the side area (138 KiB); form 2: 16-B pieces (buffer_load_dwordx4 lds, lanes 0-15)
   // after the side area; form 3: 64 dwords at offset 0, the ring moved up by 4 KiB (all DMA below 132 KiB)
-  constexpr int KW_FORM = EPI == G3_EPI_ACC_KW ? SVAE_KW_FORM : 0;
+  constexpr bool IS_KW = EPI == G3_EPI_ACC_KW || EPI == G3_EPI_F32_KW;
+  constexpr int KW_FORM = IS_KW ? SVAE_KW_FORM : 0;
   constexpr int KW_SLOT = KW_FORM == 2 ? 1024 : 256;
   constexpr int KW_BYTES = KW_FORM ? 2 * 8 * KW_SLOT : 0;
   constexpr int RING_OFF = KW_FORM == 3 ? KW_BYTES : 0;
@@ -1282,7 +1287,7 @@ __device__ __forceinline__ void gemm256_run(const GP& p, int blk, int nwg) {
       const bool do_rs = AT && p.a_rowsum && T.bn < 2;
       // p.dma_stagger: the two waves of a SIMD (wr 0 and 1, same wc) issue their pieces of the next K-tile at different
       // times -- wr 0 here, wr 1 after its first MFMA quadrant -- so one wave's DMA issue runs beside the other's MFMAs
-      const bool late = EPI != G3_EPI_ACC_KW && p.dma_stagger && wr == 1 && kt + 1 < T.nk;   // (wave-uniform)
+      const bool late = !IS_KW && p.dma_stagger && wr == 1 && kt + 1 < T.nk;   // (wave-uniform)
       if (kt + 1 < T.nk) {
         if (!late) {
           g3_issue<AT, BT>(p, T.A, T.B, sa, sb, T.m0, T.n0, T.kbeg + (kt + 1) * 64, T.kend, nxt, wave);
@@ -1320,7 +1325,7 @@ __device__ __forceinline__ void gemm256_run(const GP& p, int blk, int nwg) {
             const float* kws = (const float*)(skw + ((g & 1) * 8 + wave) * KW_SLOT) + 32 * ks + 8 * (lane >> 4);
             k0 = *(const f32x4*)kws;
             k1 = *(const f32x4*)(kws + 4);
-          } else if constexpr (EPI == G3_EPI_ACC_KW) {
+          } else if constexpr (IS_KW) {
             const int kk = T.kbeg + kt * 64 + 32 * ks + 8 * (lane >> 4);   // (K % 8 == 0: 8 inside or 8 past)
             const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
             k0 = kk < T.kend ? *(const f32x4*)(p.k_weight + kk) : z4;
@@ -1435,6 +1440,8 @@ __device__ __forceinline__ void gemm256_run(const GP& p, int blk, int nwg) {
       g3_reg_epilogue_ld<EPI>(p, acc, sbias, T.m0, T.n0, T.batch, T.split, wr, wc, lane);
     else if constexpr (EPI == G3_EPI_ACC_KW)
       g3_reg_epilogue_ld<SVAE_EPI_F32_ACC>(p, acc, sbias, T.m0, T.n0, T.batch, T.split, wr, wc, lane);
+    else if constexpr (EPI == G3_EPI_F32_KW)
+      g3_reg_epilogue_ld<SVAE_EPI_F32>(p, acc, sbias, T.m0, T.n0, T.batch, T.split, wr, wc, lane);
     else
       g3_epilogue<EPI>(p, ring + ((g + 1) & 1) * G3_STAGE, acc, sbias, slabel, T.m0, T.n0, T.bn, T.batch, T.split,
                        wr, wc, tid, lane);
@@ -1614,7 +1621,9 @@ static int validate_desc(const svae_gemm_desc* d) {
   if (d->epi == SVAE_EPI_CE_PROB && !d->aux) return SVAE_EINVAL;
   if (d->epi == SVAE_EPI_ROWSCALE_GATHER && (!d->row_b || !d->gather || d->ldg % 8 || ((uintptr_t)d->gather & 15)))
     return SVAE_EINVAL;
-  if (d->k_weight && (!d->a_rowsum || d->splits != 1)) return SVAE_EINVAL;
+  // k-weighted row sums: one split (F32_ACC), or split-K slab mode (F32_ATOMIC with aux)
+  if (d->k_weight && (!d->a_rowsum || !d->a_t || (d->splits != 1 && !(d->epi == SVAE_EPI_F32_ATOMIC && d->aux))))
+    return SVAE_EINVAL;
   if (d->epi == SVAE_EPI_ROTARY_BF16 && (!d->rot_tab || d->rot_d <= 0 || d->rot_seq <= 0)) return SVAE_EINVAL;
   if ((d->epi == SVAE_EPI_GELU || d->epi == SVAE_EPI_GELU_BWD || d->epi == SVAE_EPI_CE_STATS) && !d->aux)
     return SVAE_EINVAL;
@@ -1757,8 +1766,9 @@ static int gemm_run(const svae_gemm_desc* d, svae_stream_t stream, bool* fused_d
   int impl = forced ? forced : ((ok3 && blocks256 >= 192) ? 3 : ((kslice <= 2048 && !(d->a_t && d->b_t)) ? 2 : 1));
   if (epi_new || d->k_weight || (d->a_t && !d->b_t && acc_epi && blocks256 >= 192)) impl = 3;
   if (d->k_weight) {
-    if (d->epi != SVAE_EPI_F32_ACC) return SVAE_EINVAL;
-    epi_run = G3_EPI_ACC_KW;
+    if (d->epi == SVAE_EPI_F32_ACC && d->splits == 1) epi_run = G3_EPI_ACC_KW;
+    else if (slab) epi_run = G3_EPI_F32_KW;
+    else return SVAE_EINVAL;
   }
   if (impl == 3 && !ok3) impl = 1;
   if (impl == 3) {
@@ -1811,6 +1821,10 @@ static int gemm_run(const svae_gemm_desc* d, svae_stream_t stream, bool* fused_d
       case G3_EPI_ACC_KW:
         if (d->b_t) hipLaunchKernelGGL((gemm256_kernel<true, true, G3_EPI_ACC_KW>), grid3, dim3(512), 0, s, p);
         else hipLaunchKernelGGL((gemm256_kernel<true, false, G3_EPI_ACC_KW>), grid3, dim3(512), 0, s, p);
+        break;
+      case G3_EPI_F32_KW:
+        if (!d->b_t) return SVAE_EINVAL;
+        hipLaunchKernelGGL((gemm256_kernel<true, true, G3_EPI_F32_KW>), grid3, dim3(512), 0, s, p);
         break;
       case SVAE_EPI_CE_PROB:
         hipLaunchKernelGGL((gemm256_kernel<false, false, SVAE_EPI_CE_PROB>), grid3, dim3(512), 0, s, p);

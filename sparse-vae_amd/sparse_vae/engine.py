@@ -247,6 +247,8 @@ class VAEEngine:
         # tested, measured no faster: C2 12.725 / 12.696 vs 12.648 / 12.681 ms, C4 neutral,
         # profiles/r04j_delta_ab.log); default: the attention backward's own delta pass
         self.delta_fused = os.environ.get('SVAE_DELTA_FUSED', '0') != '0'
+        self.ncu = (torch.cuda.get_device_properties(flat.device).multi_processor_count
+                    if flat.device.type == 'cuda' else 256)
         self.side = None
         if flat.device.type == 'cuda' and os.environ.get('SVAE_DW_STREAM', '0') != '0':
             self.side = torch.cuda.Stream(device=flat.device)
@@ -293,6 +295,18 @@ class VAEEngine:
         ev = torch.cuda.Event()
         ev.record(side)
         self.ws.busy[dY.untyped_storage().data_ptr()] = ev   # the next writer of dY's buffer waits for this read
+
+    def _head_dw_splits(self, V, d):
+        """Split-K factor of the vocabulary head's dW (M = V, N = d, K = T): 2 when one split leaves the last wave of
+        256 x 256 tiles partly empty (C4 / C5: 128 x 3 = 384 tiles on 256 CUs run 1.5 waves; two splits, 768 tiles,
+        run 3 full ones: `profiles/r04_head_dw_probe_c4.log`), else 1 (C2: 256 tiles). SVAE_HEAD_DW_SPLITS > 0 forces it."""
+        env = int(os.environ.get('SVAE_HEAD_DW_SPLITS', '0') or 0)   # (0: chosen here)
+        if env > 0:
+            return env
+        tiles = -(-V // 256) * -(-d // 256)
+        ncu = self.ncu
+        eff = lambda s: tiles * s / (ncu * -(-(tiles * s) // ncu))   # noqa: E731
+        return 2 if tiles >= ncu and eff(2) > eff(1) + 0.1 else 1
 
     def _dw_pair(self, j0, j1):
         """Two _dw's ((dY, X, wname, rows, n_out, n_in[, ldy, ldx, bias])) in one paired launch (svae_gemm_pair):
@@ -919,8 +933,14 @@ class VAEEngine:
             K.ce_prob_bwd_prep(hh, sv['lse'], sv['coff'], sv['chunk_w'], sv['labels'], gs[0:1], T, L, nch, clen, d, hh_r,
                                r_t, q_t, dbias)
             # (a K-contiguous B, (r . hh)^T, measured the same: 1069 vs 1079 us; the k-weighted row sums cost ~15 %)
-            K.gemm(logits, hh_r, P.g('input_layer.0.weight'), V, d, T, a_t=True, b_t=True, lda=V, ldb=d, ldc=d,
-                   epi=EPI_F32_ACC, a_rowsum=dbias, k_weight=r_t)
+            s = self._head_dw_splits(V, d)
+            if s == 1:
+                K.gemm(logits, hh_r, P.g('input_layer.0.weight'), V, d, T, a_t=True, b_t=True, lda=V, ldb=d, ldc=d,
+                       epi=EPI_F32_ACC, a_rowsum=dbias, k_weight=r_t)
+            else:   # split-K slabs (deterministic C), summed into the gradient by slab_reduce
+                slab = ws.get('b.head_dw_slab', (s * V * d,), f32)
+                K.gemm(logits, hh_r, P.g('input_layer.0.weight'), V, d, T, a_t=True, b_t=True, lda=V, ldb=d, ldc=d,
+                       epi=EPI_F32_ATOMIC, splits=s, aux=slab, a_rowsum=dbias, k_weight=r_t)
             W = P.w('input_layer.0.weight')
             K.gemm(logits, P.wT('input_layer.0.weight', V, d), dhh, T, d, V, epi=EPI_ROWSCALE_GATHER,
                    labels=sv['labels'], row_a=r_t, row_b=q_t, gather=W, ldg=d)

@@ -72,6 +72,30 @@ def test_gemm256_at_rowsum_k_weight_exact(b_t):
         assert bad.numel() == 0, (use_kw, bad[:16].tolist(), (rs - ref)[bad[:16]].tolist())
 
 
+@pytest.mark.parametrize('splits', [2, 3])
+def test_gemm256_k_weight_split_slab_exact(splits):
+    """The k-weighted row sums in split-K slab mode (the vocabulary head's dW at C4 / C5: 384 tiles run as 2 x 384):
+    each split stores its partial tile into aux, slab_reduce adds them into C, the row sums of every split's K range
+    add into a_rowsum; bit-exact on integer data (ragged N, K not a multiple of splits x 64), repeated."""
+    g = torch.Generator(device=dev).manual_seed(9)
+    Kk, M, Nn = 4160, 16384, 776
+    A = torch.randint(-2, 3, (Kk, M), device=dev, generator=g).float()
+    B = torch.randint(-2, 3, (Kk, Nn), device=dev, generator=g).float()
+    kw = torch.randint(-2, 3, (Kk,), device=dev, generator=g).float()
+    slab = torch.empty(splits * M * Nn, device=dev)
+    ref_c = 1 + A.t() @ B
+    ref_rs = 3 + (A * kw[:, None]).sum(0)
+    for _ in range(3):
+        C = torch.ones(M, Nn, device=dev)
+        rs = torch.full((M,), 3.0, device=dev)
+        K.gemm(A.bfloat16(), B.bfloat16(), C, M, Nn, Kk, a_t=True, b_t=True, ldb=Nn, epi=N.EPI_F32_ATOMIC,
+               splits=splits, aux=slab, a_rowsum=rs, k_weight=kw)
+        torch.cuda.synchronize()
+        assert torch.equal(C, ref_c)
+        bad = (rs != ref_rs).nonzero().flatten()
+        assert bad.numel() == 0, (bad[:16].tolist(), (rs - ref_rs)[bad[:16]].tolist())
+
+
 def test_gemm256_split_k_rowsum_exact():
     """dW layout on the 256x256 kernel: split-K f32 atomics + fused bias-gradient row sums, and the
     unsplit f32 accumulate (the tied head's dW), all bit-exact on integer data."""
