@@ -4,6 +4,9 @@
 // Reference: nn.LayerNorm(d) in TransformerLayer (transformer_layer.py:23-24, 39-40, 47, 52, 56) and the
 // output head (transformer_language_model.py:59). HBM-bound: forward moves 4d (f32 in) + 2d (bf16 out)
 // bytes per row; backward reads dy (2d), x (4d), dres (4d) and writes dx (4d + 2d).
+#include <algorithm>
+#include <cstdlib>
+
 #include "common.h"
 #include "../../include/svae.h"
 
@@ -27,89 +30,87 @@ __device__ __forceinline__ void store4_bf(bf16* p, f32x4 v) {
   *(bf16x4*)p = (bf16x4){f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
 }
 
+// column of the lane's k-th float4 in a row: even MAXV = runs of 8 columns (two float4 each), odd = runs of 4
+template <int MAXV>
+__device__ __forceinline__ int ln_col(int lane, int k) {
+  return MAXV % 2 == 0 ? (lane + 64 * (k >> 1)) * 8 + 4 * (k & 1) : (lane + 64 * k) * 4;
+}
+template <typename T, int MAXV>
+__device__ __forceinline__ void ln_load_row(const T* __restrict__ xr, int lane, int D, f32x4 (&dst)[MAXV]) {
+#pragma unroll
+  for (int k = 0; k < MAXV; ++k) {
+    const int c = ln_col<MAXV>(lane, k);
+    dst[k] = (c < D) ? load4<T>(xr + c) : (f32x4){0.f, 0.f, 0.f, 0.f};
+  }
+}
+
+// A wave walks rows wave, wave + waves, ... (the launcher sizes the grid so a few rows fall to each wave) with the
+// next row's loads issued before the current row's reductions and stores: the loads stay in flight across rows
+// instead of one load round trip per wave launch.
 template <typename T, int MAXV>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, const float* __restrict__ w,
                                                      const float* __restrict__ b, bf16* __restrict__ y,
                                                      float* __restrict__ mean_out, float* __restrict__ rstd_out,
                                                      int rows, int D) {
+  // even MAXV: D % 8 == 0 (checked by the launcher), each lane owns runs of 8 consecutive columns, so the bf16 output
+  // is one 16-B store per run (the 4-column layout stores 8 B per lane); odd MAXV: runs of 4 columns
+  constexpr bool W8 = MAXV % 2 == 0;
   const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int nw = gridDim.x * 4;
+  int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
-  const T* xr = x + (long long)row * D;
-  if constexpr (MAXV % 2 == 0) {
-    // D % 8 == 0 (checked by the launcher): each lane owns runs of 8 consecutive columns, so the bf16 output is one
-    // 16-B store per run (the 4-column layout below stores 8 B per lane)
-    constexpr int NR = MAXV / 2;
-    f32x4 v[NR][2];
+  f32x4 v[MAXV], vn[MAXV];
+  ln_load_row<T, MAXV>(x + (long long)row * D, lane, D, v);
+#pragma nounroll
+  while (true) {
+    const int next = row + nw;
+    if (next < rows) ln_load_row<T, MAXV>(x + (long long)next * D, lane, D, vn);
     float s = 0.f;
 #pragma unroll
-    for (int j = 0; j < NR; ++j) {
-      const int c = (lane + 64 * j) * 8;
-      v[j][0] = (c < D) ? load4<T>(xr + c) : (f32x4){0.f, 0.f, 0.f, 0.f};
-      v[j][1] = (c < D) ? load4<T>(xr + c + 4) : (f32x4){0.f, 0.f, 0.f, 0.f};
-      s += (v[j][0][0] + v[j][0][1]) + (v[j][0][2] + v[j][0][3]) + (v[j][1][0] + v[j][1][1]) + (v[j][1][2] + v[j][1][3]);
-    }
+    for (int k = 0; k < MAXV; ++k) s += (v[k][0] + v[k][1]) + (v[k][2] + v[k][3]);
     const float mean = wave_sum(s) / D;
     float sq = 0.f;
 #pragma unroll
-    for (int j = 0; j < NR; ++j) {
-      const int c = (lane + 64 * j) * 8;
-      if (c < D) {
+    for (int k = 0; k < MAXV; ++k) {
+      const bool in = ln_col<MAXV>(lane, k) < D;
 #pragma unroll
-        for (int h = 0; h < 2; ++h)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) { const float t = v[j][h][e] - mean; sq += t * t; }
-      }
+      for (int e = 0; e < 4; ++e) { const float t = in ? v[k][e] - mean : 0.f; sq += t * t; }
     }
     const float rstd = rsqrtf(wave_sum(sq) / D + 1e-5f);
+    bf16* yr = y + (long long)row * D;
+    if constexpr (W8) {
 #pragma unroll
-    for (int j = 0; j < NR; ++j) {
-      const int c = (lane + 64 * j) * 8;
-      if (c < D) {
-        bf16x8 o;
+      for (int j = 0; j < MAXV / 2; ++j) {
+        const int c = ln_col<MAXV>(lane, 2 * j);
+        if (c < D) {
+          bf16x8 o;
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const f32x4 ww = *(const f32x4*)(w + c + 4 * h), bb = *(const f32x4*)(b + c + 4 * h);
+          for (int h = 0; h < 2; ++h) {
+            const f32x4 ww = *(const f32x4*)(w + c + 4 * h), bb = *(const f32x4*)(b + c + 4 * h);
 #pragma unroll
-          for (int e = 0; e < 4; ++e) o[4 * h + e] = f2bf((v[j][h][e] - mean) * rstd * ww[e] + bb[e]);
+            for (int e = 0; e < 4; ++e) o[4 * h + e] = f2bf((v[2 * j + h][e] - mean) * rstd * ww[e] + bb[e]);
+          }
+          *(bf16x8*)(yr + c) = o;
         }
-        *(bf16x8*)(y + (long long)row * D + c) = o;
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < MAXV; ++k) {
+        const int c = ln_col<MAXV>(lane, k);
+        if (c < D) {
+          const f32x4 ww = *(const f32x4*)(w + c), bb = *(const f32x4*)(b + c);
+          f32x4 o;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] = (v[k][e] - mean) * rstd * ww[e] + bb[e];
+          store4_bf(yr + c, o);
+        }
       }
     }
     if (lane == 0) { mean_out[row] = mean; rstd_out[row] = rstd; }
-    return;
+    if (next >= rows) break;
+    for (int k = 0; k < MAXV; ++k) v[k] = vn[k];   // (register renames once unrolled by the optimiser)
+    row = next;
   }
-  f32x4 v[MAXV];
-  float s = 0.f;
-#pragma unroll
-  for (int j = 0; j < MAXV; ++j) {
-    const int c = (lane + 64 * j) * 4;
-    v[j] = (c < D) ? load4<T>(xr + c) : (f32x4){0.f, 0.f, 0.f, 0.f};
-    s += v[j][0] + v[j][1] + v[j][2] + v[j][3];
-  }
-  const float mean = wave_sum(s) / D;
-  float sq = 0.f;
-#pragma unroll
-  for (int j = 0; j < MAXV; ++j) {
-    const int c = (lane + 64 * j) * 4;
-    if (c < D) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) { const float t = v[j][e] - mean; sq += t * t; }
-    }
-  }
-  const float rstd = rsqrtf(wave_sum(sq) / D + 1e-5f);
-#pragma unroll
-  for (int j = 0; j < MAXV; ++j) {
-    const int c = (lane + 64 * j) * 4;
-    if (c < D) {
-      const f32x4 ww = *(const f32x4*)(w + c), bb = *(const f32x4*)(b + c);
-      f32x4 o;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) o[e] = (v[j][e] - mean) * rstd * ww[e] + bb[e];
-      store4_bf(y + (long long)row * D + c, o);
-    }
-  }
-  if (lane == 0) { mean_out[row] = mean; rstd_out[row] = rstd; }
 }
 
 // Residual add + dropout + LayerNorm, fused (the TransformerLayer's "x = x + y" followed by the next LayerNorm,
@@ -373,7 +374,10 @@ __global__ __launch_bounds__(256) void colsum_kernel(const T* __restrict__ in, i
 SVAE_EXPORT int svae_layernorm_fwd(const void* x, int32_t x_dtype, const float* w, const float* b, void* y,
                                    float* mean, float* rstd, int32_t rows, int32_t D, svae_stream_t stream) {
   if (!x || !w || !b || !y || !mean || !rstd || rows <= 0 || D <= 0 || D % 4 || D > 1024) return SVAE_EINVAL;
-  dim3 grid((rows + 3) / 4);
+  // rows per wave: the grid holds at most SVAE_LN_FWD_BLOCKS blocks of 4 waves (0: one row per wave)
+  static const int cap = [] { const char* e = getenv("SVAE_LN_FWD_BLOCKS"); return e ? atoi(e) : 1024; }();
+  const int need = (rows + 3) / 4;
+  dim3 grid((unsigned)(cap > 0 ? std::min(need, cap) : need));
   hipStream_t s = (hipStream_t)stream;
 #define SVAE_LN_FWD(MV)                                                                                            \
   do {                                                                                                             \
