@@ -1287,12 +1287,12 @@ __device__ __forceinline__ void gemm256_run(const GP& p, int blk, int nwg) {
       const bool do_rs = AT && p.a_rowsum && T.bn < 2;
       // p.dma_stagger: the two waves of a SIMD (wr 0 and 1, same wc) issue their pieces of the next K-tile at different
       // times -- wr 0 here, wr 1 after its first MFMA quadrant -- so one wave's DMA issue runs beside the other's MFMAs
-      const bool late = !IS_KW && p.dma_stagger && wr == 1 && kt + 1 < T.nk;   // (wave-uniform)
+      // (the k-weighted forms: form 0 loads the weights from global memory at the use, whose wait would also wait for
+      // the late pieces, so no stagger; the LDS-slot diagnostic forms stagger)
+      const bool late = (!IS_KW || KW_FORM > 0) && p.dma_stagger && wr == 1 && kt + 1 < T.nk;   // (wave-uniform)
       if (kt + 1 < T.nk) {
-        if (!late) {
-          g3_issue<AT, BT>(p, T.A, T.B, sa, sb, T.m0, T.n0, T.kbeg + (kt + 1) * 64, T.kend, nxt, wave);
-          kw_issue(T.kbeg + (kt + 1) * 64, T.kend, (g + 1) & 1);
-        }
+        if (!late) g3_issue<AT, BT>(p, T.A, T.B, sa, sb, T.m0, T.n0, T.kbeg + (kt + 1) * 64, T.kend, nxt, wave);
+        kw_issue(T.kbeg + (kt + 1) * 64, T.kend, (g + 1) & 1);   // (every wave here, late or not)
       } else if (has_next) {   // the next tile's first K-tile, in flight during this tile's epilogue
         const G3Tile TN = g3_tile(p, t3n);
         if (TN.nk > 0) {
