@@ -1581,27 +1581,44 @@ __global__ __launch_bounds__(1024) void gemm_skinny_kernel(GP p) {
 }
 
 // C[m][n] += sum over splits of slab[s][m][n] (slab rows of N floats); 4 columns per thread
-__global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restrict__ slab, float* __restrict__ C,
-                                                          int M, int N, long long ldc, int splits) {
-  const int N4 = N / 4;
-  const long long total = (long long)M * N4, plane = (long long)M * N;
-  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+struct SlabRed {
+  const float* slab;
+  float* C;
+  int M, N;
+  long long ldc;
+  int splits;
+};
+__device__ __forceinline__ void slab_reduce_range(const SlabRed& r, int blk, int nblk) {
+  const int N4 = r.N / 4;
+  const long long total = (long long)r.M * N4, plane = (long long)r.M * r.N;
+  for (long long i = (long long)blk * 256 + threadIdx.x; i < total; i += (long long)nblk * 256) {
     const long long m = i / N4;
     const int n = (int)(i - m * N4) * 4;
-    const float* src = slab + m * N + n;
+    const float* src = r.slab + m * r.N + n;
     f32x4 acc = *(const f32x4*)src;
-    for (int s = 1; s < splits; ++s) acc += *(const f32x4*)(src + s * plane);
-    f32x4* dst = (f32x4*)(C + m * ldc + n);
+    for (int s = 1; s < r.splits; ++s) acc += *(const f32x4*)(src + s * plane);
+    f32x4* dst = (f32x4*)(r.C + m * r.ldc + n);
     *dst = *dst + acc;
   }
+}
+__global__ __launch_bounds__(256) void slab_reduce_kernel(SlabRed r) { slab_reduce_range(r, blockIdx.x, gridDim.x); }
+// the two slab reductions of a paired dW launch in one launch: blocks [0, nb0) take r0, the rest r1 (one launch
+// fewer per pair: ~1.6 us of GPU-side launch cost each, scripts/bubble_probe.py)
+__global__ __launch_bounds__(256) void slab_reduce2_kernel(SlabRed r0, SlabRed r1, int nb0) {
+  if ((int)blockIdx.x < nb0) slab_reduce_range(r0, blockIdx.x, nb0);
+  else slab_reduce_range(r1, blockIdx.x - nb0, (int)gridDim.x - nb0);
 }
 
 }  // namespace
 
+static SlabRed slab_red(const svae_gemm_desc* d) {
+  return SlabRed{(const float*)d->aux, (float*)d->C, d->M, d->N, (long long)d->ldc, d->splits};
+}
+static long long slab_blocks(const svae_gemm_desc* d) {
+  return std::min(4096LL, ((long long)d->M * (d->N / 4) + 255) / 256);
+}
 static int launch_slab_reduce(const svae_gemm_desc* d, hipStream_t s) {
-  const long long work = (long long)d->M * (d->N / 4);
-  hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)min(4096LL, (work + 255) / 256)), dim3(256), 0, s,
-                     (const float*)d->aux, (float*)d->C, d->M, d->N, (long long)d->ldc, d->splits);
+  hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)slab_blocks(d)), dim3(256), 0, s, slab_red(d));
   SVAE_LAUNCH_CHECK();
   return SVAE_OK;
 }
@@ -1922,8 +1939,15 @@ SVAE_EXPORT int svae_gemm_pair(const svae_gemm_desc* d0, const svae_gemm_desc* d
   hipLaunchKernelGGL((gemm256_pair_kernel<true, true, SVAE_EPI_F32>), dim3((unsigned)(q.nb0 + nb[1])), dim3(512), 0, s,
                      q);
   SVAE_LAUNCH_CHECK();
-  if (const int rc = launch_slab_reduce(d0, s)) return rc;
-  return launch_slab_reduce(d1, s);
+  static const int two_env = [] { const char* e = getenv("SVAE_SLAB2"); return e ? atoi(e) : 1; }();
+  if (!two_env) {   // (A/B: one launch per GEMM)
+    if (const int rc = launch_slab_reduce(d0, s)) return rc;
+    return launch_slab_reduce(d1, s);
+  }
+  const long long b0 = slab_blocks(d0), b1 = slab_blocks(d1);
+  hipLaunchKernelGGL(slab_reduce2_kernel, dim3((unsigned)(b0 + b1)), dim3(256), 0, s, slab_red(d0), slab_red(d1), (int)b0);
+  SVAE_LAUNCH_CHECK();
+  return SVAE_OK;
 }
 
 #ifdef SVAE_STAMPS
