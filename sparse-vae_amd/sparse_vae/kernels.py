@@ -2,6 +2,7 @@
 arguments it relies on and raises on a non-zero status. All work is enqueued on torch's current HIP
 stream; nothing here synchronises."""
 import ctypes
+import os
 
 import torch
 
@@ -115,27 +116,52 @@ def linear_dw(dY, X, Wgrad, rows, n_out, n_in, ldy=None, ldx=None, bgrad=None):
 
 
 def pair_splits(shapes):
-    """Split-K count for two weight gradients launched together ((n_out, n_in, rows) each): one round of <= 256
-    256x256 blocks over both, K-slices >= 512 rows. None when either would not split (then run them apart)."""
-    tiles = sum(-(-m // 256) * -(-n // 256) for m, n, _ in shapes)
-    s = 256 // tiles if tiles else 0
-    s = min([s] + [rows // 512 for _, _, rows in shapes])
-    return s if s >= 2 else None
+    """Split-K counts (s0, s1) for two weight gradients launched together ((n_out, n_in, rows) each): one round of
+    <= 256 256x256 blocks over both, every block's K-slice about the same length (rows / s, >= 512 rows), so a GEMM
+    over many more rows than its partner is split further (C2's encoder pair of a 4096-row and a 32768-row dW: 4 and
+    30 splits, 256 blocks, instead of 8 and 8, 96 blocks of which 64 ran 64 K-tiles). None when either would not
+    split (then run them apart). SVAE_DW_PAIR_EQUAL=1: one common count (the round-3 rule), for A/B."""
+    tiles = [-(-m // 256) * -(-n // 256) for m, n, _ in shapes]
+    rows = [r for _, _, r in shapes]
+    if not all(tiles):
+        return None
+    if os.environ.get('SVAE_DW_PAIR_EQUAL', '0') != '0':
+        c = min([256 // sum(tiles)] + [r // 512 for r in rows])
+        return (c, c) if c >= 2 else None
+    cap = [r // 512 for r in rows]
+    if min(cap) < 2:
+        return None
+    work = sum(t * r for t, r in zip(tiles, rows))
+    slice_rows = max(512.0, work / 256.0)
+    sp = [min(c, max(2, round(r / slice_rows))) for r, c in zip(rows, cap)]
+    while sum(t * x for t, x in zip(tiles, sp)) > 256:
+        # shorten the longest per-block slice's partner: drop a split where the slice is shortest
+        i = min((k for k in range(2) if sp[k] > 2), key=lambda k: rows[k] / sp[k], default=None)
+        if i is None:
+            return None
+        sp[i] -= 1
+    # the kernel's K-slice is a multiple of 64 rows: count only the non-empty slices
+    sp = [-(-r // (-(-(-(-r // x)) // 64) * 64)) for r, x in zip(rows, sp)]
+    longest = max(r / x for r, x in zip(rows, sp))
+    for k in range(2):   # no more slabs than the longest slice needs
+        while sp[k] > 2 and rows[k] / (sp[k] - 1) <= longest:
+            sp[k] -= 1
+    return tuple(sp)
 
 
 def linear_dw_pair(j0, j1):
     """Two linear_dw's (each (dY, X, Wgrad, rows, n_out, n_in, ldy, ldx, bgrad)) as one paired launch: each needs
     only ~half the split-K slices it would take alone to fill the chip (half the slab bytes written and reduced).
     Falls back to two linear_dw calls for shapes that would not split."""
-    s = pair_splits([(j[4], j[5], j[3]) for j in (j0, j1)])
-    if s is None:
+    sp = pair_splits([(j[4], j[5], j[3]) for j in (j0, j1)])
+    if sp is None:
         linear_dw(*j0[:8], bgrad=j0[8])
         linear_dw(*j1[:8], bgrad=j1[8])
         return
-    n0, n1 = s * j0[4] * j0[5], s * j1[4] * j1[5]
+    n0, n1 = sp[0] * j0[4] * j0[5], sp[1] * j1[4] * j1[5]
     slab = _slab_workspace(n0 + n1, j0[0].device)
     gs = []
-    for j, aux in ((j0, slab[:n0]), (j1, slab[n0:n0 + n1])):
+    for j, aux, s in ((j0, slab[:n0], sp[0]), (j1, slab[n0:n0 + n1], sp[1])):
         dY, X, Wg, rows, n_out, n_in, ldy, ldx, bg = j
         gs.append(((dY, X, Wg, n_out, n_in, rows),
                    dict(a_t=True, b_t=True, lda=ldy or n_out, ldb=ldx or n_in, ldc=n_in, epi=N.EPI_F32_ATOMIC,

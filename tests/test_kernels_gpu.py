@@ -119,14 +119,18 @@ def test_gemm256_split_k_rowsum_exact():
 @pytest.mark.parametrize('shapes', [((2048, 512, True), (512, 2048, False), 32768),    # FFN pair (8 splits)
                                     ((512, 512, True), (1536, 512, True), 32768),     # out-proj + QKV (16 splits)
                                     ((512, 512, True), (1024, 520, True), 4104),      # ragged N / K tail
-                                    ((512, 512, True), (1536, 512, False), 600)])     # too short to split: apart
+                                    ((512, 512, True), (1536, 512, False), 600),      # too short to split: apart
+                                    ((512, 512, True, 4096), (1024, 512, True, 32768), None),    # C2 encoder pair:
+                                    ((768, 768, True, 4096), (1536, 768, True, 65536), None)])   # unequal splits
 def test_linear_dw_pair_exact(shapes):
     """Two weight gradients in one paired launch (svae_gemm_pair, split-K slabs) equal dY^T X (+ the bias row sums)
-    exactly on integer data, each into its own destination."""
-    (m0, n0, b0), (m1, n1, b1), rows = shapes
-    g = torch.Generator(device=dev).manual_seed(m0 + n1 + rows)
+    exactly on integer data, each into its own destination; the two may run over different row counts (then each
+    gets its own split count, kernels.pair_splits)."""
+    s0, s1, rows = shapes
+    specs = [(t[0], t[1], t[2], t[3] if len(t) > 3 else rows) for t in (s0, s1)]
+    g = torch.Generator(device=dev).manual_seed(specs[0][0] + specs[1][1] + specs[1][3])
     jobs, refs = [], []
-    for n_out, n_in, with_bias in ((m0, n0, b0), (m1, n1, b1)):
+    for n_out, n_in, with_bias, rows in specs:
         dY = torch.randint(-2, 3, (rows, n_out), device=dev, generator=g).float()
         X = torch.randint(-2, 3, (rows, n_in), device=dev, generator=g).float()
         Wg = torch.full((n_out, n_in), 0.5, device=dev)
