@@ -634,9 +634,29 @@ __global__ __launch_bounds__(256) void dq_finalize_kernel(const float* __restric
 __global__ __launch_bounds__(256) void transpose_blocks_kernel(const bf16* __restrict__ src, bf16* __restrict__ dst,
                                                                const long long* __restrict__ table, int nb) {
   __shared__ unsigned short t[64][66];
+  __shared__ int sfirst[256];
   const int tile = blockIdx.x;
+  // the block this tile belongs to: the first tiles of up to 256 blocks come in one coalesced load and are searched
+  // in LDS (a dependent global load per table entry cost the last tiles ~100 L2 round trips); more blocks: a binary
+  // search over the table in global memory
   int b = 0;
-  while (b + 1 < nb && table[(b + 1) * 4 + 3] <= tile) ++b;
+  if (nb <= 256) {
+    for (int i = threadIdx.x; i < nb; i += 256) sfirst[i] = (int)table[i * 4 + 3];
+    __syncthreads();
+    int lo = 0, hi = nb - 1;   // last b with first_tile[b] <= tile
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (sfirst[mid] <= tile) lo = mid; else hi = mid - 1;
+    }
+    b = lo;
+  } else {
+    int lo = 0, hi = nb - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (table[mid * 4 + 3] <= tile) lo = mid; else hi = mid - 1;
+    }
+    b = lo;
+  }
   const long long off = table[b * 4], rows = table[b * 4 + 1], cols = table[b * 4 + 2];
   const int local = tile - (int)table[b * 4 + 3];
   const int tcols = (int)((cols + 63) / 64);

@@ -737,3 +737,24 @@ def test_gemm_delta_epilogue(M, Nn, Kk, hd, seq):
     H = Nn // hd
     ref = (C.float() * o32).view(M // seq, seq, H, hd).sum(-1).permute(0, 2, 1).reshape(-1)
     torch.testing.assert_close(delta, ref, rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize('nb', [5, 300])   # block table searched in LDS (<= 256 blocks) / in global memory
+def test_transpose_blocks(nb):
+    """svae_transpose_blocks (the transposed bf16 weight shadows): every block of the table transposed exactly, with
+    ragged shapes (rows, cols multiples of 8, not of 64)."""
+    g = torch.Generator().manual_seed(nb)
+    shapes = [(8 * int(torch.randint(1, 40, (1,), generator=g)), 8 * int(torch.randint(1, 40, (1,), generator=g)))
+              for _ in range(nb)]
+    rows_tab, off, tiles = [], 0, 0
+    for r, c in shapes:
+        rows_tab.append((off, r, c, tiles))
+        off += r * c
+        tiles += -(-r // 64) * -(-c // 64)
+    src = torch.randn(off, device=dev).bfloat16()
+    dst = torch.zeros(off, device=dev, dtype=torch.bfloat16)
+    table = torch.tensor(rows_tab, dtype=torch.int64, device=dev).flatten()
+    K.transpose_blocks(src, dst, table, nb, tiles)
+    torch.cuda.synchronize()
+    for o, r, c, _ in rows_tab:
+        assert torch.equal(dst[o:o + r * c].view(c, r), src[o:o + r * c].view(r, c).t())
