@@ -739,13 +739,14 @@ __global__ __launch_bounds__(256) void radam_kernel(float* __restrict__ p, bf16*
               wd = scal[7];
   const float step = lr / bcm, decay = 1.0f - lr * wd;
   const long long n4 = n / 4;   // n % 4 == 0 (checked on the host): 16-B vectors
-  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
-    const f32x4 gi = ((const f32x4*)g)[i] * coef;
-    const f32x4 mi = ((const f32x4*)m)[i] * b1 + (1.0f - b1) * gi;
-    const f32x4 vi = ((const f32x4*)v)[i] * b2 + (1.0f - b2) * gi * gi;
-    ((f32x4*)m)[i] = mi;
-    ((f32x4*)v)[i] = vi;
-    f32x4 pi = ((const f32x4*)p)[i] * decay;
+  auto update = [&](long long i, f32x4 gi, f32x4 m0, f32x4 v0, f32x4 p0) {
+    gi *= coef;
+    const f32x4 mi = m0 * b1 + (1.0f - b1) * gi;
+    const f32x4 vi = v0 * b2 + (1.0f - b2) * gi * gi;
+    // the moments are read again only by the next step's update: nontemporal
+    __builtin_nontemporal_store(mi, (f32x4*)m + i);
+    __builtin_nontemporal_store(vi, (f32x4*)v + i);
+    f32x4 pi = p0 * decay;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       if (rho_ok != 0.f) pi[e] -= step * (mi[e] / (sqrtf(vi[e]) / bcv + eps));
@@ -753,7 +754,21 @@ __global__ __launch_bounds__(256) void radam_kernel(float* __restrict__ p, bf16*
     }
     ((f32x4*)p)[i] = pi;
     if (pbf) ((bf16x4*)pbf)[i] = (bf16x4){f2bf(pi[0]), f2bf(pi[1]), f2bf(pi[2]), f2bf(pi[3])};
+  };
+  // two vectors per thread per iteration: all eight 16-B loads issued before the first update
+  const long long stride = (long long)gridDim.x * 256;
+  long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  for (; i + stride < n4; i += 2 * stride) {
+    const long long j = i + stride;
+    const f32x4 ga = ((const f32x4*)g)[i], gb = ((const f32x4*)g)[j];
+    const f32x4 ma = __builtin_nontemporal_load((const f32x4*)m + i), mb = __builtin_nontemporal_load((const f32x4*)m + j);
+    const f32x4 va = __builtin_nontemporal_load((const f32x4*)v + i), vb = __builtin_nontemporal_load((const f32x4*)v + j);
+    const f32x4 pa = ((const f32x4*)p)[i], pb = ((const f32x4*)p)[j];
+    update(i, ga, ma, va, pa);
+    update(j, gb, mb, vb, pb);
   }
+  if (i < n4)
+    update(i, ((const f32x4*)g)[i], ((const f32x4*)m)[i], ((const f32x4*)v)[i], ((const f32x4*)p)[i]);
 }
 
 // In-place clip_grad_norm_ (language_model.py:120-122) for a micro-step that is not followed by an optimiser step
