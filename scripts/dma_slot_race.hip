@@ -24,7 +24,7 @@ __device__ __forceinline__ void pieces(const u32x4& rs, char* stage, int wave, i
   }
 }
 
-template <bool LATE, bool READ_EARLY, bool SLOT_LOW>
+template <bool LATE, bool READ_EARLY, bool SLOT_LOW, bool TR = false>
 __global__ __launch_bounds__(512, 1) void race_kernel(const float* __restrict__ w, const bf16* __restrict__ src,
                                                       int src_pieces, int ntiles, unsigned* __restrict__ bad,
                                                       float* __restrict__ sink) {
@@ -56,8 +56,16 @@ __global__ __launch_bounds__(512, 1) void race_kernel(const float* __restrict__ 
   };
   auto quadrant = [&](const char* st, int q) {
     bf16x8 a[4], b;
+    if constexpr (TR) {   // transposed reads (ds_read_b64_tr_b16 pairs), as the k-weighted GEMM's A operand
 #pragma unroll
-    for (int i = 0; i < 4; ++i) a[i] = *(const bf16x8*)(st + ((wave * 4 + i + q) % 64) * 1024 + lane * 16);
+      for (int i = 0; i < 4; ++i) {
+        const char* base = st + ((wave * 4 + i + q) % 64) * 1024 + (lane & 15) * 64 + (lane >> 4) * 8;
+        a[i] = cat44(lds_read_tr(base), lds_read_tr(base + 32));
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = *(const bf16x8*)(st + ((wave * 4 + i + q) % 64) * 1024 + lane * 16);
+    }
     b = *(const bf16x8*)(st + ((wave + 32 + q) % 64) * 1024 + lane * 16);
 #pragma unroll
     for (int r = 0; r < 4; ++r)
@@ -109,6 +117,8 @@ extern "C" __attribute__((visibility("default"))) int dma_race_run(int variant, 
     case 1: hipLaunchKernelGGL((race_kernel<true, true, false>), g, b, 0, s, w, sp, src_pieces, ntiles, bad, sink); break;
     case 2: hipLaunchKernelGGL((race_kernel<true, false, false>), g, b, 0, s, w, sp, src_pieces, ntiles, bad, sink); break;
     case 3: hipLaunchKernelGGL((race_kernel<true, true, true>), g, b, 0, s, w, sp, src_pieces, ntiles, bad, sink); break;
+    case 4: hipLaunchKernelGGL((race_kernel<true, true, false, true>), g, b, 0, s, w, sp, src_pieces, ntiles, bad, sink); break;
+    case 5: hipLaunchKernelGGL((race_kernel<false, true, false, true>), g, b, 0, s, w, sp, src_pieces, ntiles, bad, sink); break;
     default: return 1;
   }
   return hipGetLastError() == hipSuccess ? 0 : 2;

@@ -4,6 +4,7 @@ wave, over repeated launches.
   variant 1: wave row 1 issues its pieces after quadrant 1 (stagger), same reads
   variant 2: stagger, every slot read after quadrant 4
   variant 3: stagger, slots below the ring (offset 0) instead of at 138 KiB
+  variant 4: as 1 with transposed (ds_read_b64_tr_b16) operand reads; variant 5: as 4 without the stagger
 """
 import ctypes
 import os
@@ -23,7 +24,7 @@ src = torch.randn(src_pieces * 512, device=dev).bfloat16()
 sink = torch.zeros(512, device=dev)
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
 for nblocks in (32, 256):
-    for variant in (0, 1, 2, 3):
+    for variant in (0, 1, 2, 3, 4, 5):
         bad = torch.zeros(8, device=dev, dtype=torch.int32)
         runs_bad = 0
         for _ in range(reps):
