@@ -140,6 +140,17 @@ int svae_layernorm_nblk(int32_t rows);
 int svae_colsum(const void* in, int32_t in_dtype, int32_t rows, int32_t cols, int64_t ld, float* out,
                 int32_t accumulate, svae_stream_t stream);
 
+/* Up to SVAE_COLSUM_MAX f32 column sums in one launch, each added into its own out (the LayerNorm-affine gradients
+ * of one layer's LayerNorm backwards). in / out 16-B aligned, cols and ld multiples of 4. */
+#define SVAE_COLSUM_MAX 8
+typedef struct svae_colsum_seg {
+  const float* in;
+  float* out;
+  int64_t ld;
+  int32_t rows, cols;
+} svae_colsum_seg;
+int svae_colsum_multi(const svae_colsum_seg* segs, int32_t n, svae_stream_t stream);
+
 /* ---- Flash attention (dense path of Attention.forward, attention.py:51-105) ------------------------
  * q/k/v/o: bf16 rows of H*hd (token-major, head-interleaved, exactly the nn.Linear output layout),
  * row strides sq/sk/sv/so elements, batch strides bq/bk/bv/bo elements (bq = 0 for learned queries).

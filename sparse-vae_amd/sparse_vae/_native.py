@@ -61,6 +61,14 @@ class AttnDesc(ctypes.Structure):
     ]
 
 
+COLSUM_MAX = 8
+
+
+class ColsumSeg(ctypes.Structure):
+    """svae_colsum_seg (include/svae.h)."""
+    _fields_ = [('inp', c_void_p), ('out', c_void_p), ('ld', c_int64), ('rows', c_int32), ('cols', c_int32)]
+
+
 _SIGS = {
     'svae_gemm': [ctypes.POINTER(GemmDesc), c_void_p],
     'svae_gemm_pair': [ctypes.POINTER(GemmDesc), ctypes.POINTER(GemmDesc), c_void_p],
@@ -75,6 +83,7 @@ _SIGS = {
                                 c_void_p, c_void_p, c_void_p],
     'svae_layernorm_nblk': [c_int32],
     'svae_colsum': [c_void_p, c_int32, c_int32, c_int32, c_int64, c_void_p, c_int32, c_void_p],
+    'svae_colsum_multi': [c_void_p, c_int32, c_void_p],
     'svae_attn_fwd': [ctypes.POINTER(AttnDesc), c_void_p],
     'svae_attn_bwd': [ctypes.POINTER(AttnDesc), c_void_p],
     'svae_attn_dq_part_elems': [c_int32, c_int32, c_int32, c_int32, c_int32],

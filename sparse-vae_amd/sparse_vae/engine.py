@@ -20,6 +20,7 @@ from collections import OrderedDict
 import torch
 
 from . import kernels as K
+from ._native import COLSUM_MAX
 from ._native import EPI_BF16, EPI_F32, EPI_F32_ACC, EPI_GELU, EPI_GELU_BWD, EPI_DROPOUT_RESID, \
     EPI_ROTARY_BF16, EPI_CE_STATS, EPI_F32_ATOMIC, EPI_CE_PROB, EPI_ROWSCALE_GATHER
 
@@ -247,6 +248,10 @@ class VAEEngine:
         # tested, measured no faster: C2 12.725 / 12.696 vs 12.648 / 12.681 ms, C4 neutral,
         # profiles/r04j_delta_ab.log); default: the attention backward's own delta pass
         self.delta_fused = os.environ.get('SVAE_DELTA_FUSED', '0') != '0'
+        # the LayerNorm-affine gradient partials of consecutive LayerNorm backwards summed in one launch
+        # (SVAE_COLSUM_BATCH=0: one colsum launch per LayerNorm, for A/B runs)
+        self.cs_batch = os.environ.get('SVAE_COLSUM_BATCH', '1') != '0'
+        self._cs_pending = []
         self.ncu = (torch.cuda.get_device_properties(flat.device).multi_processor_count
                     if flat.device.type == 'cuda' else 256)
         self.side = None
@@ -275,10 +280,26 @@ class VAEEngine:
     def _ln_bwd(self, name, dy, st, rows, dres, dx, dx_bf=None, bf_drop=None, zsplice=None):
         x, mean, rstd = st
         D = self.d
-        part = self.ws.get('ln.part', (1024 * 2 * D,), f32)
         wg = self.P.grad[self.P.offsets[name + '.weight'][0]:][:2 * D]   # [weight | bias] grads (adjacent)
+        if not self.cs_batch:
+            part = self.ws.get('ln.part', (1024 * 2 * D,), f32)
+            K.layernorm_bwd(dy, x, self.P.f(name + '.weight'), mean, rstd, dres, dx, dx_bf, wg, rows, D, part,
+                            bf_drop=bf_drop, zsplice=zsplice)
+            return
+        # the affine-gradient partials wait in their own slice of the workspace; flush_colsum sums up to
+        # COLSUM_MAX of them in one launch (at every ready() point and at the end of the backward)
+        if len(self._cs_pending) == COLSUM_MAX:
+            self.flush_colsum()
+        k, n1 = len(self._cs_pending), 1024 * 2 * D
+        part = self.ws.get('ln.parts', (COLSUM_MAX * n1,), f32)[k * n1:(k + 1) * n1]
         K.layernorm_bwd(dy, x, self.P.f(name + '.weight'), mean, rstd, dres, dx, dx_bf, wg, rows, D, part,
-                        bf_drop=bf_drop, zsplice=zsplice)
+                        bf_drop=bf_drop, zsplice=zsplice, defer=self._cs_pending)
+
+    def flush_colsum(self):
+        """Sum the deferred LayerNorm-affine gradient partials (one svae_colsum_multi launch)."""
+        if self._cs_pending:
+            K.colsum_multi(self._cs_pending)
+            self._cs_pending = []
 
     def _dw(self, dY, X, wname, rows, n_out, n_in, ldy=None, ldx=None, bias=None, on_side=True):
         bg = None
@@ -901,12 +922,11 @@ class VAEEngine:
         """Gradients of loss = nll + kl_weight * kl into the flat gradient arena (accumulating). `ready(end)`
         is called each time the arena prefix [0, end) holds final gradients (data-parallel bucketing)."""
         sv, hp, d, ws, P = self.saved, self.hp, self.d, self.ws, self.P
-        if ready is None:
-            ready = lambda end: None        # noqa: E731
-        else:                               # a bucket's gradients must be complete before its all-reduce
-            user_ready = ready
+        user_ready = ready
 
-            def ready(end):
+        def ready(end):                     # a bucket's gradients must be complete before its all-reduce
+            if user_ready is not None:
+                self.flush_colsum()
                 self.join_side()
                 user_ready(end)
         if sv is None:
@@ -1025,6 +1045,7 @@ class VAEEngine:
         self.join_side()            # the tied weight's head gradient (side stream) before the scatter-add
         self._embedding_bwd(sv, dx_emb, T, d)
         ready(P.n_live)
+        self.flush_colsum()
         self.join_side()
 
     def _embedding_bwd(self, sv, dx, T, d):

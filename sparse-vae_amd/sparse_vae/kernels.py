@@ -202,7 +202,8 @@ def layernorm_fwd(x, w, b, y, mean, rstd, rows, D):
                                  mean.data_ptr(), rstd.data_ptr(), rows, D, stream()), 'svae_layernorm_fwd')
 
 
-def layernorm_bwd(dy, x, w, mean, rstd, dres, dx, dx_bf, wgrad2, rows, D, part_ws, bf_drop=None, zsplice=None):
+def layernorm_bwd(dy, x, w, mean, rstd, dres, dx, dx_bf, wgrad2, rows, D, part_ws, bf_drop=None, zsplice=None,
+                  defer=None):
     """dx = dres + LN'(dy); wgrad2 (the adjacent [weight | bias] grads, 2D floats) += sum of affine grads.
     bf_drop = (p, seed, zero_mod): the bf16 copy dx_bf carries the next consumer's dropout backward and position-0
     zeroing (svae_layernorm_bwd_drop), replacing a dropout_bwd_cast pass over dx. zsplice = (L, zrow f32 | None,
@@ -221,7 +222,24 @@ def layernorm_bwd(dy, x, w, mean, rstd, dres, dx, dx_bf, wgrad2, rows, D, part_w
                                           part.data_ptr(), nblk, rows, D, int(zm), float(p),
                                           int(seed) & 0xFFFFFFFFFFFFFFFF, int(zmod), ptr(zrow), ptr(zrow_bf),
                                           stream()), 'svae_layernorm_bwd_drop')
-    colsum(part, nblk, 2 * D, 2 * D, wgrad2, accumulate=True)
+    if defer is not None:   # the caller sums the partials later, batched with other LayerNorms (colsum_multi)
+        defer.append((part, nblk, 2 * D, 2 * D, wgrad2))
+    else:
+        colsum(part, nblk, 2 * D, 2 * D, wgrad2, accumulate=True)
+
+
+_colsum_segs = (N.ColsumSeg * N.COLSUM_MAX)()
+
+
+def colsum_multi(segs):
+    """svae_colsum_multi: [(inp f32, rows, cols, ld, out f32)] (<= 8), each out += column sums of its inp."""
+    assert 0 < len(segs) <= N.COLSUM_MAX
+    for i, (inp, rows, cols, ld, out) in enumerate(segs):
+        _dev(inp, out)
+        assert inp.dtype == f32 and out.dtype == f32
+        _colsum_segs[i].inp, _colsum_segs[i].out = inp.data_ptr(), out.data_ptr()
+        _colsum_segs[i].ld, _colsum_segs[i].rows, _colsum_segs[i].cols = ld, rows, cols
+    check(lib.svae_colsum_multi(ctypes.addressof(_colsum_segs), len(segs), stream()), 'svae_colsum_multi')
 
 
 def colsum(inp, rows, cols, ld, out, accumulate=True):

@@ -758,3 +758,20 @@ def test_transpose_blocks(nb):
     torch.cuda.synchronize()
     for o, r, c, _ in rows_tab:
         assert torch.equal(dst[o:o + r * c].view(c, r), src[o:o + r * c].view(r, c).t())
+
+
+def test_colsum_multi_exact():
+    """svae_colsum_multi: up to 8 column sums in one launch, each added into its own output, exact on integer data
+    (ragged row counts, the LayerNorm partial shape [nblk][2D] and narrower ones)."""
+    g = torch.Generator(device=dev).manual_seed(7)
+    segs, refs = [], []
+    for rows, cols in ((1024, 1024), (1024, 1536), (37, 64), (513, 2048), (1, 4), (1024, 1024), (300, 128),
+                       (1024, 1024)):
+        inp = torch.randint(-3, 4, (rows, cols), device=dev, generator=g).float()
+        out = torch.full((cols,), 0.5, device=dev)
+        segs.append((inp, rows, cols, cols, out))
+        refs.append(0.5 + inp.sum(0))
+    K.colsum_multi(segs)
+    torch.cuda.synchronize()
+    for (_, _, _, _, out), ref in zip(segs, refs):
+        assert torch.equal(out, ref)

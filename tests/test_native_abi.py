@@ -74,3 +74,13 @@ def test_product_refuses_cpu_execution():
     batch = TextDataModule(dataset_name='synthetic', seq_len=128, batch_size=2).synthetic_batch(0)
     with pytest.raises(RuntimeError, match='no CPU fallback|There is no CPU fallback'):
         m.training_step(batch, 0)
+
+
+def test_colsum_seg_layout():
+    """svae_colsum_seg: the ctypes mirror matches the header (field order and size)."""
+    import ctypes
+    from sparse_vae import _native as N
+    assert ctypes.sizeof(N.ColsumSeg) == 32
+    assert [f[0] for f in N.ColsumSeg._fields_] == ['inp', 'out', 'ld', 'rows', 'cols']
+    hdr = open(os.path.join(ROOT, 'include', 'svae.h')).read()
+    assert '#define SVAE_COLSUM_MAX 8' in hdr and N.COLSUM_MAX == 8
