@@ -41,7 +41,8 @@ enum svae_epi {
                                  f32 workspace aux [splits][M][N] and a reduce pass adds them into C     */
   SVAE_EPI_GELU = 4,          /* C bf16 = gelu(acc + bias);  aux bf16 = gelu'(acc + bias)              */
   SVAE_EPI_GELU_BWD = 5,      /* C bf16 = acc * aux  (aux = the gelu' saved by SVAE_EPI_GELU)          */
-  SVAE_EPI_DROPOUT_RESID = 6, /* C f32 = resid + keep(seed, m*N+n) * acc / (1 - p)                     */
+  SVAE_EPI_DROPOUT_RESID = 6, /* C f32 = resid + keep(seed, m*N+n) * acc / (1 - p); with aux != NULL
+                                 (batch 1, ldaux % 8 == 0) also aux bf16 = bf16(C)                    */
   SVAE_EPI_ROTARY_BF16 = 7,   /* C bf16 = rotary(acc + bias) on cols < rot_cols (attention.py:194-208) */
   SVAE_EPI_CE_STATS = 8,      /* C bf16 = acc + bias; per (row, 128-col tile) online (max, sumexp) to
                                  aux f32 [M][ceil(N/128)][2]; label logit (f32) to resid-as-out [M]   */

@@ -285,6 +285,9 @@ __device__ __forceinline__ void epilogue_half(const GP& p, const float* cs, int 
       }
       *(f32x4*)c = x0;
       if (full) *(f32x4*)(c + 4) = x1;
+      if constexpr (EPI == SVAE_EPI_DROPOUT_RESID) {   // the bf16 copy (the vocabulary head's input)
+        if (p.aux) store_bf16((bf16*)p.aux + (long long)m * p.ldaux + n, x0, x1, full);
+      }
     } else if constexpr (EPI == SVAE_EPI_GELU) {
       // C = gelu(acc + bias), aux = gelu'(acc + bias): the backward multiplies by aux, no erf recomputed
       x0 += b0;
@@ -1109,6 +1112,11 @@ __device__ __forceinline__ void g3_reg_epilogue_ld(const GP& p, const f32x4 (&ac
         }
       } else {
         store_rows_f32((float*)p.C + cofs, p.ldc, m0 + wr * 128 + i * 16, p.M, nb, p.N, x, g, li);
+        // DROPOUT_RESID with aux: also the bf16 copy (the last decoder layer's output = the vocabulary head's input,
+        // which then needs no separate cast pass over [T, d])
+        if constexpr (EPI == SVAE_EPI_DROPOUT_RESID) {
+          if (p.aux) store_rows_bf16<false>((bf16*)p.aux, p.ldaux, m0 + wr * 128 + i * 16, p.M, nb, p.N, x, g, li);
+        }
       }
       if (i + 1 < 8) {
 #pragma unroll
@@ -1565,6 +1573,10 @@ __global__ __launch_bounds__(1024) void gemm_skinny_kernel(GP p) {
     }
     if (p.resid) x += *(const f32x4*)(p.resid + (long long)m * p.ldr + n);
     *(f32x4*)((float*)p.C + (long long)m * p.ldc + n) = x;
+    if constexpr (EPI == SVAE_EPI_DROPOUT_RESID) {
+      if (p.aux)
+        *(bf16x4*)((bf16*)p.aux + (long long)m * p.ldaux + n) = (bf16x4){f2bf(x[0]), f2bf(x[1]), f2bf(x[2]), f2bf(x[3])};
+    }
   } else if constexpr (EPI == SVAE_EPI_GELU) {
     f32x2 g0, d0, g1, d1;
     gelu_pair2((f32x2){x[0], x[1]}, g0, d0);
@@ -1645,6 +1657,9 @@ static int validate_desc(const svae_gemm_desc* d) {
   if ((d->epi == SVAE_EPI_GELU || d->epi == SVAE_EPI_GELU_BWD || d->epi == SVAE_EPI_CE_STATS) && !d->aux)
     return SVAE_EINVAL;
   if (d->epi == SVAE_EPI_DROPOUT_RESID && !d->resid) return SVAE_EINVAL;
+  // DROPOUT_RESID's optional bf16 copy in aux: one batch, 16-B aligned rows
+  if (d->epi == SVAE_EPI_DROPOUT_RESID && d->aux && (d->batch != 1 || d->ldaux % 8 || ((uintptr_t)d->aux & 15)))
+    return SVAE_EINVAL;
   if (d->epi == SVAE_EPI_CE_STATS && (!d->labels || !d->label_logit || d->splits != 1)) return SVAE_EINVAL;
   if (d->splits > 1 && d->epi != SVAE_EPI_F32_ATOMIC) return SVAE_EINVAL;
   if (d->a_rowsum && !d->a_t) return SVAE_EINVAL;

@@ -248,6 +248,9 @@ class VAEEngine:
         # tested, measured no faster: C2 12.725 / 12.696 vs 12.648 / 12.681 ms, C4 neutral,
         # profiles/r04j_delta_ab.log); default: the attention backward's own delta pass
         self.delta_fused = os.environ.get('SVAE_DELTA_FUSED', '0') != '0'
+        # the last decoder layer's dropout + residual GEMM epilogue also writes the bf16 copy of its output (the vocab
+        # head's input) instead of a separate [T, d] cast pass; SVAE_RESID_BF16=0 restores the cast (A/B runs)
+        self.resid_bf16 = os.environ.get('SVAE_RESID_BF16', '1') != '0'
         # the LayerNorm-affine gradient partials of consecutive LayerNorm backwards summed in one launch
         # (SVAE_COLSUM_BATCH=0: one colsum launch per LayerNorm, for A/B runs)
         self.cs_batch = os.environ.get('SVAE_COLSUM_BATCH', '1') != '0'
@@ -473,8 +476,9 @@ class VAEEngine:
                 K.resid_ln_fwd(xc, yf, out_bf, rows_q, d, xo=out, drop_p=drop_p, seed=seed)
         else:
             out = ws.get(tag + '.out', (rows_q, d), f32) if out is None else out
+            # (out_bf: the last decoder layer's epilogue also writes the bf16 copy the vocabulary head reads)
             K.gemm(f, P.w(pre + 'ffn.2.weight'), out, rows_q, d, 4 * d, epi=EPI_DROPOUT_RESID, resid=xc, ldr=d,
-                   drop_p=drop_p, seed=seed)
+                   drop_p=drop_p, seed=seed, aux=out_bf, ldaux=d if out_bf is not None else 0)
         st.update(h2=h2, gprime=gprime, f=f, xc=xc, rows_q=rows_q)
         return out, st
 
@@ -848,10 +852,11 @@ class VAEEngine:
                 nxt, out = None, ws.get(f'x_dec{i + 1}', (T, d), f32)
             xs, st = self.layer_fwd(f'decoder_layers.{i}.', xs, B, L, L, padm, causal=True, heads=self.H,
                                     hd=self.hd, drop_p=dropout, seed=_mix_seed(seed, i), tag=f'd{i}', out=out,
-                                    window=self.window, fuse=fuse, h_in=h_in, next_ln=nxt, out_bf=xf if last else None)
+                                    window=self.window, fuse=fuse, h_in=h_in, next_ln=nxt,
+                                    out_bf=xf if last and (fuse or self.resid_bf16) else None)
             h_in = st.pop('next_h', None)
             dec.append(st)
-        if not fuse:
+        if not fuse and not self.resid_bf16:
             K.cast_bf16(xs, xf)
         return xf, dec
 

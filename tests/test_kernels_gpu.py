@@ -198,6 +198,26 @@ def test_gemm_epilogues(M, Nn, Kk):
     assert agree.all()
 
 
+@pytest.mark.parametrize('M,Nn,Kk', [(32768, 512, 256), (1024, 512, 512), (1000, 520, 2048), (48, 512, 256)])
+def test_gemm_dropout_resid_bf16_copy(M, Nn, Kk):
+    # DROPOUT_RESID with aux: the epilogue's bf16 copy of the f32 output (the last decoder layer -> the vocab head's
+    # input) equals the round-to-nearest bf16 of C exactly, in every kernel (256x256 persistent, LDS-DMA, skinny)
+    torch.manual_seed(M + Kk)
+    X = torch.randn(M, Kk, device=dev).bfloat16()
+    W = (torch.randn(Nn, Kk, device=dev) * 0.1).bfloat16()
+    R = torch.randn(M, Nn, device=dev)
+    C32 = torch.empty(M, Nn, device=dev)
+    Cb = torch.full((M, Nn), float('nan'), device=dev, dtype=torch.bfloat16)
+    K.gemm(X, W, C32, M, Nn, Kk, epi=N.EPI_DROPOUT_RESID, resid=R, ldr=Nn, drop_p=0.1, seed=9, aux=Cb, ldaux=Nn)
+    C0 = torch.empty(M, Nn, device=dev)
+    K.gemm(X, W, C0, M, Nn, Kk, epi=N.EPI_DROPOUT_RESID, resid=R, ldr=Nn, drop_p=0.1, seed=9)
+    torch.cuda.synchronize()
+    assert torch.equal(C32, C0)                       # the f32 output is unchanged by the copy
+    assert torch.equal(Cb, C32.bfloat16())
+    with pytest.raises(RuntimeError):                 # ldaux % 8 != 0 is rejected
+        K.gemm(X, W, C32, M, Nn, Kk, epi=N.EPI_DROPOUT_RESID, resid=R, ldr=Nn, aux=Cb, ldaux=Nn - 4)
+
+
 @pytest.mark.parametrize('M,Nn,Kk', [(64, 512, 2048), (37, 520, 72), (1, 2048, 512), (64, 512, 64)])
 def test_gemm_skinny_epilogues(M, Nn, Kk):
     # M <= 64: the K-split skinny kernel (one row per sequence: encoder bottleneck, q(z|x), z projections)
