@@ -34,7 +34,9 @@ typedef void* svae_stream_t; /* hipStream_t */
  * A, B 16-byte aligned; N, ldc (and ldr, ldaux) % 4 == 0 and C 8-byte aligned (vectorised epilogue). */
 enum svae_epi {
   SVAE_EPI_BF16 = 0,          /* C bf16 = alpha*acc + bias                                            */
-  SVAE_EPI_F32 = 1,           /* C f32  = alpha*acc + bias (+ resid)                                  */
+  SVAE_EPI_F32 = 1,           /* C f32  = alpha*acc + bias (+ resid); with aux != NULL (batch 1, ldaux %
+                                 8 == 0) also aux bf16 = bf16(keep(seed, m*N+n) * C / (1 - p)) -- what
+                                 svae_dropout_bwd_cast makes of C (drop_p 0: bf16(C))                  */
   SVAE_EPI_F32_ACC = 2,       /* C f32 += alpha*acc                                                   */
   SVAE_EPI_F32_ATOMIC = 3,    /* atomicAdd(C f32, alpha*acc)   (split-K / shared destinations); with
                                  splits > 1 and aux != NULL: each split stores its partial tile into the
@@ -134,6 +136,12 @@ int svae_layernorm_bwd_drop(const void* dy, const void* x, int32_t x_dtype, cons
                             const float* rstd, const float* dres, float* dx, void* dx_bf, float* part, int32_t nblk,
                             int32_t rows, int32_t D, int32_t zero_mod, float bf_drop_p, uint64_t bf_seed,
                             int32_t bf_zero_mod, float* zrow, void* zrow_bf, svae_stream_t stream);
+/* svae_layernorm_bwd of the vocabulary head's LayerNorm (transformer_vae.py output_layer[2]) fused with the GELU
+ * backward of the linear before it (output_layer[0..1]): out_bf = bf16(LN'(dy) * gp), gp the bf16 GELU' the forward's
+ * SVAE_EPI_GELU epilogue saved; no f32 dx is written (replaces svae_layernorm_bwd + svae_gelu_bwd). part as above. */
+int svae_layernorm_bwd_gelu(const void* dy, const void* x, int32_t x_dtype, const float* w, const float* mean,
+                            const float* rstd, const void* gp, void* out_bf, float* part, int32_t nblk, int32_t rows,
+                            int32_t D, svae_stream_t stream);
 int svae_layernorm_nblk(int32_t rows);
 
 /* ---- column sums: out[j] (+)= sum_i in[i*ld + j] (bias grads, LN affine grads, batch sums) ----------

@@ -287,6 +287,14 @@ __device__ __forceinline__ void epilogue_half(const GP& p, const float* cs, int 
       if (full) *(f32x4*)(c + 4) = x1;
       if constexpr (EPI == SVAE_EPI_DROPOUT_RESID) {   // the bf16 copy (the vocabulary head's input)
         if (p.aux) store_bf16((bf16*)p.aux + (long long)m * p.ldaux + n, x0, x1, full);
+      } else if constexpr (EPI == SVAE_EPI_F32) {      // the dropout-masked bf16 copy (a layer backward's input)
+        if (p.aux) {
+          if (p.drop_p > 0.f) {
+            dropout4(p, x0, m, n);
+            if (full) dropout4(p, x1, m, n + 4);
+          }
+          store_bf16((bf16*)p.aux + (long long)m * p.ldaux + n, x0, x1, full);
+        }
       }
     } else if constexpr (EPI == SVAE_EPI_GELU) {
       // C = gelu(acc + bias), aux = gelu'(acc + bias): the backward multiplies by aux, no erf recomputed
@@ -1116,6 +1124,16 @@ __device__ __forceinline__ void g3_reg_epilogue_ld(const GP& p, const f32x4 (&ac
         // which then needs no separate cast pass over [T, d])
         if constexpr (EPI == SVAE_EPI_DROPOUT_RESID) {
           if (p.aux) store_rows_bf16<false>((bf16*)p.aux, p.ldaux, m0 + wr * 128 + i * 16, p.M, nb, p.N, x, g, li);
+        } else if constexpr (EPI == SVAE_EPI_F32) {
+          // F32 with aux: also bf16(dropout(C)) (the vocabulary head's d x -> the top decoder layer's FFN-output
+          // gradient, as svae_dropout_bwd_cast would make it from C)
+          if (p.aux) {
+            if (p.drop_p > 0.f) {
+#pragma unroll
+              for (int j = 0; j < 4; ++j) dropout4(p, x[j], m, nb + j * 16 + 4 * g);
+            }
+            store_rows_bf16<false>((bf16*)p.aux, p.ldaux, m0 + wr * 128 + i * 16, p.M, nb, p.N, x, g, li);
+          }
         }
       }
       if (i + 1 < 8) {
@@ -1573,9 +1591,9 @@ __global__ __launch_bounds__(1024) void gemm_skinny_kernel(GP p) {
     }
     if (p.resid) x += *(const f32x4*)(p.resid + (long long)m * p.ldr + n);
     *(f32x4*)((float*)p.C + (long long)m * p.ldc + n) = x;
-    if constexpr (EPI == SVAE_EPI_DROPOUT_RESID) {
-      if (p.aux)
-        *(bf16x4*)((bf16*)p.aux + (long long)m * p.ldaux + n) = (bf16x4){f2bf(x[0]), f2bf(x[1]), f2bf(x[2]), f2bf(x[3])};
+    if (p.aux) {   // DROPOUT_RESID: bf16(C); F32: bf16(dropout(C))
+      if (EPI == SVAE_EPI_F32 && p.drop_p > 0.f) dropout4(p, x, m, n);
+      *(bf16x4*)((bf16*)p.aux + (long long)m * p.ldaux + n) = (bf16x4){f2bf(x[0]), f2bf(x[1]), f2bf(x[2]), f2bf(x[3])};
     }
   } else if constexpr (EPI == SVAE_EPI_GELU) {
     f32x2 g0, d0, g1, d1;
@@ -1657,8 +1675,9 @@ static int validate_desc(const svae_gemm_desc* d) {
   if ((d->epi == SVAE_EPI_GELU || d->epi == SVAE_EPI_GELU_BWD || d->epi == SVAE_EPI_CE_STATS) && !d->aux)
     return SVAE_EINVAL;
   if (d->epi == SVAE_EPI_DROPOUT_RESID && !d->resid) return SVAE_EINVAL;
-  // DROPOUT_RESID's optional bf16 copy in aux: one batch, 16-B aligned rows
-  if (d->epi == SVAE_EPI_DROPOUT_RESID && d->aux && (d->batch != 1 || d->ldaux % 8 || ((uintptr_t)d->aux & 15)))
+  // DROPOUT_RESID's / F32's optional bf16 copy in aux: one batch, 16-B aligned rows
+  if ((d->epi == SVAE_EPI_DROPOUT_RESID || d->epi == SVAE_EPI_F32) && d->aux &&
+      (d->batch != 1 || d->ldaux % 8 || ((uintptr_t)d->aux & 15)))
     return SVAE_EINVAL;
   if (d->epi == SVAE_EPI_CE_STATS && (!d->labels || !d->label_logit || d->splits != 1)) return SVAE_EINVAL;
   if (d->splits > 1 && d->epi != SVAE_EPI_F32_ATOMIC) return SVAE_EINVAL;
@@ -1752,7 +1771,7 @@ static int gemm_run(const svae_gemm_desc* d, svae_stream_t stream, bool* fused_d
   if (slab) {
     if (d->batch != 1 || ((uintptr_t)d->aux & 15) || d->N % 4) return SVAE_EINVAL;
     p.C = d->aux; p.ldc = d->N; p.sC = 0; p.slab = (long long)d->M * d->N;
-    p.bias = nullptr; p.resid = nullptr;
+    p.bias = nullptr; p.resid = nullptr; p.aux = nullptr;   // (aux is the slab: no bf16 copy of the F32 epilogue)
     epi_run = SVAE_EPI_F32;
   }
 
@@ -1938,7 +1957,7 @@ SVAE_EXPORT int svae_gemm_pair(const svae_gemm_desc* d0, const svae_gemm_desc* d
     GP& p = q.p[i];
     fill_gp(d[i], p);
     p.C = d[i]->aux; p.ldc = d[i]->N; p.sC = 0; p.slab = (long long)d[i]->M * d[i]->N;
-    p.bias = nullptr; p.resid = nullptr;
+    p.bias = nullptr; p.resid = nullptr; p.aux = nullptr;
     const int kc3 = (d[i]->K + d[i]->splits - 1) / d[i]->splits;
     p.kchunk = (kc3 + 63) / 64 * 64;
     p.tn2 = (d[i]->N + 255) / 256;

@@ -245,14 +245,17 @@ __global__ __launch_bounds__(256) void resid_ln_fwd_kernel(const float* __restri
   if (lane == 0) { mean_out[row] = mean; rstd_out[row] = rstd; }
 }
 
-template <typename T, int MAXV>
+// GMUL: only the bf16 dx_bf = bf16(dx * gmul) is written (no f32 dx): the vocabulary head's LayerNorm backward fused
+// with the GELU backward of the linear before it (gmul = the GELU' its forward epilogue saved)
+template <typename T, int MAXV, bool GMUL = false>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16* __restrict__ dy, const T* __restrict__ x,
                                                      const float* __restrict__ w, const float* __restrict__ mean_in,
                                                      const float* __restrict__ rstd_in, const float* __restrict__ dres,
                                                      float* __restrict__ dx, bf16* __restrict__ dx_bf,
                                                      float* __restrict__ part, int rows, int D, int zero_mod,
                                                      float bf_drop_p, unsigned long long bf_seed, int bf_zero_mod,
-                                                     float* __restrict__ zrow, bf16* __restrict__ zrow_bf) {
+                                                     float* __restrict__ zrow, bf16* __restrict__ zrow_bf,
+                                                     const bf16* __restrict__ gmul = nullptr) {
   __shared__ float red[4][2][256 * MAXV];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   f32x4 adw[MAXV], adb[MAXV];
@@ -291,6 +294,13 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16* __restrict__ dy
         f32x4 o;
 #pragma unroll
         for (int e = 0; e < 4; ++e) o[e] = rstd * (g[j][e] - m1 - xh[j][e] * m2);
+        if constexpr (GMUL) {
+          const f32x4 gv = load4<bf16>(gmul + base + c);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] *= gv[e];
+          store4_bf(dx_bf + base + c, o);
+          continue;
+        }
         if (dres) {
           const f32x4 r = *(const f32x4*)(dres + base + c);
 #pragma unroll
@@ -542,6 +552,33 @@ SVAE_EXPORT int svae_layernorm_bwd(const void* dy, const void* x, int32_t x_dtyp
                                    int32_t nblk, int32_t rows, int32_t D, int32_t zero_mod, svae_stream_t stream) {
   return svae_layernorm_bwd_drop(dy, x, x_dtype, w, mean, rstd, dres, dx, dx_bf, part, nblk, rows, D, zero_mod, 0.f, 0,
                                  0, nullptr, nullptr, stream);
+}
+
+SVAE_EXPORT int svae_layernorm_bwd_gelu(const void* dy, const void* x, int32_t x_dtype, const float* w,
+                                        const float* mean, const float* rstd, const void* gp, void* out_bf, float* part,
+                                        int32_t nblk, int32_t rows, int32_t D, svae_stream_t stream) {
+  if (!dy || !x || !w || !mean || !rstd || !gp || !out_bf || !part || rows <= 0 || D <= 0 || D % 4 || D > 1024 ||
+      nblk <= 0)
+    return SVAE_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  const bf16* g = (const bf16*)gp;
+#define SVAE_LN_BWD_G(MV)                                                                                          \
+  do {                                                                                                             \
+    if (x_dtype == 0)                                                                                              \
+      hipLaunchKernelGGL((ln_bwd_kernel<float, MV, true>), dim3(nblk), dim3(256), 0, s, (const bf16*)dy,            \
+                         (const float*)x, w, mean, rstd, nullptr, nullptr, (bf16*)out_bf, part, rows, D, 0, 0.f, 0ULL, \
+                         0, nullptr, nullptr, g);                                                                  \
+    else                                                                                                           \
+      hipLaunchKernelGGL((ln_bwd_kernel<bf16, MV, true>), dim3(nblk), dim3(256), 0, s, (const bf16*)dy,             \
+                         (const bf16*)x, w, mean, rstd, nullptr, nullptr, (bf16*)out_bf, part, rows, D, 0, 0.f, 0ULL,  \
+                         0, nullptr, nullptr, g);                                                                  \
+  } while (0)
+  if (D <= 512) SVAE_LN_BWD_G(2);
+  else if (D <= 768) SVAE_LN_BWD_G(3);
+  else SVAE_LN_BWD_G(4);
+#undef SVAE_LN_BWD_G
+  SVAE_LAUNCH_CHECK();
+  return SVAE_OK;
 }
 
 SVAE_EXPORT int svae_colsum(const void* in, int32_t in_dtype, int32_t rows, int32_t cols, int64_t ld, float* out,

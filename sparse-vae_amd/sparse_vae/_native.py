@@ -81,6 +81,8 @@ _SIGS = {
     'svae_layernorm_bwd_drop': [c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                 c_void_p, c_void_p, c_int32, c_int32, c_int32, c_int32, c_float, c_uint64, c_int32,
                                 c_void_p, c_void_p, c_void_p],
+    'svae_layernorm_bwd_gelu': [c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                c_void_p, c_int32, c_int32, c_int32, c_void_p],
     'svae_layernorm_nblk': [c_int32],
     'svae_colsum': [c_void_p, c_int32, c_int32, c_int32, c_int64, c_void_p, c_int32, c_void_p],
     'svae_colsum_multi': [c_void_p, c_int32, c_void_p],

@@ -251,6 +251,11 @@ class VAEEngine:
         # the last decoder layer's dropout + residual GEMM epilogue also writes the bf16 copy of its output (the vocab
         # head's input) instead of a separate [T, d] cast pass; SVAE_RESID_BF16=0 restores the cast (A/B runs)
         self.resid_bf16 = os.environ.get('SVAE_RESID_BF16', '1') != '0'
+        # and the head's d x GEMM writes the top decoder layer's dropout-masked bf16 gradient (SVAE_HEAD_G2=0: the
+        # layer backward's own dropout_bwd_cast pass)
+        self.head_g2 = os.environ.get('SVAE_HEAD_G2', '1') != '0'
+        # the head LayerNorm's backward writes bf16(dx * GELU') directly (SVAE_LN_GELU=0: f32 dx + a gelu_bwd pass)
+        self.ln_gelu = os.environ.get('SVAE_LN_GELU', '1') != '0'
         # the LayerNorm-affine gradient partials of consecutive LayerNorm backwards summed in one launch
         # (SVAE_COLSUM_BATCH=0: one colsum launch per LayerNorm, for A/B runs)
         self.cs_batch = os.environ.get('SVAE_COLSUM_BATCH', '1') != '0'
@@ -280,12 +285,17 @@ class VAEEngine:
         K.layernorm_fwd(x, self.P.f(name + '.weight'), self.P.f(name + '.bias'), y, mean, rstd, rows, D)
         return y, (x, mean, rstd)
 
-    def _ln_bwd(self, name, dy, st, rows, dres, dx, dx_bf=None, bf_drop=None, zsplice=None):
+    def _ln_bwd(self, name, dy, st, rows, dres, dx, dx_bf=None, bf_drop=None, zsplice=None, gelu=None):
+        """LayerNorm backward; gelu = the saved GELU' (bf16) of the linear before the LayerNorm: then only
+        dx_bf = bf16(dx * gelu) is written (svae_layernorm_bwd_gelu; dres, dx, bf_drop and zsplice unused)."""
         x, mean, rstd = st
         D = self.d
         wg = self.P.grad[self.P.offsets[name + '.weight'][0]:][:2 * D]   # [weight | bias] grads (adjacent)
         if not self.cs_batch:
             part = self.ws.get('ln.part', (1024 * 2 * D,), f32)
+            if gelu is not None:
+                K.layernorm_bwd_gelu(dy, x, self.P.f(name + '.weight'), mean, rstd, gelu, dx_bf, wg, rows, D, part)
+                return
             K.layernorm_bwd(dy, x, self.P.f(name + '.weight'), mean, rstd, dres, dx, dx_bf, wg, rows, D, part,
                             bf_drop=bf_drop, zsplice=zsplice)
             return
@@ -295,6 +305,10 @@ class VAEEngine:
             self.flush_colsum()
         k, n1 = len(self._cs_pending), 1024 * 2 * D
         part = self.ws.get('ln.parts', (COLSUM_MAX * n1,), f32)[k * n1:(k + 1) * n1]
+        if gelu is not None:
+            K.layernorm_bwd_gelu(dy, x, self.P.f(name + '.weight'), mean, rstd, gelu, dx_bf, wg, rows, D, part,
+                                 defer=self._cs_pending)
+            return
         K.layernorm_bwd(dy, x, self.P.f(name + '.weight'), mean, rstd, dres, dx, dx_bf, wg, rows, D, part,
                         bf_drop=bf_drop, zsplice=zsplice, defer=self._cs_pending)
 
@@ -975,13 +989,22 @@ class VAEEngine:
             # (the vocabulary-head dW stays in order: next to the equally large head dX it only contends)
             self._dw(logits, sv['hh'], 'input_layer.0.weight', T, V, d, bias='output_layer.3.bias', on_side=False)
             K.gemm(logits, P.wT('input_layer.0.weight', V, d), dhh, T, d, V, epi=EPI_BF16)
-        dh0 = ws.get('b.dh0', (T, d), f32)
-        self._ln_bwd('output_layer.2', dhh, sv['ln_h'], T, None, dh0)
         dpre0 = ws.get('b.dpre0', (T, d))
-        K.gelu_bwd(dh0, sv['gp0'], dpre0, T * d)
+        if self.ln_gelu:   # the head LayerNorm's backward and the GELU backward before it in one pass
+            self._ln_bwd('output_layer.2', dhh, sv['ln_h'], T, None, None, dx_bf=dpre0, gelu=sv['gp0'])
+        else:
+            dh0 = ws.get('b.dh0', (T, d), f32)
+            self._ln_bwd('output_layer.2', dhh, sv['ln_h'], T, None, dh0)
+            K.gelu_bwd(dh0, sv['gp0'], dpre0, T * d)
         self._dw(dpre0, sv['xf'], 'output_layer.0.weight', T, d, d, bias='output_layer.0.bias')
         dx = ws.get('b.dx_dec', (T, d), f32)
-        K.gemm(dpre0, P.wT('output_layer.0.weight', d, d), dx, T, d, d, epi=EPI_F32)
+        # (the same epilogue writes the top decoder layer's dropout-masked bf16 FFN-output gradient, b.g2: no
+        # separate dropout_bwd_cast pass over [T, d]; SVAE_HEAD_G2=0 for A/B runs)
+        top = sv['dec_layers'][-1]
+        g2_pre = self.head_g2 and top['rows_q'] == T
+        K.gemm(dpre0, P.wT('output_layer.0.weight', d, d), dx, T, d, d, epi=EPI_F32,
+               aux=ws.get('b.g2', (T, d)) if g2_pre else None, ldaux=d if g2_pre else 0,
+               drop_p=top['drop_p'] if g2_pre else 0.0, seed=top['seed'] if g2_pre else 0)
         ready(P.end('output_layer.3.bias'))
 
         # ---- decoder layers, last to first
@@ -989,7 +1012,7 @@ class VAEEngine:
         dzh = ws.get('b.dzh', (B, d), f32)
         dzh_bf = ws.get('b.dzh_bf', (B, d))
         dx_prev = ws.get('b.dx_prev', (T, d), f32)
-        g2_ready = False
+        g2_ready = g2_pre
         for i in reversed(range(hp.num_layers)):
             st = sv['dec_layers'][i]
             # the next (lower) layer's FFN dropout backward + position-0 zeroing (extract_rows below) fused into this

@@ -228,6 +228,20 @@ def layernorm_bwd(dy, x, w, mean, rstd, dres, dx, dx_bf, wgrad2, rows, D, part_w
         colsum(part, nblk, 2 * D, 2 * D, wgrad2, accumulate=True)
 
 
+def layernorm_bwd_gelu(dy, x, w, mean, rstd, gp, out_bf, wgrad2, rows, D, part_ws, defer=None):
+    """out_bf = bf16(LN'(dy) * gp) (svae_layernorm_bwd_gelu: the head's LayerNorm backward with the GELU backward
+    of the linear before it); wgrad2 += the affine grads (or deferred, as layernorm_bwd)."""
+    nblk = lib.svae_layernorm_nblk(rows)
+    part = part_ws[: nblk * 2 * D]
+    check(lib.svae_layernorm_bwd_gelu(dy.data_ptr(), x.data_ptr(), 0 if x.dtype == f32 else 1, w.data_ptr(),
+                                      mean.data_ptr(), rstd.data_ptr(), gp.data_ptr(), out_bf.data_ptr(),
+                                      part.data_ptr(), nblk, rows, D, stream()), 'svae_layernorm_bwd_gelu')
+    if defer is not None:
+        defer.append((part, nblk, 2 * D, 2 * D, wgrad2))
+    else:
+        colsum(part, nblk, 2 * D, 2 * D, wgrad2, accumulate=True)
+
+
 _colsum_segs = (N.ColsumSeg * N.COLSUM_MAX)()
 
 

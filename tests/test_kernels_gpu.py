@@ -408,6 +408,53 @@ def test_layernorm_bwd_fused_dropout_cast(p):
     assert torch.equal(dx2, dxz) and torch.equal(got2, ref)
 
 
+@pytest.mark.parametrize('D,rows,xdt', [(512, 64 * 9, torch.float32), (768, 300, torch.float32), (256, 77, torch.bfloat16)])
+def test_layernorm_bwd_gelu_fused(D, rows, xdt):
+    # the head LayerNorm's backward fused with the GELU backward before it: bf16(LN'(dy) * gp) equals layernorm_bwd
+    # then gelu_bwd bit for bit, and the affine gradients are the same
+    torch.manual_seed(D + rows)
+    x = (torch.randn(rows, D, device=dev) * 2 + 0.5).to(xdt)
+    w = torch.randn(D, device=dev) * 0.1 + 1
+    bb = torch.randn(D, device=dev) * 0.1
+    y = torch.empty(rows, D, device=dev, dtype=torch.bfloat16)
+    mean, rstd = torch.empty(rows, device=dev), torch.empty(rows, device=dev)
+    K.layernorm_fwd(x, w, bb, y, mean, rstd, rows, D)
+    dy = torch.randn(rows, D, device=dev).bfloat16()
+    gp = torch.rand(rows, D, device=dev).bfloat16() * 1.2 - 0.1
+    part = torch.empty(1024 * 2 * D, device=dev)
+    dx0, wg0 = torch.empty(rows, D, device=dev), torch.zeros(2 * D, device=dev)
+    K.layernorm_bwd(dy, x, w, mean, rstd, None, dx0, None, wg0, rows, D, part)
+    ref = torch.empty(rows, D, device=dev, dtype=torch.bfloat16)
+    K.gelu_bwd(dx0, gp, ref, rows * D)
+    got, wg1 = torch.full((rows, D), float('nan'), device=dev, dtype=torch.bfloat16), torch.zeros(2 * D, device=dev)
+    K.layernorm_bwd_gelu(dy, x, w, mean, rstd, gp, got, wg1, rows, D, part)
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref)
+    assert torch.equal(wg1, wg0)
+
+
+@pytest.mark.parametrize('M,Nn,Kk,p', [(32768, 512, 512, 0.1), (1024, 512, 256, 0.25), (1000, 520, 2048, 0.0),
+                                       (48, 512, 256, 0.1)])
+def test_gemm_f32_dropout_bf16_copy(M, Nn, Kk, p):
+    # EPI_F32 with aux: C unchanged, aux = what dropout_bwd_cast makes of C (the head's d x -> the top decoder layer's
+    # dropout-masked FFN-output gradient), bit for bit, in the 256x256 persistent, LDS-DMA and skinny kernels
+    torch.manual_seed(M + Kk)
+    X = torch.randn(M, Kk, device=dev).bfloat16()
+    W = (torch.randn(Nn, Kk, device=dev) * 0.1).bfloat16()
+    b = torch.randn(Nn, device=dev)
+    seed = 0x243F6A8885A308D3
+    C0 = torch.empty(M, Nn, device=dev)
+    K.gemm(X, W, C0, M, Nn, Kk, epi=N.EPI_F32, bias=b)
+    C1 = torch.empty(M, Nn, device=dev)
+    got = torch.full((M, Nn), float('nan'), device=dev, dtype=torch.bfloat16)
+    K.gemm(X, W, C1, M, Nn, Kk, epi=N.EPI_F32, bias=b, aux=got, ldaux=Nn, drop_p=p, seed=seed)
+    ref = torch.empty(M, Nn, device=dev, dtype=torch.bfloat16)
+    K.dropout_bwd_cast(C0, ref, p, seed, M, Nn)
+    torch.cuda.synchronize()
+    assert torch.equal(C1, C0)
+    assert torch.equal(got, ref)
+
+
 @pytest.mark.parametrize('B,d,Z', [(64, 512, 64), (3, 200, 70), (130, 768, 128)])
 def test_zproj_bwd(B, d, Z):
     # z_projections backward in one launch: dW += g^T z, db += sum_b g, dz += g W (f32 accumulation; z, W bf16)
