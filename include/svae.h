@@ -298,6 +298,16 @@ int svae_dropout_bwd_cast(const float* g, void* out, float p, uint64_t seed, int
 /* GELU backward (transformer_language_model.py:57 head GELU): out bf16 = dx * gp, gp = gelu' saved by the
    forward's SVAE_EPI_GELU epilogue. */
 int svae_gelu_bwd(const float* dx, const void* gp, void* out, int64_t n, svae_stream_t stream);
+/* The training step's token inputs (transformer_vae.py:42-55 / language_model.py's next-token targets), one pass:
+ * ids32[t] = int32(ids[t]), labels[t] = ids[t + 1] inside a sequence of L and 0 at its last position, padm[t]
+ * (uint8) = (ids[t] == 0) for pad_mode 1 or pad[t] (bool bytes) for pad_mode 2 (pad_mode 0: no mask), and
+ * ntok_out[b] = ntok[b] for b < B when both are given. ids int64 [B][L] contiguous. */
+int svae_prep_tokens(const int64_t* ids, const void* pad, int32_t pad_mode, int32_t B, int32_t L, int32_t* ids32,
+                     int32_t* labels, void* padm, const int64_t* ntok, int64_t* ntok_out, svae_stream_t stream);
+/* The step's scalars (transformer_vae.py:55 and its autograd backward): loss[0] = nll[0] + kl_weight * kl[0] when
+ * loss != NULL; gs[0] = gloss[0], gs[1] = gloss[0] * kl_weight when gs != NULL (f32, each op rounded separately). */
+int svae_step_scalars(const float* nll, const float* kl, const float* gloss, float kl_weight, float* loss, float* gs,
+                      svae_stream_t stream);
 /* cast f32 -> bf16 (n elements). */
 int svae_cast_bf16(const float* in, void* out, int64_t n, svae_stream_t stream);
 /* Transposed bf16 weight shadows (the K-contiguous B operand of the dX GEMMs): for each of nblocks

@@ -581,6 +581,38 @@ __global__ __launch_bounds__(256) void dropout_bwd_cast_kernel(const float* __re
   }
 }
 
+// The step's token inputs in one pass (engine.forward): ids32 = int32(ids), labels = ids shifted left by one within
+// each sequence with 0 at its last position (language_model.py: the next-token targets), the uint8 key-padding mask
+// (pad_mode 1: ids == 0, 2: from the caller's bool mask, 0: none) and the per-sequence token counts.
+__global__ __launch_bounds__(256) void prep_tokens_kernel(const int64_t* __restrict__ ids, const unsigned char* __restrict__ pad,
+                                                          int pad_mode, int rows, int L, int32_t* __restrict__ ids32,
+                                                          int32_t* __restrict__ labels, unsigned char* __restrict__ padm,
+                                                          const int64_t* __restrict__ ntok, int64_t* __restrict__ ntok_out,
+                                                          int B) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t < B && ntok) ntok_out[t] = ntok[t];
+  if (t >= rows) return;
+  const int64_t v = ids[t];
+  ids32[t] = (int32_t)v;
+  labels[t] = (t % L == L - 1) ? 0 : (int32_t)ids[t + 1];
+  if (pad_mode == 1) padm[t] = v == 0;
+  else if (pad_mode == 2) padm[t] = pad[t] != 0;
+}
+
+// loss = nll + kl_weight * kl (transformer_vae.py:55) and the backward's gradient scales gs = (gloss, gloss *
+// kl_weight), each op rounded as the torch expressions it replaces (no contraction into an fma)
+__global__ __launch_bounds__(64) void step_scalars_kernel(const float* __restrict__ nll, const float* __restrict__ kl,
+                                                          const float* __restrict__ gloss, float kw,
+                                                          float* __restrict__ loss, float* __restrict__ gs) {
+  if (threadIdx.x != 0) return;
+  if (loss) loss[0] = __fadd_rn(nll[0], __fmul_rn(kw, kl[0]));
+  if (gs) {
+    const float g = gloss[0];
+    gs[0] = g;
+    gs[1] = __fmul_rn(g, kw);
+  }
+}
+
 __global__ __launch_bounds__(256) void gelu_bwd_kernel(const float* __restrict__ dx, const bf16* __restrict__ gp,
                                                        bf16* __restrict__ out, long long n) {
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256)
@@ -1001,6 +1033,29 @@ SVAE_EXPORT int svae_gelu_bwd(const float* dx, const void* gp, void* out, int64_
   if (!dx || !gp || !out || n <= 0) return SVAE_EINVAL;
   hipLaunchKernelGGL(gelu_bwd_kernel, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream, dx, (const bf16*)gp,
                      (bf16*)out, n);
+  SVAE_LAUNCH_CHECK();
+  return SVAE_OK;
+}
+
+SVAE_EXPORT int svae_prep_tokens(const int64_t* ids, const void* pad, int32_t pad_mode, int32_t B, int32_t L,
+                                 int32_t* ids32, int32_t* labels, void* padm, const int64_t* ntok, int64_t* ntok_out,
+                                 svae_stream_t stream) {
+  if (!ids || !ids32 || !labels || B <= 0 || L <= 0 || pad_mode < 0 || pad_mode > 2) return SVAE_EINVAL;
+  if ((pad_mode && !padm) || (pad_mode == 2 && !pad) || (!ntok != !ntok_out)) return SVAE_EINVAL;
+  const long long rows = (long long)B * L;
+  if (rows > 0x7FFFFFFFLL - 256) return SVAE_EINVAL;
+  const long long work = rows > B ? rows : B;
+  hipLaunchKernelGGL(prep_tokens_kernel, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, (hipStream_t)stream, ids,
+                     (const unsigned char*)pad, pad_mode, (int)rows, L, ids32, labels, (unsigned char*)padm, ntok,
+                     ntok_out, B);
+  SVAE_LAUNCH_CHECK();
+  return SVAE_OK;
+}
+
+SVAE_EXPORT int svae_step_scalars(const float* nll, const float* kl, const float* gloss, float kl_weight, float* loss,
+                                  float* gs, svae_stream_t stream) {
+  if ((!loss && !gs) || (loss && (!nll || !kl)) || (gs && !gloss)) return SVAE_EINVAL;
+  hipLaunchKernelGGL(step_scalars_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, nll, kl, gloss, kl_weight, loss, gs);
   SVAE_LAUNCH_CHECK();
   return SVAE_OK;
 }

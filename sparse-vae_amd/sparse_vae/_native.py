@@ -117,6 +117,9 @@ _SIGS = {
                      c_int32, c_int32, c_void_p],
     'svae_dropout_bwd_cast': [c_void_p, c_void_p, c_float, c_uint64, c_int64, c_int32, c_int64, c_void_p],
     'svae_gelu_bwd': [c_void_p, c_void_p, c_void_p, c_int64, c_void_p],
+    'svae_prep_tokens': [c_void_p, c_void_p, c_int32, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p,
+                         c_void_p, c_void_p],
+    'svae_step_scalars': [c_void_p, c_void_p, c_void_p, c_float, c_void_p, c_void_p, c_void_p],
     'svae_cast_bf16': [c_void_p, c_void_p, c_int64, c_void_p],
     'svae_extract_rows': [c_void_p, c_int64, c_int32, c_int32, c_int32, c_void_p, c_void_p],
     'svae_zproj_bwd': [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_int32, c_void_p],

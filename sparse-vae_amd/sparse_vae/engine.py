@@ -256,6 +256,9 @@ class VAEEngine:
         self.head_g2 = os.environ.get('SVAE_HEAD_G2', '1') != '0'
         # the head LayerNorm's backward writes bf16(dx * GELU') directly (SVAE_LN_GELU=0: f32 dx + a gelu_bwd pass)
         self.ln_gelu = os.environ.get('SVAE_LN_GELU', '1') != '0'
+        # the step's token inputs (ids32, labels, padding mask, token counts) and its scalars (loss, gradient scales)
+        # in one launch each instead of torch's copy / fill / mul / add ops (SVAE_SMALL_FUSED=0: the torch ops)
+        self.small_fused = os.environ.get('SVAE_SMALL_FUSED', '1') != '0'
         # the LayerNorm-affine gradient partials of consecutive LayerNorm backwards summed in one launch
         # (SVAE_COLSUM_BATCH=0: one colsum launch per LayerNorm, for A/B runs)
         self.cs_batch = os.environ.get('SVAE_COLSUM_BATCH', '1') != '0'
@@ -616,16 +619,23 @@ class VAEEngine:
         B, L = ids.shape
         T, V, Z, N = B * L, hp.vocab_size, hp.latent_depth, hp.num_latents
         ids32 = ws.get('ids', (B, L), torch.int32)
-        ids32.copy_(ids)
         padm = None
         if pad is not None and pad is not False:
             padm = ws.get('pad', (B, L), torch.uint8)
-            padm.copy_(ids.eq(0) if pad is True else pad)
         labels = ws.get('labels', (B, L), torch.int32)
-        labels[:, :-1].copy_(ids32[:, 1:])
-        labels[:, -1] = 0
         ntok64 = ws.get('ntok', (B,), torch.int64)
-        ntok64.copy_(ntok)
+        if (self.small_fused and ids.dtype == torch.int64 and ids.is_contiguous() and isinstance(ntok, torch.Tensor) and ntok.is_cuda
+                and ntok.dtype == torch.int64 and ntok.is_contiguous() and ntok.numel() == B
+                and (padm is None or pad is True or (pad.dtype == torch.bool and pad.is_contiguous()))):
+            # ids32, the next-token labels, the padding mask and the token counts in one launch
+            K.prep_tokens(ids, pad if padm is not None else None, B, L, ids32, labels, padm, ntok, ntok64)
+        else:
+            ids32.copy_(ids)
+            if padm is not None:
+                padm.copy_(ids.eq(0) if pad is True else pad)
+            labels[:, :-1].copy_(ids32[:, 1:])
+            labels[:, -1] = 0
+            ntok64.copy_(ntok)
         sv = {'B': B, 'L': L, 'dropout': dropout, 'seed': seed}
 
         x_emb = ws.get('x_emb', (T, d), f32)
@@ -694,7 +704,12 @@ class VAEEngine:
         sv.update(xf=xf, gp0=gp0, h0=h0, hh=hh, ln_h=ln_h, logits=logits, lse=lse, chunk_w=chunk_w,
                   nchunks=nchunks, chunk_len=chunk_len, labels=labels, ids32=ids32, ntok=ntok64, x_emb=x_emb,
                   row_loss=row_loss, head=head, coff=coff)
-        loss = nll[0] + kl_weight * kl[0]                                          # transformer_vae.py:55
+        if self.small_fused:
+            lbuf = ws.get('loss', (1,), f32)
+            K.step_scalars(kl_weight, nll=nll, kl=kl, loss=lbuf)                  # transformer_vae.py:55
+            loss = lbuf[0]
+        else:
+            loss = nll[0] + kl_weight * kl[0]
         self.saved = sv
         return {'loss': loss, 'nll': nll[0], 'kl': kl[0], 'train_kl': kl[1], 'raw_kl': raw_kl,
                 'mu': stats[:, :Z], 'logvar': stats[:, Z:], 'stats': stats, 'kl_buf': kl, 'z': zf, 'eps': eps_buf,
@@ -953,8 +968,12 @@ class VAEEngine:
         B, L = sv['B'], sv['L']
         T, V, Z, N = B * L, hp.vocab_size, hp.latent_depth, hp.num_latents
         gs = ws.get('gscale', (2,), f32)
-        gs[0:1].copy_(gloss.reshape(1))
-        gs[1:2].copy_(gloss.reshape(1) * kl_weight)
+        gl = gloss.reshape(1)
+        if self.small_fused and gl.is_cuda and gl.dtype == f32:
+            K.step_scalars(kl_weight, gloss=gl, gs=gs)
+        else:
+            gs[0:1].copy_(gl)
+            gs[1:2].copy_(gl * kl_weight)
 
         # ---- head
         logits = sv['logits']

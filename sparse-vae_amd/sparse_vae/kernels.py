@@ -431,6 +431,28 @@ def ce_grad(logits, ld, lse, chunk_w, labels, gscale, rows, V, seq, nchunks, chu
                            gscale.data_ptr(), ptr(dbias), rows, V, seq, nchunks, chunk_len, stream()), 'svae_ce_grad')
 
 
+def prep_tokens(ids, pad, B, L, ids32, labels, padm=None, ntok=None, ntok_out=None):
+    """svae_prep_tokens: ids int64 [B, L] -> ids32, next-token labels (0 at each sequence's end), the uint8
+    padding mask (pad True: ids == 0; a bool tensor: copied; None / False: none) and the ntok copy."""
+    assert ids.dtype == torch.int64 and ids.is_contiguous() and ids.numel() == B * L
+    mode = 0 if pad is None or pad is False else (1 if pad is True else 2)
+    if mode == 2:
+        assert pad.dtype == torch.bool and pad.is_contiguous() and pad.numel() == B * L
+    if ntok is not None:
+        assert ntok.dtype == torch.int64 and ntok.is_contiguous() and ntok.numel() == B
+    _dev(ids, ids32, labels)
+    check(lib.svae_prep_tokens(ids.data_ptr(), pad.data_ptr() if mode == 2 else None, mode, B, L, ids32.data_ptr(),
+                               labels.data_ptr(), ptr(padm), ptr(ntok), ptr(ntok_out), stream()), 'svae_prep_tokens')
+
+
+def step_scalars(kl_weight, nll=None, kl=None, loss=None, gloss=None, gs=None):
+    """svae_step_scalars: loss = nll + kl_weight * kl and / or gs = (gloss, gloss * kl_weight), f32 on the device."""
+    for t in (nll, kl, loss, gloss, gs):
+        assert t is None or (t.is_cuda and t.dtype == f32)
+    check(lib.svae_step_scalars(ptr(nll), ptr(kl), ptr(gloss), float(kl_weight), ptr(loss), ptr(gs), stream()),
+          'svae_step_scalars')
+
+
 def dropout_bwd_cast(g, out, p, seed, rows, cols, ld_in=None):
     check(lib.svae_dropout_bwd_cast(g.data_ptr(), out.data_ptr(), p, seed & 0xFFFFFFFFFFFFFFFF, rows * cols, cols,
                                     ld_in or cols, stream()), 'svae_dropout_bwd_cast')

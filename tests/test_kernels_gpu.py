@@ -455,6 +455,42 @@ def test_gemm_f32_dropout_bf16_copy(M, Nn, Kk, p):
     assert torch.equal(got, ref)
 
 
+@pytest.mark.parametrize('B,L,mode', [(64, 512, 'bool'), (3, 37, 'ids'), (5, 1, 'none'), (300, 64, 'bool')])
+def test_prep_tokens(B, L, mode):
+    # the step's token inputs in one launch equal the torch op sequence it replaces
+    torch.manual_seed(B + L)
+    ids = torch.randint(0, 5, (B, L), device=dev, dtype=torch.int64) * 7919
+    pad = {'bool': ids.eq(0), 'ids': True, 'none': None}[mode]
+    ntok = torch.randint(1, L + 1, (B,), device=dev, dtype=torch.int64)
+    ids32 = torch.full((B, L), -5, device=dev, dtype=torch.int32)
+    labels = torch.full((B, L), -5, device=dev, dtype=torch.int32)
+    padm = torch.full((B, L), 9, device=dev, dtype=torch.uint8) if pad is not None else None
+    nt = torch.full((B,), -1, device=dev, dtype=torch.int64)
+    K.prep_tokens(ids, pad, B, L, ids32, labels, padm, ntok, nt)
+    torch.cuda.synchronize()
+    assert torch.equal(ids32, ids.to(torch.int32))
+    ref = torch.zeros(B, L, device=dev, dtype=torch.int32)
+    ref[:, :-1] = ids[:, 1:].to(torch.int32)
+    assert torch.equal(labels, ref)
+    if padm is not None:
+        assert torch.equal(padm, ids.eq(0).to(torch.uint8))
+    assert torch.equal(nt, ntok)
+
+
+@pytest.mark.parametrize('kw', [0.3, 0.7123, 1.0])
+def test_step_scalars(kw):
+    # loss = nll + kw * kl and gs = (gloss, gloss * kw): bit-equal to the torch expressions they replace
+    nll = torch.tensor([7.123456], device=dev)
+    kl = torch.tensor([1.98765], device=dev)
+    gl = torch.tensor([0.3333333], device=dev)
+    loss, gs = torch.empty(1, device=dev), torch.empty(2, device=dev)
+    K.step_scalars(kw, nll=nll, kl=kl, loss=loss)
+    K.step_scalars(kw, gloss=gl, gs=gs)
+    torch.cuda.synchronize()
+    assert torch.equal(loss[0], nll[0] + kw * kl[0])
+    assert torch.equal(gs, torch.cat([gl, gl * kw]))
+
+
 @pytest.mark.parametrize('B,d,Z', [(64, 512, 64), (3, 200, 70), (130, 768, 128)])
 def test_zproj_bwd(B, d, Z):
     # z_projections backward in one launch: dW += g^T z, db += sum_b g, dz += g W (f32 accumulation; z, W bf16)
