@@ -325,6 +325,18 @@ int svae_extract_rows(float* x, int64_t ld, int32_t rows, int32_t mod, int32_t D
  * dW GEMM with fused bias row sums and the split-K dz GEMM of a decoder layer). */
 int svae_zproj_bwd(const float* g, const void* z, const void* W, float* dW, float* db, float* dz, int32_t B,
                    int32_t d, int32_t Z, svae_stream_t stream);
+/* n (<= SVAE_ZPROJ_MAX) z-projection backwards sharing z and dz in one launch: for each segment, dW += g^T z and
+ * db += sum_b g as svae_zproj_bwd; dz += g_0 W_0, then += g_1 W_1, ... in list order -- the same f32 results as n
+ * svae_zproj_bwd calls in that order. */
+#define SVAE_ZPROJ_MAX 32
+typedef struct svae_zproj_seg {
+  const float* g;   /* [B][d] f32 */
+  const void* W;    /* [d][Z] bf16 */
+  float* dW;        /* [d][Z] f32 */
+  float* db;        /* [d] f32 */
+} svae_zproj_seg;
+int svae_zproj_bwd_multi(const svae_zproj_seg* segs, int32_t n, const void* z, float* dz, int32_t B, int32_t d,
+                         int32_t Z, svae_stream_t stream);
 
 /* ---- optimiser (RAdam, rectified_adam.py:16-88; clip_grad_norm_, language_model.py:120-122) -------
  * sumsq: partial sums of g^2 over n elements into part[nblk]; radam: reads part to form the global

@@ -1145,6 +1145,100 @@ __global__ __launch_bounds__(1024) void zproj_bwd_kernel(const float* __restrict
   }
 }
 
+// The backward of n z projections in one launch (svae_zproj_bwd_multi): blocks [0, n * nbw) take the dW / db part of
+// segment blk / nbw; the B blocks after them sum dz[b] += g_i[b] W_i over the segments in list order, each segment's
+// partial reduced exactly as zproj_bwd_kernel reduces it and added in the same order as n separate launches would.
+struct ZprojSegs {
+  svae_zproj_seg s[SVAE_ZPROJ_MAX];
+};
+
+__global__ __launch_bounds__(1024) void zproj_bwd_multi_kernel(ZprojSegs segs, int nseg, const bf16* __restrict__ z,
+                                                               float* __restrict__ dz, int B, int d, int Z, int nbw) {
+  __shared__ float gs[1024];
+  __shared__ float red[16][64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int blk = blockIdx.x;
+  if (blk < nseg * nbw) {
+    __shared__ float zs[64][65];
+    const svae_zproj_seg& sg = segs.s[blk / nbw];
+    const float* g = sg.g;
+    float* dW = sg.dW;
+    const int m0 = (blk % nbw) * 16, m = m0 + wave;
+    for (int n0 = 0; n0 < Z; n0 += 64) {
+      const int n = n0 + lane;
+      float acc = 0.f;
+      for (int b0 = 0; b0 < B; b0 += 64) {
+        const int nb = min(64, B - b0);
+        for (int e = tid; e < 64 * 64; e += 1024) {
+          const int i = e >> 6, j = e & 63;
+          zs[i][j] = (i < nb && n0 + j < Z) ? (float)z[(long long)(b0 + i) * Z + n0 + j] : 0.f;
+        }
+        {
+          const int i = tid >> 4, w = tid & 15;
+          gs[tid] = (i < nb && m0 + w < d) ? g[(long long)(b0 + i) * d + m0 + w] : 0.f;
+        }
+        __syncthreads();
+#pragma unroll 16
+        for (int i = 0; i < 64; ++i) acc = fmaf(gs[16 * i + wave], zs[i][lane], acc);
+        __syncthreads();
+      }
+      if (m < d && n < Z) dW[(long long)m * Z + n] += acc;
+    }
+    if (m < d) {
+      float s = 0.f;
+      for (int b = lane; b < B; b += 64) s += g[(long long)b * d + m];
+      s = wave_sum(s);
+      if (lane == 0) sg.db[m] += s;
+    }
+    return;
+  }
+  const int b = blk - nseg * nbw;
+  for (int n0 = 0; n0 < Z; n0 += 64) {
+    const int n = n0 + lane;
+    float out = (wave == 0 && n < Z) ? dz[(long long)b * Z + n] : 0.f;
+    for (int si = 0; si < nseg; ++si) {
+      const float* gb = segs.s[si].g + (long long)b * d;
+      const bf16* W = (const bf16*)segs.s[si].W;
+      float acc = 0.f;
+      for (int c0 = 0; c0 < d; c0 += 1024) {
+        const int nc = min(1024, d - c0);
+        if (tid < nc) gs[tid] = gb[c0 + tid];
+        __syncthreads();
+        if (n < Z) {
+#pragma unroll 8
+          for (int mm = wave; mm < nc; mm += 16) acc = fmaf(gs[mm], (float)W[(long long)(c0 + mm) * Z + n], acc);
+        }
+        __syncthreads();
+      }
+      red[wave][lane] = acc;
+      __syncthreads();
+      if (wave == 0 && n < Z) {
+        float t = 0.f;
+#pragma unroll
+        for (int w = 0; w < 16; ++w) t += red[w][lane];
+        out += t;
+      }
+      __syncthreads();
+    }
+    if (wave == 0 && n < Z) dz[(long long)b * Z + n] = out;
+  }
+}
+
+SVAE_EXPORT int svae_zproj_bwd_multi(const svae_zproj_seg* segs, int32_t n, const void* z, float* dz, int32_t B,
+                                     int32_t d, int32_t Z, svae_stream_t stream) {
+  if (!segs || n <= 0 || n > SVAE_ZPROJ_MAX || !z || !dz || B <= 0 || d <= 0 || Z <= 0) return SVAE_EINVAL;
+  ZprojSegs a;
+  for (int i = 0; i < n; ++i) {
+    if (!segs[i].g || !segs[i].W || !segs[i].dW || !segs[i].db) return SVAE_EINVAL;
+    a.s[i] = segs[i];
+  }
+  const int nbw = (d + 15) / 16;
+  hipLaunchKernelGGL(zproj_bwd_multi_kernel, dim3(n * nbw + B), dim3(1024), 0, (hipStream_t)stream, a, (int)n,
+                     (const bf16*)z, dz, B, d, Z, nbw);
+  SVAE_LAUNCH_CHECK();
+  return SVAE_OK;
+}
+
 SVAE_EXPORT int svae_zproj_bwd(const float* g, const void* z, const void* W, float* dW, float* db, float* dz,
                                int32_t B, int32_t d, int32_t Z, svae_stream_t stream) {
   if (!g || !z || !W || !dW || !db || !dz || B <= 0 || d <= 0 || Z <= 0) return SVAE_EINVAL;

@@ -64,6 +64,14 @@ class AttnDesc(ctypes.Structure):
 COLSUM_MAX = 8
 
 
+ZPROJ_MAX = 32
+
+
+class ZprojSeg(ctypes.Structure):
+    """svae_zproj_seg (include/svae.h)."""
+    _fields_ = [('g', c_void_p), ('W', c_void_p), ('dW', c_void_p), ('db', c_void_p)]
+
+
 class ColsumSeg(ctypes.Structure):
     """svae_colsum_seg (include/svae.h)."""
     _fields_ = [('inp', c_void_p), ('out', c_void_p), ('ld', c_int64), ('rows', c_int32), ('cols', c_int32)]
@@ -120,6 +128,7 @@ _SIGS = {
     'svae_prep_tokens': [c_void_p, c_void_p, c_int32, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p,
                          c_void_p, c_void_p],
     'svae_step_scalars': [c_void_p, c_void_p, c_void_p, c_float, c_void_p, c_void_p, c_void_p],
+    'svae_zproj_bwd_multi': [c_void_p, c_int32, c_void_p, c_void_p, c_int32, c_int32, c_int32, c_void_p],
     'svae_cast_bf16': [c_void_p, c_void_p, c_int64, c_void_p],
     'svae_extract_rows': [c_void_p, c_int64, c_int32, c_int32, c_int32, c_void_p, c_void_p],
     'svae_zproj_bwd': [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_int32, c_void_p],

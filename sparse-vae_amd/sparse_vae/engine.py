@@ -20,7 +20,7 @@ from collections import OrderedDict
 import torch
 
 from . import kernels as K
-from ._native import COLSUM_MAX
+from ._native import COLSUM_MAX, ZPROJ_MAX
 from ._native import EPI_BF16, EPI_F32, EPI_F32_ACC, EPI_GELU, EPI_GELU_BWD, EPI_DROPOUT_RESID, \
     EPI_ROTARY_BF16, EPI_CE_STATS, EPI_F32_ATOMIC, EPI_CE_PROB, EPI_ROWSCALE_GATHER
 
@@ -259,6 +259,9 @@ class VAEEngine:
         # the step's token inputs (ids32, labels, padding mask, token counts) and its scalars (loss, gradient scales)
         # in one launch each instead of torch's copy / fill / mul / add ops (SVAE_SMALL_FUSED=0: the torch ops)
         self.small_fused = os.environ.get('SVAE_SMALL_FUSED', '1') != '0'
+        # the decoder layers' z-projection backwards in one launch (SVAE_ZPROJ_BATCH=0: one launch per layer)
+        self.zp_batch = os.environ.get('SVAE_ZPROJ_BATCH', '1') != '0'
+        self._zp_pending, self._zp_ctx = [], None
         # the LayerNorm-affine gradient partials of consecutive LayerNorm backwards summed in one launch
         # (SVAE_COLSUM_BATCH=0: one colsum launch per LayerNorm, for A/B runs)
         self.cs_batch = os.environ.get('SVAE_COLSUM_BATCH', '1') != '0'
@@ -314,6 +317,13 @@ class VAEEngine:
             return
         K.layernorm_bwd(dy, x, self.P.f(name + '.weight'), mean, rstd, dres, dx, dx_bf, wg, rows, D, part,
                         bf_drop=bf_drop, zsplice=zsplice, defer=self._cs_pending)
+
+    def flush_zproj(self):
+        """The deferred z-projection backwards (one svae_zproj_bwd_multi launch, in deferral order)."""
+        if self._zp_pending:
+            z_bf, dz, B, d, Z = self._zp_ctx
+            K.zproj_bwd_multi(self._zp_pending, z_bf, dz, B, d, Z)
+            self._zp_pending = []
 
     def flush_colsum(self):
         """Sum the deferred LayerNorm-affine gradient partials (one svae_colsum_multi launch)."""
@@ -961,6 +971,7 @@ class VAEEngine:
         def ready(end):                     # a bucket's gradients must be complete before its all-reduce
             if user_ready is not None:
                 self.flush_colsum()
+                self.flush_zproj()
                 self.join_side()
                 user_ready(end)
         if sv is None:
@@ -1042,13 +1053,22 @@ class VAEEngine:
                 nd = (nst['drop_p'], nst['seed'], L)
             # position-0 splice: its gradient feeds z_projections[i]; earlier layers see zero there (moved out of dx by
             # the layer's last LayerNorm backward when it is a residual layer)
-            zs = (L, dzh, None) if st['resid'] and st['rows_q'] == T else None
+            dzh_i = ws.get('b.dzh_all', (hp.num_layers, B, d), f32)[i] if self.zp_batch else dzh
+            zs = (L, dzh_i, None) if st['resid'] and st['rows_q'] == T else None
             self.layer_bwd(st, dx, dx_prev, g2_ready=g2_ready, next_drop=nd, zsplice=zs)
             g2_ready = nd is not None
             wz, bz = f'z_projections.{i}.weight', f'z_projections.{i}.bias'
-            if zs is not None:   # dW, d bias and dz of z_projections[i] in one f32 launch
+            if zs is not None and self.zp_batch:
+                # dW, d bias and dz of z_projections[i]: deferred, then every layer's in one launch (flush_zproj, also
+                # at each data-parallel bucket point); dz sums the layers in this loop's order either way
+                if len(self._zp_pending) == ZPROJ_MAX:
+                    self.flush_zproj()
+                self._zp_ctx = (sv['z_bf'], dz, B, d, Z)
+                self._zp_pending.append((dzh_i, P.w(wz), P.g(wz), P.g(bz)))
+            elif zs is not None:   # dW, d bias and dz of z_projections[i] in one f32 launch
                 K.zproj_bwd(dzh, sv['z_bf'], P.w(wz), P.g(wz), P.g(bz), dz, B, d, Z)
             else:
+                self.flush_zproj()
                 K.extract_rows(dx_prev, d, T, L, d, dzh)
                 K.cast_bf16(dzh, dzh_bf)
                 self._dw(dzh_bf, sv['z_bf'], wz, B, d, Z, bias=bz)   # (bias gradient = the fused row sums)
@@ -1056,6 +1076,7 @@ class VAEEngine:
                 K.gemm(dzh_bf, P.w(wz), dz, B, Z, d, b_t=True, epi=EPI_F32_ATOMIC, splits=max(1, min(8, d // 64)))
             ready(P.end(f'z_projections.{i}.bias'))
             dx, dx_prev = dx_prev, dx
+        self.flush_zproj()                            # (before reparam_bwd reads dz)
         dx_emb = dx                                   # decoder part of d x_emb (rows 0 already zero)
 
         # ---- reparameterise + q(z|x)

@@ -484,6 +484,24 @@ def zproj_bwd(g, z, W, dW, db, dz, B, d, Z):
                              B, d, Z, stream()), 'svae_zproj_bwd')
 
 
+_zproj_segs = (N.ZprojSeg * N.ZPROJ_MAX)()
+
+
+def zproj_bwd_multi(segs, z, dz, B, d, Z):
+    """svae_zproj_bwd_multi: segs = [(g f32 [B, d], W bf16 [d, Z], dW f32, db f32)] (<= 32) sharing z and dz; the
+    same results as zproj_bwd per segment in list order."""
+    assert 0 < len(segs) <= N.ZPROJ_MAX
+    _dev(z, dz)
+    assert z.dtype == bf16 and dz.dtype == f32
+    for i, (g, W, dW, db) in enumerate(segs):
+        _dev(g, W, dW, db)
+        assert g.dtype == f32 and W.dtype == bf16 and dW.dtype == f32 and db.dtype == f32
+        _zproj_segs[i].g, _zproj_segs[i].W = g.data_ptr(), W.data_ptr()
+        _zproj_segs[i].dW, _zproj_segs[i].db = dW.data_ptr(), db.data_ptr()
+    check(lib.svae_zproj_bwd_multi(ctypes.addressof(_zproj_segs), len(segs), z.data_ptr(), dz.data_ptr(), B, d, Z,
+                                   stream()), 'svae_zproj_bwd_multi')
+
+
 def sumsq(g, n, part):
     check(lib.svae_sumsq(g.data_ptr(), n, part.data_ptr(), part.numel(), stream()), 'svae_sumsq')
 

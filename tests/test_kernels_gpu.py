@@ -477,6 +477,27 @@ def test_prep_tokens(B, L, mode):
     assert torch.equal(nt, ntok)
 
 
+@pytest.mark.parametrize('n,B,d,Z', [(6, 64, 512, 64), (3, 5, 200, 70), (12, 130, 768, 128)])
+def test_zproj_bwd_multi_matches_sequential(n, B, d, Z):
+    # n z-projection backwards in one launch equal n svae_zproj_bwd calls in list order, bit for bit (dW, db, dz)
+    torch.manual_seed(n + B + d)
+    z = torch.randn(B, Z, device=dev).bfloat16()
+    dz0 = torch.randn(B, Z, device=dev)
+    gs = [torch.randn(B, d, device=dev) for _ in range(n)]
+    Ws = [(torch.randn(d, Z, device=dev) * 0.1).bfloat16() for _ in range(n)]
+    dW0 = [torch.randn(d, Z, device=dev) for _ in range(n)]
+    db0 = [torch.randn(d, device=dev) for _ in range(n)]
+    dz_a, dW_a, db_a = dz0.clone(), [t.clone() for t in dW0], [t.clone() for t in db0]
+    for i in range(n):
+        K.zproj_bwd(gs[i], z, Ws[i], dW_a[i], db_a[i], dz_a, B, d, Z)
+    dz_b, dW_b, db_b = dz0.clone(), [t.clone() for t in dW0], [t.clone() for t in db0]
+    K.zproj_bwd_multi([(gs[i], Ws[i], dW_b[i], db_b[i]) for i in range(n)], z, dz_b, B, d, Z)
+    torch.cuda.synchronize()
+    assert torch.equal(dz_a, dz_b)
+    for i in range(n):
+        assert torch.equal(dW_a[i], dW_b[i]) and torch.equal(db_a[i], db_b[i])
+
+
 @pytest.mark.parametrize('kw', [0.3, 0.7123, 1.0])
 def test_step_scalars(kw):
     # loss = nll + kw * kl and gs = (gloss, gloss * kw): bit-equal to the torch expressions they replace

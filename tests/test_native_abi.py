@@ -84,3 +84,13 @@ def test_colsum_seg_layout():
     assert [f[0] for f in N.ColsumSeg._fields_] == ['inp', 'out', 'ld', 'rows', 'cols']
     hdr = open(os.path.join(ROOT, 'include', 'svae.h')).read()
     assert '#define SVAE_COLSUM_MAX 8' in hdr and N.COLSUM_MAX == 8
+
+
+def test_zproj_seg_layout():
+    """svae_zproj_seg: the ctypes mirror matches the header (four pointers, 32 B) and the segment cap."""
+    import ctypes
+    from sparse_vae import _native as N
+    assert ctypes.sizeof(N.ZprojSeg) == 32
+    assert [f[0] for f in N.ZprojSeg._fields_] == ['g', 'W', 'dW', 'db']
+    hdr = open(os.path.join(ROOT, 'include', 'svae.h')).read()
+    assert '#define SVAE_ZPROJ_MAX 32' in hdr and N.ZPROJ_MAX == 32
