@@ -142,6 +142,10 @@ int svae_layernorm_bwd_drop(const void* dy, const void* x, int32_t x_dtype, cons
 int svae_layernorm_bwd_gelu(const void* dy, const void* x, int32_t x_dtype, const float* w, const float* mean,
                             const float* rstd, const void* gp, void* out_bf, float* part, int32_t nblk, int32_t rows,
                             int32_t D, svae_stream_t stream);
+/* svae_layernorm_fwd (f32 x, D % 8 == 0, 16-B aligned x / zrows) with the z splice of transformer_vae.py:89-90: rows
+ * r % zmod == 0 are taken from zrows[r / zmod] (f32 [rows / zmod][D]) and also written into x (the residual stream). */
+int svae_layernorm_fwd_z(float* x, const float* zrows, int32_t zmod, const float* w, const float* b, void* y,
+                         float* mean, float* rstd, int32_t rows, int32_t D, svae_stream_t stream);
 int svae_layernorm_nblk(int32_t rows);
 
 /* ---- column sums: out[j] (+)= sum_i in[i*ld + j] (bias grads, LN affine grads, batch sums) ----------
@@ -337,6 +341,15 @@ typedef struct svae_zproj_seg {
 } svae_zproj_seg;
 int svae_zproj_bwd_multi(const svae_zproj_seg* segs, int32_t n, const void* z, float* dz, int32_t B, int32_t d,
                          int32_t Z, svae_stream_t stream);
+/* The forward of n (<= SVAE_ZPROJ_MAX) z projections in one launch (transformer_vae.py:89, z_projections[i](z)):
+ * out_i [B][d] f32 = z W_i^T + bias_i, z bf16 [B][Z] (Z <= 1024), W_i bf16 [d][Z]; f32 FMAs over k in order. */
+typedef struct svae_zproj_fwd_seg {
+  const void* W;       /* [d][Z] bf16 */
+  const float* bias;   /* [d] f32 */
+  float* out;          /* [B][d] f32 */
+} svae_zproj_fwd_seg;
+int svae_zproj_fwd_multi(const svae_zproj_fwd_seg* segs, int32_t n, const void* z, int32_t B, int32_t d, int32_t Z,
+                         svae_stream_t stream);
 
 /* ---- optimiser (RAdam, rectified_adam.py:16-88; clip_grad_norm_, language_model.py:120-122) -------
  * sumsq: partial sums of g^2 over n elements into part[nblk]; radam: reads part to form the global

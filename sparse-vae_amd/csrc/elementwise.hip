@@ -1224,6 +1224,43 @@ __global__ __launch_bounds__(1024) void zproj_bwd_multi_kernel(ZprojSegs segs, i
   }
 }
 
+// Forward of n z projections (transformer_vae.py:89: z_projections[i](z)) in one launch: out_i [B][d] f32 =
+// z W_i^T + b_i, z bf16 [B][Z], W_i bf16 [d][Z]; one block per (segment, sequence), z's row in LDS, 4 outputs per thread
+// per pass (f32 FMAs over k in order).
+struct ZfwdSegs {
+  svae_zproj_fwd_seg s[SVAE_ZPROJ_MAX];
+};
+
+__global__ __launch_bounds__(256) void zproj_fwd_multi_kernel(ZfwdSegs segs, const bf16* __restrict__ z, int B, int d,
+                                                              int Z) {
+  __shared__ float zr[1024];
+  const int si = blockIdx.x / B, b = blockIdx.x - si * B;
+  const svae_zproj_fwd_seg& sg = segs.s[si];
+  for (int k = threadIdx.x; k < Z; k += 256) zr[k] = (float)z[(long long)b * Z + k];
+  __syncthreads();
+  const bf16* W = (const bf16*)sg.W;
+  for (int m = threadIdx.x; m < d; m += 256) {
+    const bf16* wr = W + (long long)m * Z;
+    float acc = 0.f;
+    for (int k = 0; k < Z; ++k) acc = fmaf(zr[k], (float)wr[k], acc);
+    sg.out[(long long)b * d + m] = acc + sg.bias[m];
+  }
+}
+
+SVAE_EXPORT int svae_zproj_fwd_multi(const svae_zproj_fwd_seg* segs, int32_t n, const void* z, int32_t B, int32_t d,
+                                     int32_t Z, svae_stream_t stream) {
+  if (!segs || n <= 0 || n > SVAE_ZPROJ_MAX || !z || B <= 0 || d <= 0 || Z <= 0 || Z > 1024) return SVAE_EINVAL;
+  ZfwdSegs a;
+  for (int i = 0; i < n; ++i) {
+    if (!segs[i].W || !segs[i].bias || !segs[i].out) return SVAE_EINVAL;
+    a.s[i] = segs[i];
+  }
+  hipLaunchKernelGGL(zproj_fwd_multi_kernel, dim3((unsigned)(n * B)), dim3(256), 0, (hipStream_t)stream, a,
+                     (const bf16*)z, B, d, Z);
+  SVAE_LAUNCH_CHECK();
+  return SVAE_OK;
+}
+
 SVAE_EXPORT int svae_zproj_bwd_multi(const svae_zproj_seg* segs, int32_t n, const void* z, float* dz, int32_t B,
                                      int32_t d, int32_t Z, svae_stream_t stream) {
   if (!segs || n <= 0 || n > SVAE_ZPROJ_MAX || !z || !dz || B <= 0 || d <= 0 || Z <= 0) return SVAE_EINVAL;

@@ -47,11 +47,15 @@ __device__ __forceinline__ void ln_load_row(const T* __restrict__ xr, int lane, 
 // A wave walks rows wave, wave + waves, ... (the launcher sizes the grid so a few rows fall to each wave) with the
 // next row's loads issued before the current row's reductions and stores: the loads stay in flight across rows
 // instead of one load round trip per wave launch.
-template <typename T, int MAXV>
+// ZR (f32 x only): rows r % zmod == 0 are taken from zrows[r / zmod] and written into x (xw) -- the z splice of
+// transformer_vae.py:89-90 applied by the layer's first LayerNorm, so the z projections of all layers run as one
+// launch ahead of the decoder
+template <typename T, int MAXV, bool ZR = false>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, const float* __restrict__ w,
                                                      const float* __restrict__ b, bf16* __restrict__ y,
                                                      float* __restrict__ mean_out, float* __restrict__ rstd_out,
-                                                     int rows, int D) {
+                                                     int rows, int D, const float* __restrict__ zrows = nullptr,
+                                                     int zmod = 0, float* __restrict__ xw = nullptr) {
   // even MAXV: D % 8 == 0 (checked by the launcher), each lane owns runs of 8 consecutive columns, so the bf16 output
   // is one 16-B store per run (the 4-column layout stores 8 B per lane); odd MAXV: runs of 4 columns
   constexpr bool W8 = MAXV % 2 == 0;
@@ -60,11 +64,26 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, co
   int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
   f32x4 v[MAXV], vn[MAXV];
-  ln_load_row<T, MAXV>(x + (long long)row * D, lane, D, v);
+  auto src = [&](int r) -> const T* {
+    if constexpr (ZR) {
+      if (r % zmod == 0) return (const T*)(zrows + (long long)(r / zmod) * D);
+    }
+    return x + (long long)r * D;
+  };
+  ln_load_row<T, MAXV>(src(row), lane, D, v);
 #pragma nounroll
   while (true) {
     const int next = row + nw;
-    if (next < rows) ln_load_row<T, MAXV>(x + (long long)next * D, lane, D, vn);
+    if (next < rows) ln_load_row<T, MAXV>(src(next), lane, D, vn);
+    if constexpr (ZR) {
+      if (row % zmod == 0) {   // the spliced row into x (the residual stream)
+#pragma unroll
+        for (int k = 0; k < MAXV; ++k) {
+          const int c = ln_col<MAXV>(lane, k);
+          if (c < D) *(f32x4*)(xw + (long long)row * D + c) = v[k];
+        }
+      }
+    }
     float s = 0.f;
 #pragma unroll
     for (int k = 0; k < MAXV; ++k) s += (v[k][0] + v[k][1]) + (v[k][2] + v[k][3]);
@@ -482,6 +501,25 @@ SVAE_EXPORT int svae_layernorm_fwd(const void* x, int32_t x_dtype, const float* 
   else if (D <= 768) SVAE_LN_FWD(3);
   else SVAE_LN_FWD(5);
 #undef SVAE_LN_FWD
+  SVAE_LAUNCH_CHECK();
+  return SVAE_OK;
+}
+
+SVAE_EXPORT int svae_layernorm_fwd_z(float* x, const float* zrows, int32_t zmod, const float* w, const float* b, void* y,
+                                     float* mean, float* rstd, int32_t rows, int32_t D, svae_stream_t stream) {
+  if (!x || !zrows || zmod <= 0 || !w || !b || !y || !mean || !rstd || rows <= 0 || D <= 0 || D % 8 || D > 1024)
+    return SVAE_EINVAL;
+  if (((uintptr_t)x | (uintptr_t)zrows) & 15) return SVAE_EINVAL;
+  static const int cap = [] { const char* e = getenv("SVAE_LN_FWD_BLOCKS"); return e ? atoi(e) : 1024; }();
+  const int need = (rows + 3) / 4;
+  dim3 grid((unsigned)(cap > 0 ? std::min(need, cap) : need));
+  hipStream_t s = (hipStream_t)stream;
+  if (D <= 512)
+    hipLaunchKernelGGL((ln_fwd_kernel<float, 2, true>), grid, dim3(256), 0, s, (const float*)x, w, b, (bf16*)y, mean,
+                       rstd, rows, D, zrows, zmod, x);
+  else
+    hipLaunchKernelGGL((ln_fwd_kernel<float, 4, true>), grid, dim3(256), 0, s, (const float*)x, w, b, (bf16*)y, mean,
+                       rstd, rows, D, zrows, zmod, x);
   SVAE_LAUNCH_CHECK();
   return SVAE_OK;
 }

@@ -72,6 +72,11 @@ class ZprojSeg(ctypes.Structure):
     _fields_ = [('g', c_void_p), ('W', c_void_p), ('dW', c_void_p), ('db', c_void_p)]
 
 
+class ZprojFwdSeg(ctypes.Structure):
+    """svae_zproj_fwd_seg (include/svae.h)."""
+    _fields_ = [('W', c_void_p), ('bias', c_void_p), ('out', c_void_p)]
+
+
 class ColsumSeg(ctypes.Structure):
     """svae_colsum_seg (include/svae.h)."""
     _fields_ = [('inp', c_void_p), ('out', c_void_p), ('ld', c_int64), ('rows', c_int32), ('cols', c_int32)]
@@ -129,6 +134,9 @@ _SIGS = {
                          c_void_p, c_void_p],
     'svae_step_scalars': [c_void_p, c_void_p, c_void_p, c_float, c_void_p, c_void_p, c_void_p],
     'svae_zproj_bwd_multi': [c_void_p, c_int32, c_void_p, c_void_p, c_int32, c_int32, c_int32, c_void_p],
+    'svae_zproj_fwd_multi': [c_void_p, c_int32, c_void_p, c_int32, c_int32, c_int32, c_void_p],
+    'svae_layernorm_fwd_z': [c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32,
+                             c_int32, c_void_p],
     'svae_cast_bf16': [c_void_p, c_void_p, c_int64, c_void_p],
     'svae_extract_rows': [c_void_p, c_int64, c_int32, c_int32, c_int32, c_void_p, c_void_p],
     'svae_zproj_bwd': [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_int32, c_void_p],

@@ -261,6 +261,9 @@ class VAEEngine:
         self.small_fused = os.environ.get('SVAE_SMALL_FUSED', '1') != '0'
         # the decoder layers' z-projection backwards in one launch (SVAE_ZPROJ_BATCH=0: one launch per layer)
         self.zp_batch = os.environ.get('SVAE_ZPROJ_BATCH', '1') != '0'
+        # and their forwards (one launch; each layer's first LayerNorm splices its rows in; SVAE_ZPROJ_FWD_BATCH=0: a
+        # skinny GEMM per layer into the position-0 rows)
+        self.zf_batch = os.environ.get('SVAE_ZPROJ_FWD_BATCH', '1') != '0'
         self._zp_pending, self._zp_ctx = [], None
         # the LayerNorm-affine gradient partials of consecutive LayerNorm backwards summed in one launch
         # (SVAE_COLSUM_BATCH=0: one colsum launch per LayerNorm, for A/B runs)
@@ -283,12 +286,17 @@ class VAEEngine:
             self._rot[base] = t
         return t
 
-    def _ln_fwd(self, name, x, rows, tag):
+    def _ln_fwd(self, name, x, rows, tag, zsplice=None):
+        """zsplice = (zrows f32 [rows / zmod, D], zmod): rows r % zmod == 0 of x are replaced by zrows first."""
         D = self.d
         y = self.ws.get(tag + '.y', (rows, D))
         mean = self.ws.get(tag + '.mean', (rows,), f32)
         rstd = self.ws.get(tag + '.rstd', (rows,), f32)
-        K.layernorm_fwd(x, self.P.f(name + '.weight'), self.P.f(name + '.bias'), y, mean, rstd, rows, D)
+        if zsplice is not None:
+            K.layernorm_fwd_z(x, zsplice[0], zsplice[1], self.P.f(name + '.weight'), self.P.f(name + '.bias'), y, mean,
+                              rstd, rows, D)
+        else:
+            K.layernorm_fwd(x, self.P.f(name + '.weight'), self.P.f(name + '.bias'), y, mean, rstd, rows, D)
         return y, (x, mean, rstd)
 
     def _ln_bwd(self, name, dy, st, rows, dres, dx, dx_bf=None, bf_drop=None, zsplice=None, gelu=None):
@@ -389,7 +397,8 @@ class VAEEngine:
 
     # ------------------------------------------------------------------ one transformer layer
     def layer_fwd(self, pre, x, B, Sx, L, pad, *, learned=0, cross=False, causal=False, ctx=None, heads, hd,
-                  drop_p=0.0, seed=0, tag, out=None, window=0, fuse=False, h_in=None, next_ln=None, out_bf=None):
+                  drop_p=0.0, seed=0, tag, out=None, window=0, fuse=False, h_in=None, next_ln=None, out_bf=None,
+                  zsplice=None):
         """TransformerLayer.forward (transformer_layer.py:44-61) on x f32 [B*Sx, d]. Returns the f32 output
         [B*Lq, d] and the saved state for layer_bwd. window > 0: sliding-window self-attention.
 
@@ -409,8 +418,8 @@ class VAEEngine:
         fuse = fuse and not cross
         if h_in is not None:
             h, st['ln_a'] = h_in
-        else:
-            h, st['ln_a'] = self._ln_fwd(pre + 'attn_layer_norm', x, rows_x, tag + '.ln_a')
+        else:   # (zsplice: the position-0 rows of x come from the batched z projections, svae_layernorm_fwd_z)
+            h, st['ln_a'] = self._ln_fwd(pre + 'attn_layer_norm', x, rows_x, tag + '.ln_a', zsplice=zsplice)
         st['h'] = h
         pad_k = pad if Sx == L else None          # PaddedTensor getter: mask iff key length == L
         if learned:
@@ -873,7 +882,15 @@ class VAEEngine:
         xf = ws.get('xf_bf', (T, d))
         dec = []
         h_in = None
-        K.gemm(zb, P.w('z_projections.0.weight'), xs, B, d, Z, ldc=L * d, epi=EPI_F32, bias=P.f('z_projections.0.bias'))
+        # (zf_batch: every layer's z projection in one launch, spliced in by the layer's first LayerNorm)
+        zf_batch = self.zf_batch and not fuse and d % 8 == 0
+        if zf_batch:
+            zall = ws.get('zproj_all', (hp.num_layers, B, d), f32)
+            K.zproj_fwd_multi([(P.w(f'z_projections.{i}.weight'), P.f(f'z_projections.{i}.bias'), zall[i])
+                               for i in range(hp.num_layers)], zb, B, d, Z)
+        else:
+            K.gemm(zb, P.w('z_projections.0.weight'), xs, B, d, Z, ldc=L * d, epi=EPI_F32,
+                   bias=P.f('z_projections.0.bias'))
         for i in range(hp.num_layers):
             last = i + 1 == hp.num_layers
             if fuse:
@@ -885,14 +902,15 @@ class VAEEngine:
                     nxt = (f'decoder_layers.{i + 1}.attn_layer_norm', zrows, L, f'd{i + 1}')
                 out = None if last else ws.get(f'x_dec{i + 1}', (T, d), f32)
             else:
-                if i > 0:
+                if i > 0 and not zf_batch:
                     K.gemm(zb, P.w(f'z_projections.{i}.weight'), xs, B, d, Z, ldc=L * d, epi=EPI_F32,
                            bias=P.f(f'z_projections.{i}.bias'))
                 nxt, out = None, ws.get(f'x_dec{i + 1}', (T, d), f32)
             xs, st = self.layer_fwd(f'decoder_layers.{i}.', xs, B, L, L, padm, causal=True, heads=self.H,
                                     hd=self.hd, drop_p=dropout, seed=_mix_seed(seed, i), tag=f'd{i}', out=out,
                                     window=self.window, fuse=fuse, h_in=h_in, next_ln=nxt,
-                                    out_bf=xf if last and (fuse or self.resid_bf16) else None)
+                                    out_bf=xf if last and (fuse or self.resid_bf16) else None,
+                                    zsplice=(zall[i], L) if zf_batch else None)
             h_in = st.pop('next_h', None)
             dec.append(st)
         if not fuse and not self.resid_bf16:

@@ -484,6 +484,30 @@ def zproj_bwd(g, z, W, dW, db, dz, B, d, Z):
                              B, d, Z, stream()), 'svae_zproj_bwd')
 
 
+_zfwd_segs = (N.ZprojFwdSeg * N.ZPROJ_MAX)()
+
+
+def zproj_fwd_multi(segs, z, B, d, Z):
+    """svae_zproj_fwd_multi: segs = [(W bf16 [d, Z], bias f32 [d], out f32 [B, d])] (<= 32): out = z W^T + bias."""
+    assert 0 < len(segs) <= N.ZPROJ_MAX
+    _dev(z)
+    assert z.dtype == bf16 and z.is_contiguous()
+    for i, (W, bias, out) in enumerate(segs):
+        _dev(W, bias, out)
+        assert W.dtype == bf16 and bias.dtype == f32 and out.dtype == f32 and out.is_contiguous()
+        _zfwd_segs[i].W, _zfwd_segs[i].bias, _zfwd_segs[i].out = W.data_ptr(), bias.data_ptr(), out.data_ptr()
+    check(lib.svae_zproj_fwd_multi(ctypes.addressof(_zfwd_segs), len(segs), z.data_ptr(), B, d, Z, stream()),
+          'svae_zproj_fwd_multi')
+
+
+def layernorm_fwd_z(x, zrows, zmod, w, b, y, mean, rstd, rows, D):
+    """svae_layernorm_fwd_z: LayerNorm forward of f32 x whose rows r % zmod == 0 come from zrows (and are written into x)."""
+    _dev(x, zrows, w, b, y, mean, rstd)
+    assert x.dtype == f32 and zrows.dtype == f32 and x.is_contiguous() and zrows.is_contiguous()
+    check(lib.svae_layernorm_fwd_z(x.data_ptr(), zrows.data_ptr(), zmod, w.data_ptr(), b.data_ptr(), y.data_ptr(),
+                                   mean.data_ptr(), rstd.data_ptr(), rows, D, stream()), 'svae_layernorm_fwd_z')
+
+
 _zproj_segs = (N.ZprojSeg * N.ZPROJ_MAX)()
 
 

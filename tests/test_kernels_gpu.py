@@ -478,6 +478,42 @@ def test_prep_tokens(B, L, mode):
 
 
 @pytest.mark.parametrize('n,B,d,Z', [(6, 64, 512, 64), (3, 5, 200, 70), (12, 130, 768, 128)])
+def test_zproj_fwd_multi(n, B, d, Z):
+    # n z projections in one launch: z W_i^T + b_i against torch fp32 on the same bf16 operands
+    torch.manual_seed(n + B + d + 1)
+    z = torch.randn(B, Z, device=dev).bfloat16()
+    Ws = [(torch.randn(d, Z, device=dev) * 0.1).bfloat16() for _ in range(n)]
+    bs = [torch.randn(d, device=dev) for _ in range(n)]
+    outs = [torch.full((B, d), float('nan'), device=dev) for _ in range(n)]
+    K.zproj_fwd_multi([(Ws[i], bs[i], outs[i]) for i in range(n)], z, B, d, Z)
+    torch.cuda.synchronize()
+    for i in range(n):
+        ref = z.float() @ Ws[i].float().t() + bs[i]
+        assert torch.allclose(outs[i], ref, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize('rows,L,D', [(64 * 512, 512, 512), (3 * 40, 40, 768), (7 * 16, 16, 256)])
+def test_layernorm_fwd_zsplice(rows, L, D):
+    # the layer's first LayerNorm with the z splice equals writing the z rows into x, then the plain LayerNorm
+    torch.manual_seed(rows + D)
+    x = torch.randn(rows, D, device=dev) * 2 + 0.3
+    zr = torch.randn(rows // L, D, device=dev)
+    w = torch.randn(D, device=dev) * 0.1 + 1
+    bb = torch.randn(D, device=dev) * 0.1
+    x_ref = x.clone()
+    x_ref[::L] = zr
+    y0 = torch.empty(rows, D, device=dev, dtype=torch.bfloat16)
+    m0, r0 = torch.empty(rows, device=dev), torch.empty(rows, device=dev)
+    K.layernorm_fwd(x_ref, w, bb, y0, m0, r0, rows, D)
+    y1 = torch.empty(rows, D, device=dev, dtype=torch.bfloat16)
+    m1, r1 = torch.empty(rows, device=dev), torch.empty(rows, device=dev)
+    K.layernorm_fwd_z(x, zr, L, w, bb, y1, m1, r1, rows, D)
+    torch.cuda.synchronize()
+    assert torch.equal(x, x_ref)
+    assert torch.equal(y1, y0) and torch.equal(m1, m0) and torch.equal(r1, r0)
+
+
+@pytest.mark.parametrize('n,B,d,Z', [(6, 64, 512, 64), (3, 5, 200, 70), (12, 130, 768, 128)])
 def test_zproj_bwd_multi_matches_sequential(n, B, d, Z):
     # n z-projection backwards in one launch equal n svae_zproj_bwd calls in list order, bit for bit (dW, db, dz)
     torch.manual_seed(n + B + d)

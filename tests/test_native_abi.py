@@ -94,3 +94,11 @@ def test_zproj_seg_layout():
     assert [f[0] for f in N.ZprojSeg._fields_] == ['g', 'W', 'dW', 'db']
     hdr = open(os.path.join(ROOT, 'include', 'svae.h')).read()
     assert '#define SVAE_ZPROJ_MAX 32' in hdr and N.ZPROJ_MAX == 32
+
+
+def test_zproj_fwd_seg_layout():
+    """svae_zproj_fwd_seg: three pointers, 24 B, in header order."""
+    import ctypes
+    from sparse_vae import _native as N
+    assert ctypes.sizeof(N.ZprojFwdSeg) == 24
+    assert [f[0] for f in N.ZprojFwdSeg._fields_] == ['W', 'bias', 'out']
