@@ -174,7 +174,8 @@ class Trainer:
                         if world > 1 and hasattr(model, 'reduce_logged'):
                             model.reduce_logged()          # rank means of the logged scalars
                         if rank == 0 and self.global_step % self.log_every_n_steps == 0:
-                            logs = {k: _scalar(v) for k, v in model.logged.items()}
+                            logs = (model.logged_values() if hasattr(model, 'logged_values')
+                                    else {k: _scalar(v) for k, v in model.logged.items()})
                             logs['step'] = self.global_step
                             logs['elapsed_s'] = round(time.time() - t0, 2)
                             self.history.append(logs)

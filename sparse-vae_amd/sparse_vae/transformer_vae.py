@@ -102,6 +102,8 @@ class TransformerVAE(ContinuousVAEHooks, LanguageModel):
         self._norm_part = None
         self._norm_valid = False
         self._dp = None
+        self._log_consts = None
+        self.logged_reduced = {}
         self._step_seed = 7295
         # DDP's flag (Lightning sets it through no_sync under accumulate_grad_batches): False marks a gradient-
         # accumulation micro-step that no optimiser step follows -- its backward runs no all-reduce (the final
@@ -327,25 +329,39 @@ class TransformerVAE(ContinuousVAEHooks, LanguageModel):
         transformer_vae.py:61). One all-reduce of a FIXED-length vector: for every key of `keys`, the value (0 where
         this rank did not log it) and a presence count, so ranks whose batches log different key sets (a
         1-sequence token-budget batch logs no `train_mc_mutual_info`) still issue identical collectives; a key
-        is the mean over the ranks that logged it, and is dropped where no rank did. On RCCL `wait()` only orders
-        the caller's stream after it (no host synchronisation). Every rank calls it at the same optimiser steps
-        (the trainer does, once per optimiser step)."""
+        is the mean over the ranks that logged it, and is dropped where no rank did. Everything stays on the
+        device: the vector is stacked from device scalars (no host-to-device copy), `wait()` on RCCL only orders
+        the caller's stream after the collective, and the means and presence counts land in `logged_reduced`
+        (device tensors). `logged_values()` reads them back to the host -- the trainer calls it only where it
+        prints a log line (rank 0, every log_every_n_steps), so an optimiser step carries no host synchronisation.
+        Every rank calls it at the same optimiser steps (the trainer does, once per optimiser step)."""
         dp = self._dp
         if dp is None:
             return
         keys = tuple(keys)
-        zero = torch.zeros((), dtype=torch.float32, device=self.device)
-        vals = torch.stack([torch.as_tensor(self.logged[k], dtype=torch.float32, device=self.device).reshape(())
-                            if k in self.logged else zero for k in keys]
-                           + [torch.tensor(float(k in self.logged), device=self.device) for k in keys])
+        if self._log_consts is None or self._log_consts[0].device != self._flat.master.device:
+            dev = self._flat.master.device
+            self._log_consts = (torch.zeros((), dtype=torch.float32, device=dev),
+                                torch.ones((), dtype=torch.float32, device=dev))
+        zero, one = self._log_consts
+        present = [k in self.logged for k in keys]
+        vals = torch.stack([torch.as_tensor(self.logged[k], dtype=torch.float32, device=zero.device).reshape(())
+                            if p else zero for k, p in zip(keys, present)]
+                           + [one if p else zero for p in present])
         dist.all_reduce(vals, op=dist.ReduceOp.SUM, group=dp['group'], async_op=True).wait()
         n = len(keys)
-        counts = vals[n:].tolist()
-        for i, k in enumerate(keys):
-            if counts[i] > 0:
-                self.logged[k] = vals[i] / counts[i]
-            else:
-                self.logged.pop(k, None)
+        means = vals[:n] / vals[n:].clamp_min(1.0)
+        self.logged_reduced = {k: (means[i], vals[n + i]) for i, k in enumerate(keys)}
+
+    def logged_values(self):
+        """Host values of the logged scalars: the data-parallel means of `reduce_logged` where a reduction ran
+        (a key no rank logged is dropped: its presence count is read here), the local values otherwise. One
+        host synchronisation; call it only where the values are printed."""
+        out = {k: v for k, v in self.logged.items() if k not in self.logged_reduced}
+        for k, (mean, count) in self.logged_reduced.items():
+            if float(count) > 0:
+                out[k] = mean
+        return {k: (v.item() if torch.is_tensor(v) else v) for k, v in out.items()}
 
     # ------------------------------------------------------------------ inference-side helpers
     @torch.no_grad()

@@ -50,9 +50,8 @@ def _worker(rank, world, port, bucket_mb, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize('bucket_mb', [0.5, 64.0])
-def test_gradients_are_averaged_and_weights_broadcast(bucket_mb):
-    world = 2
+@pytest.mark.parametrize('world,bucket_mb', [(2, 0.5), (2, 64.0), (4, 0.5)])
+def test_gradients_are_averaged_and_weights_broadcast(world, bucket_mb):
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     port = _free_port()
@@ -63,14 +62,68 @@ def test_gradients_are_averaged_and_weights_broadcast(bucket_mb):
     for p in ps:
         p.join(timeout=60)
         assert p.exitcode == 0
-    (_, w0, g0, d0), (_, w1, g1, d1) = [(r, *(torch.from_numpy(a) for a in t)) for r, *t in res]
-    assert torch.equal(w0, w1)                         # rank 0's weights everywhere
+    ranks = [[torch.from_numpy(a) for a in t] for _, *t in res]
+    w0, g0, d0 = ranks[0]
     n = g0.numel()
-    expect = torch.arange(n, dtype=torch.float32) * 1e-6 + 0.5      # mean over ranks of (base + rank)
+    expect = torch.arange(n, dtype=torch.float32) * 1e-6 + (world - 1) / 2    # mean over ranks of (base + rank)
     torch.testing.assert_close(g0, expect, rtol=1e-6, atol=1e-6)
-    assert torch.equal(g0, g1)
-    # gradients of parameters that never receive one (pos_linear) are not communicated
-    assert not torch.equal(d0, d1)
+    for w1, g1, d1 in ranks[1:]:
+        assert torch.equal(w0, w1)                     # rank 0's weights everywhere
+        assert torch.equal(g0, g1)
+        # gradients of parameters that never receive one (pos_linear) are not communicated
+        assert not torch.equal(d0, d1)
+
+
+GLOBAL_B = 8
+
+
+def _sample_grad(total, s):
+    """Per-sequence gradient of sample s of the global batch (distinct per sample and per element)."""
+    return torch.arange(total, dtype=torch.float64) * 1e-6 * (s + 1) + torch.sin(torch.tensor(float(s))) * 3
+
+
+def _worker_shard(rank, world, port, q):
+    """The global batch of GLOBAL_B sequences sharded over `world` ranks (equal shards, RankBatchSampler's
+    split): each rank's backward leaves its local mean / world in the arena, the model's buckets all-reduce."""
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'sparse-vae_amd'))
+    from sparse_vae import TransformerVAE, TransformerVAEHparams
+    hp = TransformerVAEHparams(d_model=128, num_layers=4, num_heads=8, sparse_self_attention=False)
+    m = TransformerVAE(hp, device='cpu')
+    m.enable_data_parallel(bucket_mb=0.25)
+    flat = m._flat
+    per = GLOBAL_B // world
+    local = sum(_sample_grad(flat.total, s) for s in range(rank * per, (rank + 1) * per)) / per
+    flat.grad.copy_((local / world).float())
+    for end in _ready_sequence(flat, m._ehp):
+        m._dp_ready(end)
+    m._dp_finish()
+    q.put((rank, flat.grad[:flat.n_live].numpy().copy()))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('world', [1, 2, 4, 8])
+def test_world_sizes_give_the_global_batch_gradient(world):
+    """ranks 1 / 2 / 4 / 8 over the same global batch give the same averaged gradient -- the
+    global-batch mean -- on every rank."""
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker_shard, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in range(world)], key=lambda r: r[0])
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    g0 = torch.from_numpy(res[0][1]).double()
+    n = g0.numel()
+    expect = sum(_sample_grad(n, s) for s in range(GLOBAL_B)) / GLOBAL_B
+    torch.testing.assert_close(g0, expect, rtol=2e-6, atol=2e-6)
+    for _, g in res[1:]:
+        assert torch.equal(torch.from_numpy(g), torch.from_numpy(res[0][1]))
 
 
 class _FakeEngine:
@@ -112,10 +165,10 @@ def _worker_accum(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_gradient_accumulation_reduces_once():
+@pytest.mark.parametrize('world', [2, 4])
+def test_gradient_accumulation_reduces_once(world):
     """DP + accumulate_grad_batches=2 (the train.py default, train.py:16-23): the result is the rank-mean of
     each rank's summed micro-gradients -- the first micro-step's gradient is not reduced twice."""
-    world = 2
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     port = _free_port()
@@ -126,13 +179,14 @@ def test_gradient_accumulation_reduces_once():
     for p in ps:
         p.join(timeout=60)
         assert p.exitcode == 0
-    g0, g1 = torch.from_numpy(res[0][1]), torch.from_numpy(res[1][1])
+    g0 = torch.from_numpy(res[0][1])
     n = g0.numel()
     ar = torch.arange(n, dtype=torch.float32) * 1e-6
-    # sum over k = 1, 2 of (ar * k + rank + 10 k), averaged over ranks 0, 1
-    expect = ar * 3 + 0.5 * 2 + 30
+    # sum over k = 1, 2 of (ar * k + rank + 10 k), averaged over the ranks
+    expect = ar * 3 + (world - 1) / 2 * 2 + 30
     torch.testing.assert_close(g0, expect, rtol=1e-6, atol=1e-5)
-    assert torch.equal(g0, g1)
+    for _, g in res[1:]:
+        assert torch.equal(g0, torch.from_numpy(g))
 
 
 def _fake_sumsq(g, n, part):
@@ -179,7 +233,8 @@ def _worker_clip(rank, world, port, q):
     m.logged.update({'train_nll': torch.tensor(1.0 + rank), 'train_kl': torch.tensor(10.0 * (rank + 1)),
                      'loss': torch.tensor(3.0 - rank)})
     m.reduce_logged()
-    red = {k: float(m.logged[k]) for k in ('train_nll', 'train_kl', 'loss')}
+    vals = m.logged_values()
+    red = {k: vals[k] for k in ('train_nll', 'train_kl', 'loss')}
     q.put((rank, logged_norm, (clipped.double() * world).norm().item(), (clipped.double() * world / v.double()).std().item(), sync_norm, red))
     dist.destroy_process_group()
 

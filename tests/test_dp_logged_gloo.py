@@ -55,11 +55,13 @@ def _worker(rank, world, port, q):
     if rank == 0:
         m.logged['train_mc_mutual_info'] = torch.tensor(0.75)
     m.reduce_logged()
-    step1 = {k: float(v) for k, v in m.logged.items()}
+    # the reduction stays on the device; logged_values() is the one host read (the trainer's log point)
+    assert all(torch.is_tensor(v) for v, _ in m.logged_reduced.values())
+    step1 = m.logged_values()
     # step 2: no rank logged it -> the key disappears everywhere (no stale value is reduced again)
     m.logged.pop('train_mc_mutual_info', None)
     m.reduce_logged()
-    step2 = sorted(m.logged)
+    step2 = sorted(m.logged_values())
     # validation: rank 0 runs 3 batches with both keys, rank 1 runs 2 batches with val_nll only
     tr = Trainer()
     tr.datamodule = _DM(3 if rank == 0 else 2)
