@@ -7,7 +7,8 @@
 `--gpus N` (N > 1) without WORLD_SIZE in the environment: this process launches the N ranks itself (one child
 per GPU with the torchrun environment, as Lightning's Trainer(gpus=N) does for the reference, train.py:63-64, 94),
 never touching the GPU; it exits non-zero at once when fewer than N GPUs are visible. At N > 1 the line also
-carries `scaling_efficiency` against a same-run N=1 rate (all-reduce off, after the timed region).
+carries `scaling_efficiency` against a same-run N=1 rate (all-reduce off, after the timed region) and
+`exposed_comm_ms`: the part of the gradient all-reduce the backward did not hide, per step, max over ranks.
 
 A step = TransformerVAE.training_step (forward) + loss.backward() (engine backward with the bucketed RCCL
 gradient all-reduce overlapped) + on_after_backward (grad norm, KL anneal) + RAdam.step (fused clip +
@@ -295,6 +296,8 @@ def main():
     # dominant-kernel timing: HIP events around every vocab-head GEMM launch of the timed steps
     probes = []
     eng.probe = probes
+    comm = [] if world > 1 else None
+    model.comm_probe = comm
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -306,10 +309,18 @@ def main():
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     eng.probe = None
+    model.comm_probe = None
+    exposed = None
     if world > 1:
         t = torch.tensor([dt], device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = t.item()
+        # exposed communication per step: the compute stream's wait for the gradient all-reduce past the end of the
+        # backward (the buckets launched during the backward overlap it; what remains is this tail), max over ranks
+        ex = sum(a.elapsed_time(b) for a, b in comm) / max(1, len(comm))
+        te = torch.tensor([ex], device=device)
+        dist.all_reduce(te, op=dist.ReduceOp.MAX)
+        exposed = te.item()
     ms = dt / args.steps * 1e3
     tokens = cfg['B'] * cfg['L'] * world * args.steps
     value = tokens / dt
@@ -371,6 +382,10 @@ def main():
         }
         if scaling is not None:
             res['scaling_efficiency'] = scaling
+        if exposed is not None:
+            res['exposed_comm_ms'] = {'value': round(exposed, 4), 'fraction_of_step': round(exposed / ms, 4),
+                                      'basis': 'HIP events on the compute stream from the end of the backward to the '
+                                               'last bucket all-reduce wait, mean over the timed steps, max over ranks'}
         if os.environ.get('SVAE_BENCH_SHARE_GPUS') == '1':
             res['rehearsal'] = (f'NOT a measurement: {world} ranks share {torch.cuda.device_count()} GPU(s), backend '
                                 f'{os.environ.get("SVAE_DIST_BACKEND", "nccl")}')

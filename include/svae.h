@@ -203,6 +203,11 @@ typedef struct svae_attn_desc {
   /* backward: 1 = delta already holds rowsum(dO . O) (svae_gemm's delta epilogue on the dO GEMM): the delta pass is
      skipped */
   int32_t delta_ready;
+  /* optional bf16 residual of O (the alternative to o32, 2 B per element instead of 4): the forward writes
+     o_lo = bf16(O - bf16(O)) (row stride so_lo, batch stride bo_lo), the backward's delta pass reads dO . (o + o_lo):
+     O to ~16 significant bits, where the f32-accumulated O itself carries ~19 */
+  void* o_lo;
+  int64_t so_lo, bo_lo;
 } svae_attn_desc;
 
 int svae_attn_fwd(const svae_attn_desc* d, svae_stream_t stream);

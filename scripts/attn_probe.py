@@ -36,17 +36,19 @@ def main():
           continue
       if only == 'c2c4' and (B, L, causal, hd) not in ((64, 512, True, 64), (64, 1024, True, 96)):
           continue
-      for with_o32 in (True, False):
+      for with_o32 in (True, 'olo', False):
         H = 8
-        if not with_o32 and (B, L, hd) != (64, 512, 64):
+        if with_o32 is not True and (B, L, hd) != (64, 512, 64) and not only:
             continue
         d = H * hd
         qkv = torch.randn(B * L, 3 * d, device=dev).bfloat16()
         o = torch.empty(B * L, d, device=dev).bfloat16()
         o32 = torch.empty(B * L, d, device=dev)
         lse = torch.empty(B, H, L, device=dev)
+        olo = torch.empty(B * L, d, device=dev).bfloat16()
         kw = dict(B=B, H=H, Lq=L, Lk=L, hd=hd, sq=3 * d, sk=3 * d, sv=3 * d, so=d, bq=L * 3 * d, bk=L * 3 * d,
-                  bv=L * 3 * d, bo=L * d, causal=causal, o32=o32 if with_o32 else None, so32=d, bo32=L * d)
+                  bv=L * 3 * d, bo=L * d, causal=causal, o32=o32 if with_o32 is True else None, so32=d, bo32=L * d,
+                  o_lo=olo if with_o32 == 'olo' else None, so_lo=d, bo_lo=L * d)
         fwd = lambda: K.attention(qkv, qkv[:, d:], qkv[:, 2 * d:], o, lse, **kw)
         t = timeit(fwd)
         fl = 4.0 * B * H * L * L * hd * (0.5 if causal else 1.0)
@@ -61,7 +63,8 @@ def main():
             print(f'B={B:4d} L={L:5d} hd={hd:3d} causal={int(causal)} no-o32 fwd {t:8.1f} us', flush=True)
             continue
         tb = timeit(bwd)
-        print(f'B={B:4d} L={L:5d} hd={hd:3d} causal={int(causal)}  fwd {t:8.1f} us {fl / t / 1e6:7.1f} TF/s   '
+        tag = 'o32' if with_o32 is True else 'olo'
+        print(f'B={B:4d} L={L:5d} hd={hd:3d} causal={int(causal)} {tag} fwd {t:8.1f} us {fl / t / 1e6:7.1f} TF/s   '
               f'bwd(+delta+dq) {tb:8.1f} us {2.5 * fl / tb / 1e6:7.1f} TF/s', flush=True)
 
 

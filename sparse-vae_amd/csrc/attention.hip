@@ -17,6 +17,7 @@
 // atomics) and attn_dq_reduce_kernel sums the slices in a fixed order (deterministic).
 #include "common.h"
 #include <algorithm>
+#include <type_traits>
 #include "../../include/svae.h"
 
 using namespace svae;
@@ -37,6 +38,7 @@ struct AP {
   const float* rot; int rot_d;
   float* o32; long long so32, bo32;
   float* dq_part; void* dq_bf; long long ldq_bf;
+  bf16* olo; long long solo, bolo;   // bf16 residual O - bf16(O) (alternative to o32)
   int window;        // > 0: causal sliding window of `window` 32-key blocks plus key block 0 (SparseAttention)
   int kblk;          // backward: keys per dQ partial (the key block of the kernel that wrote dq_part)
   int dq_direct;     // backward (attn_bwd8, causal): key block 0 stores the final dQ of queries < 256 itself
@@ -210,6 +212,11 @@ constexpr float LOG2E = 1.4426950408889634f;
 __device__ __forceinline__ void wait_vmcnt(int n) {
   switch (n) {
     case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
     case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
     case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
     case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
@@ -495,6 +502,23 @@ __device__ __forceinline__ void attn_fwd_tile(const AP& p, char* smem, int bx, i
       }
       if (p.o32)
         store_rows_f32<true, NP>(p.o32 + b * p.bo32 + (long long)h * HDC, p.so32, qw + 16 * j, p.Lq, 0, HDC, v, g, li);
+      if (p.olo) {   // bf16 residual O - bf16(O)
+        f32x4 lo[2 * NP];
+#pragma unroll
+        for (int t = 0; t < 2 * NP; ++t)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) lo[t][e] = v[t][e] - (float)f2bf(v[t][e]);
+        bf16* OL = p.olo + b * p.bolo + (long long)h * HDC;
+        store_rows_bf16<false>(OL, p.solo, qw + 16 * j, p.Lq, 0, 64, *(const f32x4(*)[4])lo, g, li);
+        if (HDC == 96 && qrow < p.Lq) {
+#pragma unroll
+          for (int t = 4; t < 2 * NP; ++t) {
+            const int d = 16 * t + 4 * g;
+            *(bf16x4*)(OL + (long long)qrow * p.solo + d) =
+                (bf16x4){f2bf(lo[t][0]), f2bf(lo[t][1]), f2bf(lo[t][2]), f2bf(lo[t][3])};
+          }
+        }
+      }
       if (g == 0 && qrow < p.Lq) p.lse[((long long)b * p.H + h) * p.Lq + qrow] = m[j] * p.scale + __logf(lsum);
     }
   } else {
@@ -512,6 +536,10 @@ __device__ __forceinline__ void attn_fwd_tile(const AP& p, char* smem, int bx, i
           const f32x4 v = o[j][t] * inv;
           *(bf16x4*)(O + d) = (bf16x4){f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
           if (p.o32) *(f32x4*)(p.o32 + b * p.bo32 + (long long)h * p.hd + (long long)qrow * p.so32 + d) = v;
+          if (p.olo)
+            *(bf16x4*)(p.olo + b * p.bolo + (long long)h * p.hd + (long long)qrow * p.solo + d) =
+                (bf16x4){f2bf(v[0] - (float)f2bf(v[0])), f2bf(v[1] - (float)f2bf(v[1])), f2bf(v[2] - (float)f2bf(v[2])),
+                         f2bf(v[3] - (float)f2bf(v[3]))};
         }
       }
       if (g == 0) p.lse[((long long)b * p.H + h) * p.Lq + qrow] = m[j] * p.scale + __logf(lsum);
@@ -534,6 +562,358 @@ __global__ __launch_bounds__(256, HDC <= 96 ? 3 : 2) void attn_fwd_kernel(AP p) 
   attn_fwd_tile<HDP, HDC>(p, smem, bx, h, b);
 }
 
+// ===================================================================================== forward, 32 x 32 MFMA form
+// attn_fwd32_kernel<HDC> (HDC = 64: hd <= 64, zero-padded; HDC = 96): the same flash forward as attn_fwd_kernel, with
+// v_mfma_f32_32x32x16_bf16 instead of 16x16x32 and a deferred running max. Why (the forward is issue-bound: per 64-key
+// tile a wave issues ~930 cycles of VALU + MFMA beside 512 cycles of MFMA work, §6):
+//  * a 32x32x16 MFMA holds the SIMD's vector issue for 8 of its 32 cycles, the 16x16x32 form for 8 of 16: half the
+//    MFMA issue cost for the same flops (MI355X_MICROARCH.md, 'vector-instruction ISSUE cost');
+//  * S^T = K . Q^T puts ONE query on each lane (column = lane & 31) with 16 keys per 32-key tile in the registers, so a
+//    row reduction is in-lane plus one permlane32 swap, and the accumulator is the B operand of O^T += V^T . P^T with no
+//    lane movement (cdna_hip_programming.md §3, 'An accumulator tile as the next MFMA's operand');
+//  * no per-tile row max: p = exp2(s c - m c) against the running reference m, and only when some lane's tile sum
+//    exceeds 2^16 (or is not finite) does the wave take the rescale path (recompute S, true max, rescale O and l).
+//    Every p then stays <= 2^16 (bf16 keeps its relative precision at any magnitude; O and l accumulate in f32), and
+//    the lse = m scale + ln l is exact for any reference m. A wave's first live tile sets m to the true max.
+// K / V images: 64 key rows, 16-B chunks XOR-swizzled so that both the row-wise ds_read_b128 K reads (lane = key row
+// 0..31) and the transposed ds_read_b64_tr_b16 V reads (4 consecutive rows x 4 chunks per 32 lanes) are conflict-free.
+template <int HDC>
+struct KVImg {
+  static_assert(HDC == 64 || HDC == 96, "KVImg: 64 or 96 dims");
+  static constexpr int BYTES = 64 * HDC * 2;         // 8 / 12 KiB
+  static constexpr int PIECES = BYTES / 1024;        // LDS-DMA wave-instructions per image
+  // dims 0-63: 128-B rows, chunk c at c ^ F(r). b128 reads: the 8 even (odd) rows of a 16-lane group get 8 distinct
+  // chunks; tr reads: rows r0, r0 + 2 (r0 % 4 == 0) differ in bit 2 of F, so their 4-chunk groups are disjoint.
+  __device__ static __forceinline__ int F(int r) { return (((r >> 1) & 1) << 2) | ((r >> 2) & 3); }
+  // dims 64-95 (HDC 96): 64-B rows at 8192, chunk c at c ^ T(r): the 4 rows of each r % 4 class in a 16-lane b128 group
+  // get 4 distinct chunks
+  __device__ static __forceinline__ int T(int r) { return ((r >> 2) ^ (r >> 3)) & 3; }
+  __device__ static __forceinline__ int off(int r, int c) {
+    if (HDC == 64 || c < 8) return r * 128 + ((c ^ F(r)) << 4);
+    return 8192 + r * 64 + (((c - 8) ^ T(r)) << 4);
+  }
+  // the source row r and logical chunk c of lane `lane`'s 16-B slot in DMA piece i
+  __device__ static __forceinline__ void piece_src(int i, int lane, int& r, int& c) {
+    if (HDC == 64 || i < 8) {
+      r = 8 * i + (lane >> 3);
+      c = (lane & 7) ^ F(r);
+    } else {
+      r = 16 * (i - 8) + (lane >> 2);
+      c = 8 + ((lane & 3) ^ T(r));
+    }
+  }
+};
+
+__device__ __forceinline__ f32x16 mfma32(const bf16x8& a, const bf16x8& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ bf16x8 lds_read_b128(const lds_char* p) {
+  return *(const __attribute__((address_space(3))) bf16x8*)p;
+}
+// registers 8 s .. 8 s + 7 of a 32x32 accumulator as a bf16 fragment (k-step s of the next product)
+__device__ __forceinline__ bf16x8 pack_acc8(const f32x16& x, int s) {
+  return (bf16x8){f2bf(x[8 * s]), f2bf(x[8 * s + 1]), f2bf(x[8 * s + 2]), f2bf(x[8 * s + 3]),
+                  f2bf(x[8 * s + 4]), f2bf(x[8 * s + 5]), f2bf(x[8 * s + 6]), f2bf(x[8 * s + 7])};
+}
+// reductions over the lane pair (l, l ^ 32) (one permlane32 swap: each lane gets its own and its partner's value)
+__device__ __forceinline__ float max_x32(float v) {
+  auto c = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(c[0]), __uint_as_float(c[1]));
+}
+__device__ __forceinline__ float sum_x32(float v) {
+  auto c = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(c[0]) + __uint_as_float(c[1]);
+}
+
+#ifndef SVAE_FWD32_DIAG
+#define SVAE_FWD32_DIAG 0   // diagnostic builds only (scripts/build_variant.sh ... -DSVAE_FWD32_DIAG=n): 1 no tile body, 2 no
+#endif                      // exp2 / fma, 3 one S MFMA per subtile, 4 one PV MFMA per k-step; results are wrong
+constexpr int FWD32_MAXPAD = 4096;    // keys whose padding bits fit the block's LDS bit mask
+constexpr float FWD32_THRESH = 65536.f;
+
+template <int HDC, int OCC, int NS>
+__global__ __launch_bounds__(256, OCC) void attn_fwd32_kernel(AP p) {
+  using I = KVImg<HDC>;                 // NS: K / V ring stages (NS - 1 tiles ahead)
+  constexpr int KS = HDC / 16;          // k-steps of S = Q K^T
+  constexpr int DT = HDC / 32;          // 32-dim tiles of O^T
+  constexpr int PW = I::PIECES / 4;     // DMA pieces per wave per image
+  __shared__ __attribute__((aligned(16))) char smem[NS * 2 * I::BYTES + FWD32_MAXPAD / 8];
+  int bx, h, b;
+  xcd_block(bx, h, b, p.causal ? 1 : 0);
+  const int tid = threadIdx.x, lane = tid & 63, r32 = lane & 31, hh = lane >> 5;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int q0 = bx * 128, qw = q0 + 32 * w, qrow = qw + r32;
+  const bf16* Q = p.q + b * p.bq + (long long)h * p.hd;
+  const bf16* K = p.k + b * p.bk + (long long)h * p.hd;
+  const bf16* V = p.v + b * p.bv + (long long)h * p.hd;
+
+  // Q fragments (B operand of S^T = K Q^T): lane holds Q[qrow][16 ks + 8 hh .. + 7]
+  bf16x8 qf[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    const int d = 16 * ks + 8 * hh;
+    u32x4 v = {0u, 0u, 0u, 0u};
+    if (qrow < p.Lq && d < p.hd) v = *(const u32x4*)(Q + (long long)qrow * p.sq + d);
+    qf[ks] = __builtin_bit_cast(bf16x8, v);
+  }
+  // key padding as a bit mask in LDS (bit k of word k / 64), built once per block by ballots: plain loads, read after
+  // the first tile's barrier (no per-tile DMA ring, no wave reading another wave's DMA)
+  const unsigned char* pad = p.pad ? p.pad + (long long)b * p.Lk : nullptr;
+  unsigned long long* pbits = (unsigned long long*)(smem + NS * 2 * I::BYTES);
+  if (pad) {
+    for (int k0 = 64 * w; k0 < p.Lk; k0 += 256) {
+      const int key = k0 + lane;
+      const unsigned long long bal = __builtin_amdgcn_ballot_w64(key < p.Lk && pad[key] != 0);
+      if (lane == 0) pbits[k0 >> 6] = bal;
+    }
+  }
+
+  const int kv_end = p.causal ? min(p.Lk, q0 + 128) : p.Lk;
+  const int ntiles = (kv_end + 63) / 64;
+  const int kt1 = max(1, band_lo(q0, p.window) / 64);   // tile 0, then the band from kt1 (dense: all tiles)
+  const int nvisit = 1 + max(0, ntiles - kt1);
+  const int lo_w = band_lo(qw, p.window);
+  const u32x4 krs = buffer_rsrc(K, 0x7FFFFFF0u), vrs = buffer_rsrc(V, 0x7FFFFFF0u);
+  auto issue = [&](int it2) {
+    const int kn = (it2 == 0 ? 0 : kt1 + it2 - 1) * 64;
+    char* kb = smem + (it2 % NS) * 2 * I::BYTES;
+    const int ln = lane_id_fresh();   // (offsets recomputed at the issue, never kept live across the key loop)
+#pragma unroll
+    for (int i = 0; i < PW; ++i) {
+      int r, c;
+      I::piece_src(w * PW + i, ln, r, c);
+      const bool ok = kn + r < p.Lk && c * 8 < p.hd;
+      dma16_lds(krs, kb + (w * PW + i) * 1024, ok ? ((kn + r) * (int)p.sk + c * 8) * 2 : 0x7FFFFFF0);
+      dma16_lds(vrs, kb + I::BYTES + (w * PW + i) * 1024, ok ? ((kn + r) * (int)p.sv + c * 8) * 2 : 0x7FFFFFF0);
+    }
+  };
+#pragma unroll
+  for (int t = 0; t < NS - 1; ++t)
+    if (t < nvisit) issue(t);
+  // consume the Q fragments after the first DMA is in flight (the compiler's wait for them is a vmcnt(0): here it costs
+  // nothing, inside the loop it would drain the ring)
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) asm volatile("" ::"v"(__builtin_bit_cast(u32x4, qf[ks])));
+
+  // per-lane LDS offsets (stage 0, key subtile 0). K (A operand of S^T, ds_read_b128): row r32, chunk 2 ks + hh.
+  int koff[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) koff[ks] = I::off(r32, 2 * ks + hh);
+  // V (A operand of O^T, ds_read_b64_tr_b16): lane 16 G + 4 q + p reads row 16 s + 8 j2 + 4 (G >> 1) + q, dims
+  // 32 dt + 16 (G & 1) + 4 p; dims < 64 need one offset per (dt, j2), the 96-dim tail one per (s, j2)
+  const int G = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
+  int voff[2][2], vtail[2][2];
+#pragma unroll
+  for (int j2 = 0; j2 < 2; ++j2) {
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) {
+      const int row = 8 * j2 + 4 * (G >> 1) + qq;
+      voff[dt][j2] = I::off(row, 4 * dt + 2 * (G & 1) + (pp >> 1)) + 8 * (pp & 1);
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const int row = 16 * s2 + 8 * j2 + 4 * (G >> 1) + qq;
+      vtail[s2][j2] = HDC == 96 ? I::off(row, 8 + 2 * (G & 1) + (pp >> 1)) + 8 * (pp & 1) : 0;
+    }
+  }
+
+  f32x16 o[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) o[dt][i] = 0.f;
+  const float c = p.scale * LOG2E;
+  float m = -1e30f, mc = m * c, ls = 0.f;   // reference point of this lane's query (raw score units), row sum
+  bool started = false;                      // wave-uniform: the first live tile sets m to the true max
+
+  auto tile = [&](auto STC, int kbase, bool edge, bool diag_only, unsigned long long pm) {
+    constexpr int ST = decltype(STC)::value;
+    const lds_char* Ks = lds_ptr(smem) + ST * 2 * I::BYTES;
+    const lds_char* Vs = Ks + I::BYTES;
+    // the limits of this lane's keys kl = 32 kt2 + (i & 3) + 8 (i >> 2) + 4 hh: visible iff kl < lim
+    const int lim = (p.causal ? min(p.Lk, qrow + 1) : p.Lk) - kbase - 4 * hh;
+    const int hlo = SBLK - kbase - 4 * hh, hhi = lo_w - kbase - 4 * hh;
+    const unsigned long long pml = pm >> (4 * hh);
+    auto compute_s = [&](f32x16 (&s)[2]) {
+#pragma unroll
+      for (int kt2 = 0; kt2 < 2; ++kt2) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) s[kt2][i] = 0.f;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+#if SVAE_FWD32_DIAG == 3
+          if (ks) break;   // diagnostic build: one S MFMA per subtile
+#endif
+          s[kt2] = mfma32(lds_read_b128(Ks + koff[ks] + kt2 * 32 * (2 * ks < 8 ? 128 : 64)), qf[ks], s[kt2]);
+        }
+      }
+      // (wave-uniform branches outside the unrolled element loops: inside them the compiler kept a branch per score)
+      if (edge && diag_only) {
+#pragma unroll
+        for (int kt2 = 0; kt2 < 2; ++kt2)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int kc = 32 * kt2 + (i & 3) + 8 * (i >> 2);   // kl - 4 hh
+            s[kt2][i] = kc < lim ? s[kt2][i] : -INFINITY;
+          }
+      } else if (edge) {
+        const unsigned plo = (unsigned)pml, phi = (unsigned)(pml >> 32);
+#pragma unroll
+        for (int kt2 = 0; kt2 < 2; ++kt2)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int kc = 32 * kt2 + (i & 3) + 8 * (i >> 2);
+            const unsigned pb = kc < 32 ? (plo >> kc) & 1u : (phi >> (kc - 32)) & 1u;
+            const unsigned hid = pb | ((unsigned)(kc >= hlo) & (unsigned)(kc < hhi)) | (unsigned)(kc >= lim);
+            s[kt2][i] = hid ? -INFINITY : s[kt2][i];
+          }
+      }
+    };
+    auto row_max = [&](const f32x16 (&s)[2]) {
+      float mx = -INFINITY;
+#pragma unroll
+      for (int kt2 = 0; kt2 < 2; ++kt2)
+#pragma unroll
+        for (int i = 0; i < 16; i += 2) mx = fmaxf(fmaxf(mx, s[kt2][i]), s[kt2][i + 1]);
+      return max_x32(mx);
+    };
+    auto exps = [&](f32x16 (&s)[2]) {
+      float l0 = 0.f, l1 = 0.f;
+#pragma unroll
+      for (int kt2 = 0; kt2 < 2; ++kt2)
+#pragma unroll
+        for (int i = 0; i < 16; i += 2) {
+#if SVAE_FWD32_DIAG == 2
+          const float e0 = s[kt2][i] * 1e-3f, e1 = s[kt2][i + 1] * 1e-3f;   // diagnostic build: no exp2 / fma
+#else
+          const float e0 = __builtin_amdgcn_exp2f(fmaf(s[kt2][i], c, -mc));
+          const float e1 = __builtin_amdgcn_exp2f(fmaf(s[kt2][i + 1], c, -mc));
+#endif
+          s[kt2][i] = e0;
+          s[kt2][i + 1] = e1;
+          l0 += e0;
+          l1 += e1;
+        }
+      return l0 + l1;
+    };
+#if SVAE_FWD32_DIAG == 1
+    return;   // diagnostic build: DMA, barriers, prologue and epilogue only
+#endif
+    f32x16 s[2];
+    compute_s(s);
+    if (!started) {
+      m = fmaxf(m, row_max(s));
+      mc = m * c;
+      started = true;
+    }
+    float lt = exps(s);
+    if (__builtin_amdgcn_ballot_w64(!(lt <= FWD32_THRESH)) != 0) {
+      // the max grew by more than 16 (log2 units) on some row: recompute S, move the reference to the true max (the
+      // clobber makes the compiler re-read the K fragments here instead of keeping 32 VGPRs of them live across the
+      // exponentials of the common path)
+      asm volatile("" ::: "memory");
+      compute_s(s);
+      const float mn = fmaxf(m, row_max(s));
+      const float alpha = __builtin_amdgcn_exp2f((m - mn) * c);
+      m = mn;
+      mc = m * c;
+      ls *= alpha;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) o[dt] *= alpha;
+      lt = exps(s);
+    }
+    ls += lt;
+    // O^T += V^T . P^T over the 4 k-steps of 16 keys (key order of k-step (kt2, s2): 32 kt2 + 16 s2 + 8 (j >> 2) +
+    // 4 hh + (j & 3), matched by the two transposed V reads j2 = 0, 1)
+#pragma unroll
+    for (int kt2 = 0; kt2 < 2; ++kt2)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const bf16x8 pf = pack_acc8(s[kt2], s2);
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) {
+          const lds_char *a0, *a1;
+          if (dt < 2) {
+            const int ro = (32 * kt2 + 16 * s2) * 128;
+            a0 = Vs + voff[dt][0] + ro;
+            a1 = Vs + voff[dt][1] + ro;
+          } else {
+            a0 = Vs + vtail[s2][0] + 32 * kt2 * 64;
+            a1 = Vs + vtail[s2][1] + 32 * kt2 * 64;
+          }
+#if SVAE_FWD32_DIAG == 4
+          if (dt) continue;   // diagnostic build: one PV MFMA per k-step
+#endif
+          o[dt] = mfma32(cat44(lds_read_tr3(a0), lds_read_tr3(a1)), pf, o[dt]);
+        }
+      }
+  };
+
+  for (int it = 0; it < nvisit; ++it) {
+    const int kt = it == 0 ? 0 : kt1 + it - 1;
+    wait_vmcnt(min(NS - 2, nvisit - 1 - it) * 2 * PW);   // this wave's pieces of tile it have landed
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();                        // everyone's have; stage (it - 1) % NS is free
+    if (it + NS - 1 < nvisit) issue(it + NS - 1);
+    const int kbase = kt * 64;
+    if ((!p.causal || kbase <= qw + 31) && (kbase < SBLK || kbase + 63 >= lo_w)) {
+      const unsigned long long pm = pad ? pbits[kt] : 0ull;
+      const bool band_edge = kbase + 63 >= SBLK && kbase < lo_w;
+      const bool edge = pm != 0ull || kbase + 64 > p.Lk || (p.causal && kbase + 63 > qw) || band_edge;
+      const bool diag_only = pm == 0ull && !band_edge;
+      const int st = it % NS;
+      if (st == 0) tile(std::integral_constant<int, 0>(), kbase, edge, diag_only, pm);
+      else if (NS == 2 || st == 1) tile(std::integral_constant<int, 1>(), kbase, edge, diag_only, pm);
+      else tile(std::integral_constant<int, NS == 3 ? 2 : 1>(), kbase, edge, diag_only, pm);
+    }
+  }
+
+  // epilogue: O = O^T / l (lane: query qrow, dims 32 dt + 8 j + 4 hh + (0..3)), lse = m scale + ln l
+  const float lsum = sum_x32(ls);
+  const float inv = lsum > 0.f ? 1.0f / lsum : 0.f;
+  const bool qok = qrow < p.Lq;
+  const __amdgpu_buffer_rsrc_t ors =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(p.o + b * p.bo + (long long)h * p.hd), 0, 0x7FFFFFF0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t olrs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(p.olo ? p.olo + b * p.bolo + (long long)h * p.hd : p.o), 0, 0x7FFFFFF0, 0x00020000);
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) {
+    const f32x16 v = o[dt] * inv;
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      // lanes hh = 0 / 1 hold dims +0..3 / +4..7 (j = 2a) and +8..11 / +12..15 (j = 2a + 1): one swap per dword gives
+      // each lane 8 consecutive dims, 32 dt + 16 a + 8 hh
+      const unsigned x0 = pack_bf16x2(v[8 * a], v[8 * a + 1]), x1 = pack_bf16x2(v[8 * a + 2], v[8 * a + 3]);
+      const unsigned y0 = pack_bf16x2(v[8 * a + 4], v[8 * a + 5]), y1 = pack_bf16x2(v[8 * a + 6], v[8 * a + 7]);
+      const auto s0 = __builtin_amdgcn_permlane32_swap(x0, y0, false, false);
+      const auto s1 = __builtin_amdgcn_permlane32_swap(x1, y1, false, false);
+      const int d = 32 * dt + 16 * a + 8 * hh;
+      const int off = qok && d < p.hd ? (qrow * (int)p.so + d) * 2 : 0x7FFFFFF0;
+      __builtin_amdgcn_raw_buffer_store_b128((u32x4){s0[0], s1[0], s0[1], s1[1]}, ors, off, 0, 0);
+      if (p.olo) {   // the bf16 residual, same layout
+        float r[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) r[e] = v[8 * a + e] - (float)f2bf(v[8 * a + e]);
+        const auto t0 = __builtin_amdgcn_permlane32_swap(pack_bf16x2(r[0], r[1]), pack_bf16x2(r[4], r[5]), false, false);
+        const auto t1 = __builtin_amdgcn_permlane32_swap(pack_bf16x2(r[2], r[3]), pack_bf16x2(r[6], r[7]), false, false);
+        const int offl = qok && d < p.hd ? (qrow * (int)p.solo + d) * 2 : 0x7FFFFFF0;
+        __builtin_amdgcn_raw_buffer_store_b128((u32x4){t0[0], t1[0], t0[1], t1[1]}, olrs, offl, 0, 0);
+      }
+    }
+    if (p.o32) {
+      float* O32 = p.o32 + b * p.bo32 + (long long)h * p.hd;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int d = 32 * dt + 8 * j + 4 * hh;
+        if (qok && d < p.hd)
+          __builtin_nontemporal_store((f32x4){v[4 * j], v[4 * j + 1], v[4 * j + 2], v[4 * j + 3]},
+                                      (f32x4*)(O32 + (long long)qrow * p.so32 + d));
+      }
+    }
+  }
+  if (hh == 0 && qok) p.lse[((long long)b * p.H + h) * p.Lq + qrow] = m * p.scale + __logf(lsum);
+}
+
 // ===================================================================================== backward
 // delta[b][h][q] = sum_d dO . O   (LPR = hd / 8 lanes per (q, h) row: 8 for hd <= 64, 16 for hd <= 128, so no
 // lane idles)
@@ -546,7 +926,15 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(AP p) {
   const int h = gid % p.H, q = (gid / p.H) % p.Lq, b = gid / (p.H * p.Lq);
   const bf16* dO = p.dout + b * p.bdo + (long long)q * p.sdo + (long long)h * p.hd;
   float s = 0.f;
-  if (p.o32) {
+  if (p.olo) {
+    const bf16* O = p.o + b * p.bo + (long long)q * p.so + (long long)h * p.hd;
+    const bf16* OL = p.olo + b * p.bolo + (long long)q * p.solo + (long long)h * p.hd;
+    for (int d = li * 8; d < p.hd; d += 8 * LPR) {
+      const bf16x8 a = *(const bf16x8*)(O + d), l = *(const bf16x8*)(OL + d), c = *(const bf16x8*)(dO + d);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s += ((float)a[e] + (float)l[e]) * (float)c[e];
+    }
+  } else if (p.o32) {
     const float* O = p.o32 + b * p.bo32 + (long long)q * p.so32 + (long long)h * p.hd;
     for (int d = li * 8; d < p.hd; d += 8 * LPR) {
       const bf16x8 c = *(const bf16x8*)(dO + d);
@@ -1051,6 +1439,9 @@ __device__ __forceinline__ void attn_bwd_tile_wide(const AP& p, char* smem, int 
 // 64-dim Tile plus a 32-dim tail image), so hd 96 keeps K, dS^T and double-buffered Q / dO in 129 KiB.
 //
 constexpr int BWD8_KEYS = 256;
+#ifndef SVAE_BWD8_DIAG
+#define SVAE_BWD8_DIAG 0   // diagnostic build only (-DSVAE_BWD8_DIAG=1): no S / dP / dV / dK / dQ products (DMA, barriers,
+#endif                     // zero dS^T writes and every store kept): the kernel's memory and synchronisation skeleton
 
 #ifdef SVAE_STAMPS
 // diagnostic build only: per (hardware block < 1024, wave) cycle sums of the q-tile phases of attn_bwd8 --
@@ -1180,7 +1571,7 @@ __device__ __forceinline__ void attn_bwd8_tile(const AP& p, char* smem, int kb, 
 #ifdef SVAE_STAMPS
     if (live) st_acc[6] += 1;
 #endif
-    if (live) {
+    if (live && SVAE_BWD8_DIAG != 1) {
       const char* Kw = Ks + (w >> 1) * R::BYTES;     // this wave's 32 keys: rows 32 (w & 1) .. of image w / 2
       const bool edge = !keys_all_ok || qb + 64 > p.Lq || (p.causal && kw + 31 > qb) || qb + 63 >= band_end;
       const int qlim = min(p.Lq, band_end) - qb;
@@ -1307,7 +1698,7 @@ __device__ __forceinline__ void attn_bwd8_tile(const AP& p, char* smem, int kb, 
       }
 #pragma unroll
       for (int kk = 0; kk < BWD8_KEYS / 32; ++kk) {
-        if (32 * kk >= kvis) break;
+        if (32 * kk >= kvis || SVAE_BWD8_DIAG == 1) break;
         const int so = kk * 32 * TS::PITCH;
         const bf16x8 a = cat44(lds_read_tr3(sp0 + so), lds_read_tr3(sp4 + so));
 #pragma unroll
@@ -1510,6 +1901,8 @@ bool fill(const svae_attn_desc* d, AP& p) {
   p.o32 = d->o32; p.so32 = d->so32; p.bo32 = d->bo32;
   p.dq_part = d->dq_part; p.dq_bf = d->dq_bf; p.ldq_bf = d->ldq_bf;
   p.window = d->window;
+  p.olo = (bf16*)d->o_lo; p.solo = d->so_lo; p.bolo = d->bo_lo;
+  if (p.olo && ((p.solo | p.bolo) % 8)) return false;
   p.kblk = BWD_KEYS;
   p.dq_direct = 0;
   if (p.window < 0 || (p.window > 0 && !p.causal)) return false;
@@ -1525,7 +1918,18 @@ SVAE_EXPORT int svae_attn_fwd(const svae_attn_desc* d, svae_stream_t stream) {
   if (d->causal && d->Lq != d->Lk) return SVAE_EINVAL;
   dim3 grid((d->Lq + 127) / 128, d->H, d->B);
   hipStream_t s = (hipStream_t)stream;
-  if (d->hd <= 64) hipLaunchKernelGGL(attn_fwd_kernel<64>, grid, dim3(256), 0, s, p);
+  // the 32x32-MFMA kernel for hd <= 96 (SVAE_ATTN_FWD32=0: the 16x16 kernels, for A/B runs); its padding bit mask holds
+  // FWD32_MAXPAD keys and its DMA / store offsets are 32-bit byte offsets from a sequence's row 0
+  static const int fwd32_env = [] { const char* e = getenv("SVAE_ATTN_FWD32"); return e ? atoi(e) : 1; }();
+  static const int occ_env = [] { const char* e = getenv("SVAE_ATTN_FWD32_OCC"); return e ? atoi(e) : 3; }();
+  static const int ns_env = [] { const char* e = getenv("SVAE_ATTN_FWD32_NS"); return e ? atoi(e) : 2; }();
+  const bool fit32 = ((long long)d->Lk + 64) * std::max(d->sk, d->sv) * 2 < 0x7FFFFFF0LL &&
+                     ((long long)d->Lq + 128) * d->so * 2 < 0x7FFFFFF0LL && (!d->key_pad || d->Lk <= FWD32_MAXPAD);
+  if (fwd32_env && fit32 && d->hd <= 64) {
+    if (ns_env == 3) hipLaunchKernelGGL((attn_fwd32_kernel<64, 3, 3>), grid, dim3(256), 0, s, p);
+    else if (occ_env == 4) hipLaunchKernelGGL((attn_fwd32_kernel<64, 4, 2>), grid, dim3(256), 0, s, p);
+    else hipLaunchKernelGGL((attn_fwd32_kernel<64, 3, 2>), grid, dim3(256), 0, s, p);
+  } else if (d->hd <= 64) hipLaunchKernelGGL(attn_fwd_kernel<64>, grid, dim3(256), 0, s, p);
   else if (d->hd <= 96) hipLaunchKernelGGL((attn_fwd_kernel<128, 96>), grid, dim3(256), 0, s, p);
   else hipLaunchKernelGGL(attn_fwd_kernel<128>, grid, dim3(256), 0, s, p);
   SVAE_LAUNCH_CHECK();

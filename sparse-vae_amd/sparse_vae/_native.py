@@ -58,6 +58,7 @@ class AttnDesc(ctypes.Structure):
         ('dq_part', c_void_p), ('dq_bf', c_void_p), ('ldq_bf', c_int64),
         ('window', c_int32),
         ('delta_ready', c_int32),
+        ('o_lo', c_void_p), ('so_lo', c_int64), ('bo_lo', c_int64),
     ]
 
 

@@ -248,6 +248,9 @@ class VAEEngine:
         # tested, measured no faster: C2 12.725 / 12.696 vs 12.648 / 12.681 ms, C4 neutral,
         # profiles/r04j_delta_ab.log); default: the attention backward's own delta pass
         self.delta_fused = os.environ.get('SVAE_DELTA_FUSED', '0') != '0'
+        # the attention forward's copy of O for the backward's delta: the bf16 residual O - bf16(O) (2 B per element)
+        # unless SVAE_ATTN_O32=1 (the f32 copy, 4 B; A/B runs)
+        self.o32_mode = os.environ.get('SVAE_ATTN_O32', '0') != '0'
         # the last decoder layer's dropout + residual GEMM epilogue also writes the bf16 copy of its output (the vocab
         # head's input) instead of a separate [T, d] cast pass; SVAE_RESID_BF16=0 restores the cast (A/B runs)
         self.resid_bf16 = os.environ.get('SVAE_RESID_BF16', '1') != '0'
@@ -442,12 +445,11 @@ class VAEEngine:
             st['qkv'] = qkv
         rows_q = B * Lq
         O = ws.get(tag + '.O', (rows_q, d))
-        O32 = ws.get(tag + '.O32', (rows_q, d), f32)
+        Ox = self._o_extra(tag + '.O', rows_q, d, Lq)
         lse = ws.get(tag + '.lse', (B, heads, Lq), f32)
         K.attention(q, kt, vt, O, lse, B=B, H=heads, Lq=Lq, Lk=Sx, hd=hd, so=d, bo=Lq * d, sk=sk, sv=sk,
-                    bk=Sx * sk, bv=Sx * sk, key_pad=pad_k, causal=causal, window=window, o32=O32, so32=d, bo32=Lq * d,
-                    **qargs)
-        st.update(O=O, O32=O32, lse=lse, Lq=Lq, pad_k=pad_k)
+                    bk=Sx * sk, bv=Sx * sk, key_pad=pad_k, causal=causal, window=window, **Ox, **qargs)
+        st.update(O=O, Ox=Ox, lse=lse, Lq=Lq, pad_k=pad_k)
         resid = Lq == Sx                           # transformer_layer.py:49
         x1 = ws.get(tag + '.x1', (rows_q, d), f32)
         if fuse:
@@ -479,12 +481,11 @@ class VAEEngine:
             K.gemm(cx, P.w(c + 'k_linear.weight'), kvc, rows_c, 2 * d, d, epi=EPI_ROTARY_BF16,
                    bias=P.f(c + 'k_linear.bias'), rot=rot, rot_cols=d, rot_d=d, rot_seq=L)
             Oc = ws.get(tag + '.Oc', (rows_q, d))
-            Oc32 = ws.get(tag + '.Oc32', (rows_q, d), f32)
+            Ocx = self._o_extra(tag + '.Oc', rows_q, d, Lq)
             lsec = ws.get(tag + '.lsec', (B, heads, Lq), f32)
             K.attention(qc, kvc, kvc[:, d:], Oc, lsec, B=B, H=heads, Lq=Lq, Lk=L, hd=hd, sq=d, bq=Lq * d, sk=2 * d,
-                        sv=2 * d, bk=L * 2 * d, bv=L * 2 * d, so=d, bo=Lq * d, key_pad=pad, causal=False, o32=Oc32,
-                        so32=d, bo32=Lq * d)
-            st['Oc32'] = Oc32
+                        sv=2 * d, bk=L * 2 * d, bv=L * 2 * d, so=d, bo=Lq * d, key_pad=pad, causal=False, **Ocx)
+            st['Ocx'] = Ocx
             x2 = ws.get(tag + '.x2', (rows_q, d), f32)
             K.gemm(Oc, P.w(c + 'output_linear.weight'), x2, rows_q, d, d, epi=EPI_F32,
                    bias=P.f(c + 'output_linear.bias'), resid=x1, ldr=d)
@@ -517,6 +518,14 @@ class VAEEngine:
                    drop_p=drop_p, seed=seed, aux=out_bf, ldaux=d if out_bf is not None else 0)
         st.update(h2=h2, gprime=gprime, f=f, xc=xc, rows_q=rows_q)
         return out, st
+
+    def _o_extra(self, tag, rows_q, d, Lq):
+        """The forward's extra copy of O for the backward's delta = rowsum(dO . O): the bf16 residual O - bf16(O)
+        (o_lo, 2 B per element) by default; the f32 copy (o32) where the dO GEMM's delta epilogue reads it
+        (SVAE_DELTA_FUSED=1) or SVAE_ATTN_O32=1. Keyword arguments for kernels.attention."""
+        if self.delta_fused or self.o32_mode:
+            return dict(o32=self.ws.get(tag + '32', (rows_q, d), f32), so32=d, bo32=Lq * d)
+        return dict(o_lo=self.ws.get(tag + 'lo', (rows_q, d)), so_lo=d, bo_lo=Lq * d)
 
     def _dq_part(self, B, H, Lq, Lk, hd):
         """f32 workspace for the attention backward's per-key-block dQ partials (shared by all layers)."""
@@ -562,15 +571,15 @@ class VAEEngine:
             delta = ws.get('b.delta', (B, heads, Lq), f32)
             # the dO GEMM also writes delta = rowsum(dO . O) per head (its epilogue holds dO; no separate pass)
             K.gemm(gxc, P.wT(c + 'output_linear.weight', d, d), dOc, rows_q, d, d, epi=EPI_BF16, delta=delta if self.delta_fused else None,
-                   delta_o32=st['Oc32'], ld_o32=d, delta_hd=hd, delta_seq=Lq)
+                   delta_o32=st['Ocx'].get('o32'), ld_o32=d, delta_hd=hd, delta_seq=Lq)
             dqc = ws.get('b.dqc', (rows_q, d))
             dkvc = ws.get('b.dkvc', (rows_c, 2 * d))
             K.attention(st['qc'], st['kvc'], st['kvc'][:, d:], st['Oc'], st['lsec'], B=B, H=heads, Lq=Lq, Lk=L,
                         hd=hd, sq=d, bq=Lq * d, sk=2 * d, sv=2 * d, bk=L * 2 * d, bv=L * 2 * d, so=d, bo=Lq * d,
                         key_pad=st['pad_ctx'], causal=False, backward=True, delta_ready=self.delta_fused,
                         dout=dOc, sdo=d, bdo=Lq * d, delta=delta, dq_bf=dqc, ldq_bf=d, dk=dkvc, dv=dkvc[:, d:],
-                        sdk=2 * d, sdv=2 * d, bdk=L * 2 * d, bdv=L * 2 * d, rot=rot, rot_d=d, o32=st['Oc32'],
-                        so32=d, bo32=Lq * d, dq_part=self._dq_part(B, heads, Lq, L, hd))
+                        sdk=2 * d, sdv=2 * d, bdk=L * 2 * d, bdv=L * 2 * d, rot=rot, rot_d=d, **st['Ocx'],
+                        dq_part=self._dq_part(B, heads, Lq, L, hd))
             self._dw_pair((gxc, st['Oc'], c + 'output_linear.weight', rows_q, d, d, None, None,
                            c + 'output_linear.bias'),
                           (dqc, st['hq'], c + 'q_linear.weight', rows_q, d, d, None, None, c + 'q_linear.bias'))
@@ -588,7 +597,7 @@ class VAEEngine:
         dO = ws.get('b.dO', (rows_q, d))
         delta = ws.get('b.delta', (B, heads, Lq), f32)
         K.gemm(gx1, P.wT(a + 'output_linear.weight', d, d), dO, rows_q, d, d, epi=EPI_BF16, delta=delta if self.delta_fused else None,
-               delta_o32=st['O32'], ld_o32=d, delta_hd=hd, delta_seq=Lq)
+               delta_o32=st['Ox'].get('o32'), ld_o32=d, delta_hd=hd, delta_seq=Lq)
         if st['learned']:
             kv = st['kv']
             dq32 = ws.get('b.dq32', (B * Lq, d), f32)
@@ -597,7 +606,7 @@ class VAEEngine:
                         Lq=Lq, Lk=Sx, hd=hd, sq=d, bq=0, sk=2 * d, sv=2 * d, bk=Sx * 2 * d, bv=Sx * 2 * d, so=d,
                         bo=Lq * d, key_pad=st['pad_k'], causal=False, backward=True, dout=dO, sdo=d, bdo=Lq * d,
                         delta=delta, delta_ready=self.delta_fused, dq=dq32, bdq=Lq * d, dk=dkv, dv=dkv[:, d:], sdk=2 * d, sdv=2 * d,
-                        bdk=Sx * 2 * d, bdv=Sx * 2 * d, rot=rot, rot_d=d, o32=st['O32'], so32=d, bo32=Lq * d,
+                        bdk=Sx * 2 * d, bdv=Sx * 2 * d, rot=rot, rot_d=d, **st['Ox'],
                         dq_part=self._dq_part(B, heads, Lq, Sx, hd))
             K.colsum(dq32, B, Lq * d, Lq * d, P.g(a + 'learned_queries').view(-1))
             self._dw_pair(wo_dw, (dkv, st['h'], a + 'k_linear.weight', rows_x, 2 * d, d, None, None,
@@ -612,8 +621,8 @@ class VAEEngine:
                         key_pad=st['pad_k'], causal=st['causal'], window=st['window'], backward=True, dout=dO,
                         sdo=d, bdo=Lq * d,
                         delta=delta, delta_ready=self.delta_fused, dq_bf=dqkv, ldq_bf=3 * d, dk=dqkv[:, d:], dv=dqkv[:, 2 * d:], sdk=3 * d,
-                        sdv=3 * d, bdk=Sx * 3 * d, bdv=Sx * 3 * d, rot=rot, rot_d=d, o32=st['O32'], so32=d,
-                        bo32=Lq * d, dq_part=self._dq_part(B, heads, Lq, Sx, hd))
+                        sdv=3 * d, bdk=Sx * 3 * d, bdv=Sx * 3 * d, rot=rot, rot_d=d, **st['Ox'],
+                        dq_part=self._dq_part(B, heads, Lq, Sx, hd))
             self._dw_pair(wo_dw, (dqkv, st['h'], a + 'q_linear.weight', rows_x, 3 * d, d, None, None,
                                   a + 'q_linear.bias'))
             dh = ws.get('b.dh', (rows_x, d))
@@ -883,11 +892,15 @@ class VAEEngine:
         dec = []
         h_in = None
         # (zf_batch: every layer's z projection in one launch, spliced in by the layer's first LayerNorm)
-        zf_batch = self.zf_batch and not fuse and d % 8 == 0
+        # (the launch takes <= ZPROJ_MAX layers and a latent of <= 1024: deeper models run it in chunks, wider latents
+        # the per-layer GEMM path)
+        zf_batch = self.zf_batch and not fuse and d % 8 == 0 and Z <= 1024
         if zf_batch:
             zall = ws.get('zproj_all', (hp.num_layers, B, d), f32)
-            K.zproj_fwd_multi([(P.w(f'z_projections.{i}.weight'), P.f(f'z_projections.{i}.bias'), zall[i])
-                               for i in range(hp.num_layers)], zb, B, d, Z)
+            segs = [(P.w(f'z_projections.{i}.weight'), P.f(f'z_projections.{i}.bias'), zall[i])
+                    for i in range(hp.num_layers)]
+            for c0 in range(0, len(segs), ZPROJ_MAX):
+                K.zproj_fwd_multi(segs[c0:c0 + ZPROJ_MAX], zb, B, d, Z)
         else:
             K.gemm(zb, P.w('z_projections.0.weight'), xs, B, d, Z, ldc=L * d, epi=EPI_F32,
                    bias=P.f('z_projections.0.bias'))

@@ -267,8 +267,10 @@ _attn_desc = N.AttnDesc()
 def attention(q, k, v, o, lse, *, B, H, Lq, Lk, hd, sq, sk, sv, so, bq, bk, bv, bo, key_pad=None, causal=False,
               window=0, scale=None, backward=False, dout=None, sdo=0, bdo=0, delta=None, dq=None, bdq=0, dk=None, dv=None,
               sdk=0, sdv=0, bdk=0, bdv=0, rot=None, rot_d=0, o32=None, so32=0, bo32=0, dq_part=None, dq_bf=None,
-              ldq_bf=0, delta_ready=False):
-    """Forward (o, lse[, o32]) or backward (dk, dv and dq: f32 `dq` or bf16 `dq_bf` with inverse rotary).
+              ldq_bf=0, delta_ready=False, o_lo=None, so_lo=0, bo_lo=0):
+    """Forward (o, lse[, o32 | o_lo]) or backward (dk, dv and dq: f32 `dq` or bf16 `dq_bf` with inverse rotary).
+    o_lo: bf16 residual O - bf16(O) (written by the forward, read by the backward's delta pass; the 2-byte alternative
+    to the f32 copy o32).
     dq_part: f32 workspace of attn_dq_part_elems(...) floats (allocated here when not given).
     window > 0 (causal): SparseAttention's sliding window of `window` 32-key blocks + the [CLS] block."""
     d = _attn_desc
@@ -281,6 +283,7 @@ def attention(q, k, v, o, lse, *, B, H, Lq, Lk, hd, sq, sk, sv, so, bq, bk, bv, 
     d.delta_ready = int(bool(delta_ready))
     d.scale = hd ** -0.5 if scale is None else scale
     d.o32, d.so32, d.bo32 = ptr(o32), so32, bo32
+    d.o_lo, d.so_lo, d.bo_lo = ptr(o_lo), so_lo, bo_lo
     if backward:
         d.dout, d.sdo, d.bdo = dout.data_ptr(), sdo, bdo
         d.delta, d.bdq = delta.data_ptr(), bdq

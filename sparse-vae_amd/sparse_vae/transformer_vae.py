@@ -104,6 +104,7 @@ class TransformerVAE(ContinuousVAEHooks, LanguageModel):
         self._dp = None
         self._log_consts = None
         self.logged_reduced = {}
+        self.comm_probe = None     # a list: (start, end) HIP events of each step's exposed all-reduce tail (bench.py)
         self._step_seed = 7295
         # DDP's flag (Lightning sets it through no_sync under accumulate_grad_batches): False marks a gradient-
         # accumulation micro-step that no optimiser step follows -- its backward runs no all-reduce (the final
@@ -202,9 +203,19 @@ class TransformerVAE(ContinuousVAEHooks, LanguageModel):
         dp = self._dp
         if dp is None:
             return
+        probe = self.comm_probe
+        if probe is not None:
+            # exposed communication: from the end of the backward on the compute stream (every bucket but the last
+            # already in flight) to the point where that stream may proceed past the last bucket's all-reduce
+            e0 = torch.cuda.Event(enable_timing=True)
+            e0.record()
         self._dp_ready(self._flat.n_live, final=True)
         for w in dp['works']:
             w.wait()
+        if probe is not None:
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record()
+            probe.append((e0, e1))
         dp['works'] = []
         dp['start'] = 0
 

@@ -26,4 +26,6 @@ def test_two_rank_bench_rehearsal():
     assert res['n_gpus'] == 2 and res['config']['parallelism'] == 'dp2' and res['config']['global_batch'] == 128
     assert res['value'] > 0 and 'rehearsal' in res
     assert 0 < res['scaling_efficiency']['value'] < 10
+    # the all-reduce tail the backward did not hide (HIP events on the compute stream, max over ranks)
+    assert res['exposed_comm_ms']['value'] >= 0 and 0 <= res['exposed_comm_ms']['fraction_of_step'] < 10
     assert 'cpu_baseline' not in res and 'parity' not in res

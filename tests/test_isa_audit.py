@@ -26,3 +26,8 @@ def test_isa_has_no_dma_hazards_and_no_spills_in_the_attention_loops(tmp_path):
     assert len(bwd8) == 2
     for k, v in bwd8.items():
         assert v['scratch_in_mfma_loops'] == 0, (k, v)
+    # the 32x32-MFMA forward at the product occupancy (3 workgroups per CU): no spill code in its key loop
+    fwd32 = {k: v for k, v in rep.items() if 'attn_fwd32_kernelILi64ELi3E' in k}
+    assert len(fwd32) == 2
+    for k, v in fwd32.items():
+        assert v['scratch'] == 0, (k, v)

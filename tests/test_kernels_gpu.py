@@ -648,6 +648,72 @@ def test_attention_fwd_bwd(B, H, Lq, Lk, hd, causal, padded, learned):
     assert _rel(dv, unheads(vr.grad)) < 2e-2
 
 
+@pytest.mark.parametrize('hd,L', [(64, 512), (96, 1024), (32, 130)])
+def test_attention_o_lo_matches_o32(hd, L):
+    """The forward's bf16 residual o_lo = O - bf16(O) carries the f32 O to ~16 bits: the delta pass from (O, o_lo)
+    gives the backward of the f32 copy o32 to ~1e-5."""
+    torch.manual_seed(hd * 3 + L)
+    B, H = 2, 3
+    d = H * hd
+    qkv = torch.randn(B * L, 3 * d, device=dev).bfloat16()
+    common = dict(B=B, H=H, Lq=L, Lk=L, hd=hd, sq=3 * d, bq=L * 3 * d, sk=3 * d, sv=3 * d, bk=L * 3 * d,
+                  bv=L * 3 * d, so=d, bo=L * d, causal=True)
+    o, o2 = (torch.empty(B * L, d, device=dev, dtype=torch.bfloat16) for _ in range(2))
+    lse, lse2 = torch.empty(B, H, L, device=dev), torch.empty(B, H, L, device=dev)
+    o32 = torch.empty(B * L, d, device=dev)
+    olo = torch.empty(B * L, d, device=dev, dtype=torch.bfloat16)
+    K.attention(qkv, qkv[:, d:], qkv[:, 2 * d:], o, lse, o32=o32, so32=d, bo32=L * d, **common)
+    K.attention(qkv, qkv[:, d:], qkv[:, 2 * d:], o2, lse2, o_lo=olo, so_lo=d, bo_lo=L * d, **common)
+    assert torch.equal(o, o2) and torch.equal(lse, lse2)
+    assert torch.equal(o.float(), o32.bfloat16().float())                 # O is bf16(o32)
+    assert (o.float() + olo.float() - o32).abs().max() <= o32.abs().max() * 2.0 ** -16
+    do = torch.randn(B * L, d, device=dev).bfloat16()
+    outs = []
+    for extra in (dict(o32=o32, so32=d, bo32=L * d), dict(o_lo=olo, so_lo=d, bo_lo=L * d)):
+        delta = torch.empty(B, H, L, device=dev)
+        g = torch.empty(B * L, 3 * d, device=dev, dtype=torch.bfloat16)
+        K.attention(qkv, qkv[:, d:], qkv[:, 2 * d:], o, lse, backward=True, dout=do, sdo=d, bdo=L * d, delta=delta,
+                    dq_bf=g, ldq_bf=3 * d, dk=g[:, d:], dv=g[:, 2 * d:], sdk=3 * d, sdv=3 * d, bdk=L * 3 * d,
+                    bdv=L * 3 * d, **extra, **common)
+        outs.append((delta.clone(), g.float()))
+    (d32, g32), (dlo, glo) = outs
+    assert _rel(dlo, d32) < 1e-5
+    assert _rel(glo, g32) < 1e-3      # bf16 outputs: a few last-bit flips from delta's last bits
+
+
+@pytest.mark.parametrize('hd,L,causal,order', [(64, 512, True, 'up'), (64, 512, False, 'up'), (96, 1024, True, 'up'),
+                                                 (64, 520, False, 'perm'), (96, 300, True, 'perm')])
+def test_attention_fwd_running_max_growth(hd, L, causal, order):
+    """Scores that grow by far more than 2^16 (log2 units) from one key tile to the next: the forward's deferred running
+    max must take its rescale path (recompute S, rescale O and the row sum) and still match fp32 softmax; 'perm' puts
+    the large keys at random positions (growth at any tile, including inside the first). O and lse are checked (the
+    backward recomputes P from lse)."""
+    torch.manual_seed(hd + L)
+    B, H = 2, 2
+    d = H * hd
+    q = (torch.rand(B, L, d, device=dev) * 0.5 + 0.75).bfloat16()           # positive: s grows with the key's norm
+    mag = torch.linspace(0.0, 40.0, L, device=dev)
+    if order == 'perm':
+        mag = mag[torch.randperm(L, device=dev)]
+    k = (torch.rand(B, L, d, device=dev) * 0.2 + mag[None, :, None]).bfloat16()
+    v = torch.randn(B, L, d, device=dev).bfloat16()
+    o = torch.empty(B, L, d, device=dev, dtype=torch.bfloat16)
+    lse = torch.empty(B, H, L, device=dev)
+    scale = hd ** -0.5
+    K.attention(q, k, v, o, lse, B=B, H=H, Lq=L, Lk=L, hd=hd, sq=d, bq=L * d, sk=d, sv=d, bk=L * d, bv=L * d, so=d,
+                bo=L * d, causal=causal)
+
+    def heads(t):
+        return t.float().view(B, L, H, hd).transpose(1, 2)
+
+    s = heads(q) @ heads(k).transpose(-1, -2) * scale
+    if causal:
+        s = s.masked_fill(torch.ones(L, L, device=dev, dtype=torch.bool).triu(1), -float('inf'))
+    ref = (s.softmax(-1) @ heads(v)).transpose(1, 2).reshape(B, L, d)
+    assert _rel(o, ref) < 1e-2
+    torch.testing.assert_close(lse, torch.logsumexp(s, -1), rtol=1e-5, atol=1e-3)
+
+
 @pytest.mark.parametrize('B,H,L,hd,window,padded', [
     (2, 4, 512, 64, 4, True),       # the reference default (attn_window_size 4), C2 head dim
     (1, 2, 1024, 64, 4, False),     # band far from the [CLS] block
