@@ -602,56 +602,85 @@ __global__ __launch_bounds__(256, 3) void gemm_glds_kernel(GP p) {
 // B fragments across the turn), 16 MFMAs each. Layouts: A [M][K] (K-contiguous, 128-B rows, kc_off
 // swizzle); B [N][K] likewise, or B [K][N] (b_t) as two [64][128] MN-contiguous halves read with
 // ds_read_b64_tr_b16 (mn_off swizzle). All swizzles are applied on the DMA SOURCE address (the LDS image is
-// lane-linear per 1-KiB piece) and undone by the fragment reads. Epilogue: four 64-row passes staged as
-// f32 through the (then idle) LDS and handed to the shared vectorised epilogue, one 128-column half per
-// 256 threads.
+// lane-linear per 1-KiB piece) and undone by the fragment reads. Epilogues run straight from the
+// accumulator registers (g3_reg_epilogue / g3_reg_epilogue_ld below); float-atomic split-K without a slab
+// workspace is left to the 128-tile kernels.
 constexpr int G3_T = 256 * 64 * 2;   // 32 KiB per operand K-tile
 constexpr int G3_STAGE = 2 * G3_T;
 // internal instantiation: SVAE_EPI_BF16 that also writes the attention backward's delta (svae_gemm_desc.delta)
 constexpr int G3_EPI_BF16_DELTA = 65;
+// internal instantiation: SVAE_EPI_F32_ACC whose fused bias-gradient row sums are weighted by k_weight (the
+// vocabulary head's dW, where the per-token weight r folds the softmax normalisation into the row sums)
+constexpr int G3_EPI_ACC_KW = 64;
+// internal: the split-K slab form of the same (each split stores its partial tile, slab_reduce adds them into C;
+// the k-weighted row sums of each split's K range go to a_rowsum by atomics as in every split-K row sum)
+constexpr int G3_EPI_F32_KW = 66;
+// internal: the split-K slab store (plain f32 partial tile: no residual, no bf16 copy) -- SVAE_EPI_F32 without the
+// operand loads and branches of its optional inputs, whose registers spilled in the heaviest instantiations
+constexpr int G3_EPI_SLAB = 67;
 
-// Per-lane DMA source offsets of one operand's K-tile, hoisted out of the K loop: only the tile base (a
-// scalar) moves with k0. off[i] already carries the M/N-bound (out-of-range -> OOB offset); the K tail
-// (last tile when K % 64 != 0) is checked per tile against kq[i] (the piece's k offset inside the tile).
+// Per-lane DMA source offsets of one operand's K-tile relative to the tile base (a scalar that moves with m0 / n0 and
+// k0): they do not depend on the tile, so they are computed once per kernel and are the only per-lane DMA state kept
+// across the tile loop (8 VGPRs). A tile that is interior (its 256 rows / columns inside M / N) and a full K-tile
+// issue them as they are; an edge tile or the K tail recomputes its offsets from a fresh lane id with the bound
+// checks (out-of-range -> OOB offset, the piece reads zeros). Keeping per-tile checked offsets (and the compiler's
+// unchecked copies) live across the tile loop spilled them in the register-heaviest instantiations, and a spill
+// reload's vmcnt(0) inside the K loop drains the DMA ring.
 struct G3Src {
   int off[4];
-  int kq[4];
 };
 
-// K-contiguous operand [rows][K] (128-B rows of the tile): piece = 8 rows x 128 B
-__device__ __forceinline__ G3Src g3_src_k(long long ld, int row0, int nrows, int wave, int lane) {
-  G3Src s;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int piece = wave * 4 + i;
-    const int r = piece * 8 + (lane >> 3), c = (lane & 7) ^ ((r >> 1) & 7);
-    s.off[i] = (row0 + r < nrows) ? (r * (int)ld + c * 8) * 2 : 0x7FFFFFF0;
-    s.kq[i] = c * 8;
-  }
-  return s;
+// K-contiguous operand [rows][K] (128-B rows of the tile): piece = 8 rows x 128 B; lane -> (row r, 16-B chunk c)
+__device__ __forceinline__ void g3_piece_k(int piece, int lane, int& r, int& c) {
+  r = piece * 8 + (lane >> 3);
+  c = (lane & 7) ^ ((r >> 1) & 7);
 }
-// MN-contiguous operand [K][cols] as two [64][128] halves: piece = 4 k-rows x 256 B
-__device__ __forceinline__ G3Src g3_src_mn(long long ld, int col0, int ncols, int wave, int lane) {
-  G3Src s;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int piece = wave * 4 + i, half = piece >> 4;
-    const int kr = (piece & 15) * 4 + (lane >> 4);
-    const int sk = (kr & 3) | (((kr >> 3) & 1) << 2);
-    const int col = half * 128 + (((lane & 15) ^ (sk << 1)) * 8);
-    s.off[i] = (col0 + col < ncols) ? (kr * (int)ld + col) * 2 : 0x7FFFFFF0;
-    s.kq[i] = kr;
-  }
-  return s;
+// MN-contiguous operand [K][cols] as two [64][128] halves: piece = 4 k-rows x 256 B; lane -> (k-row kr, column col)
+__device__ __forceinline__ void g3_piece_mn(int piece, int lane, int& kr, int& col) {
+  const int half = piece >> 4;
+  kr = (piece & 15) * 4 + (lane >> 4);
+  const int sk = (kr & 3) | (((kr >> 3) & 1) << 2);
+  col = half * 128 + (((lane & 15) ^ (sk << 1)) * 8);
 }
 
 template <bool MN>
-__device__ __forceinline__ void g3_issue_one(const bf16* tile_base, const G3Src& src, int krem, char* dst, int wave) {
-  const u32x4 rs = buffer_rsrc(tile_base, 0x7FFFFFF0u);
+__device__ __forceinline__ G3Src g3_src(long long ld, int wave, int lane) {
+  G3Src s;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int off = (krem >= 64 || src.kq[i] < krem) ? src.off[i] : 0x7FFFFFF0;
-    dma16_lds(rs, dst + (wave * 4 + i) * 1024, off);
+    int x, y;
+    if constexpr (MN) { g3_piece_mn(wave * 4 + i, lane, x, y); s.off[i] = (x * (int)ld + y) * 2; }
+    else { g3_piece_k(wave * 4 + i, lane, x, y); s.off[i] = (x * (int)ld + y * 8) * 2; }
+  }
+  return s;
+}
+
+// One operand's K-tile: full = interior tile and a whole K-tile (wave-uniform); otherwise the checked offsets
+// (row / column bound nb - base0, K bound krem) from a fresh lane id
+template <bool MN>
+__device__ __forceinline__ void g3_issue_one(const bf16* tile_base, const G3Src& src, bool full, long long ld, int nrem,
+                                             int krem, char* dst, int wave) {
+  const u32x4 rs = buffer_rsrc(tile_base, 0x7FFFFFF0u);
+  if (full) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dma16_lds(rs, dst + (wave * 4 + i) * 1024, src.off[i]);
+  } else {
+    const int lane = lane_id_fresh();
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      int x, y, off;
+      bool ok;
+      if constexpr (MN) {   // x = k-row, y = column
+        g3_piece_mn(wave * 4 + i, lane, x, y);
+        ok = y < nrem && x < krem;
+        off = (x * (int)ld + y) * 2;
+      } else {              // x = row, y = 16-B chunk
+        g3_piece_k(wave * 4 + i, lane, x, y);
+        ok = x < nrem && y * 8 < krem;
+        off = (x * (int)ld + y * 8) * 2;
+      }
+      dma16_lds(rs, dst + (wave * 4 + i) * 1024, ok ? off : 0x7FFFFFF0);
+    }
   }
 }
 
@@ -659,10 +688,11 @@ template <bool AT, bool BT>
 __device__ __forceinline__ void g3_issue(const GP& p, const bf16* A, const bf16* B, const G3Src& sa, const G3Src& sb,
                                          int m0, int n0, int k0, int kend, char* stage, int wave) {
   const int krem = kend - k0;
-  if constexpr (AT) g3_issue_one<true>(A + (long long)k0 * p.lda + m0, sa, krem, stage, wave);
-  else g3_issue_one<false>(A + (long long)m0 * p.lda + k0, sa, krem, stage, wave);
-  if constexpr (BT) g3_issue_one<true>(B + (long long)k0 * p.ldb + n0, sb, krem, stage + G3_T, wave);
-  else g3_issue_one<false>(B + (long long)n0 * p.ldb + k0, sb, krem, stage + G3_T, wave);
+  const bool fa = krem >= 64 && m0 + 256 <= p.M, fb = krem >= 64 && n0 + 256 <= p.N;
+  if constexpr (AT) g3_issue_one<true>(A + (long long)k0 * p.lda + m0, sa, fa, p.lda, p.M - m0, krem, stage, wave);
+  else g3_issue_one<false>(A + (long long)m0 * p.lda + k0, sa, fa, p.lda, p.M - m0, krem, stage, wave);
+  if constexpr (BT) g3_issue_one<true>(B + (long long)k0 * p.ldb + n0, sb, fb, p.ldb, p.N - n0, krem, stage + G3_T, wave);
+  else g3_issue_one<false>(B + (long long)n0 * p.ldb + k0, sb, fb, p.ldb, p.N - n0, krem, stage + G3_T, wave);
 }
 
 // B fragment (16 n x 32 k) of n-tile at column cb (0..255) of the B tile, k-step ks
@@ -681,41 +711,6 @@ __device__ __forceinline__ bf16x8 g3_afrag(const char* la, int rb, int ks, int l
 
 // gemm256 accumulators are C^T fragments (MFMA operands swapped): acc[i][j] lane l holds row
 // wr*128 + 16i + (l & 15), columns wc*64 + 16j + 4(l >> 4) + (0..3) -- one row, 4 consecutive columns.
-//
-// Staged epilogue (the f32-output, rotary and GELU' epilogues, which read other tensors): 4 passes of 64 rows;
-// staging = two [64][128] f32 halves (the ring stage the last K-tile was read from), one 16-B write per fragment.
-// The bias (side area) goes in with the staging write and no global load precedes the first store, so the passes'
-// stores stay in flight (raw barriers, no vmcnt drain) into the next tile's first K-step.
-template <int EPI>
-__device__ __forceinline__ void g3_epilogue(const GP& p, char* smem, const f32x4 (&acc)[8][4], const float* sbias,
-                                            const int* slab_, int m0, int n0, int bn, int batch, int split, int wr,
-                                            int wc, int tid, int lane) {
-  float* cs = (float*)smem;
-  const long long cofs = (long long)batch * p.sC + split * p.slab;
-  const int half = tid >> 8;
-#pragma unroll
-  for (int pass = 0; pass < 4; ++pass) {
-    if (wr == (pass >> 1)) {
-#pragma unroll
-      for (int ii = 0; ii < 4; ++ii) {
-        const int i = (pass & 1) * 4 + ii;
-        const int row = ii * 16 + (lane & 15);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int col = wc * 64 + j * 16 + 4 * (lane >> 4);
-          const f32x4 b4 = *(const f32x4*)(sbias + col);
-          *(f32x4*)(cs + (col >> 7) * 8192 + row * 128 + cs_swz8(row, col & 127)) = p.alpha * acc[i][j] + b4;
-        }
-      }
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    epilogue_half<EPI, true, true>(p, cs + half * 8192, m0, n0 + 128 * half, bn * 2 + half, pass * 64, cofs, tid & 255,
-                             EPI == SVAE_EPI_CE_STATS ? slab_[pass * 64 + ((tid & 255) >> 2)] : -1);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-  }
-}
 
 // Register epilogue (bf16 out, GELU, rotary, CE statistics): straight from the C^T fragments, no staging. Each fragment
 // is one 8-B bf16x4 store per lane (16 rows x 32 B per instruction; a row's 128-B line completes over the 4 j).
@@ -1084,10 +1079,10 @@ __device__ __forceinline__ void g3_reg_epilogue_ld(const GP& p, const f32x4 (&ac
     }
     return;
   } else {
-    // f32 out: F32 (+resid when given), F32_ACC (+C), DROPOUT_RESID (dropout then +resid)
+    // f32 out: F32 (+resid when given), F32_ACC (+C), DROPOUT_RESID (dropout then +resid), SLAB (nothing added)
     const float* src = EPI == SVAE_EPI_F32_ACC ? (const float*)p.C + cofs : p.resid;
     const long long lds_ = EPI == SVAE_EPI_F32_ACC ? p.ldc : p.ldr;
-    const bool ld = src != nullptr;
+    const bool ld = EPI != G3_EPI_SLAB && src != nullptr;
     auto ld_row = [&](int i, f32x4 (&r)[4]) {
       const int m = m0 + wr * 128 + i * 16 + li;
 #pragma unroll
@@ -1097,10 +1092,10 @@ __device__ __forceinline__ void g3_reg_epilogue_ld(const GP& p, const f32x4 (&ac
       }
     };
     f32x4 cur[4], nxt[4];
-    ld_row(0, cur);
+    if constexpr (EPI != G3_EPI_SLAB) ld_row(0, cur);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      if (i + 1 < 8) ld_row(i + 1, nxt);
+      if (EPI != G3_EPI_SLAB && i + 1 < 8) ld_row(i + 1, nxt);
       const int m = m0 + wr * 128 + i * 16 + li;
       f32x4 x[4];
 #pragma unroll
@@ -1110,7 +1105,7 @@ __device__ __forceinline__ void g3_reg_epilogue_ld(const GP& p, const f32x4 (&ac
         if constexpr (EPI == SVAE_EPI_DROPOUT_RESID) {
           if (p.drop_p > 0.f) dropout4(p, x[j], m, n);
         }
-        x[j] += cur[j];
+        if constexpr (EPI != G3_EPI_SLAB) x[j] += cur[j];
       }
       if constexpr (EPI == SVAE_EPI_F32_ACC) {   // (the head dW: the merge's registers cost spills, 1185 -> 1211 us)
 #pragma unroll
@@ -1136,7 +1131,7 @@ __device__ __forceinline__ void g3_reg_epilogue_ld(const GP& p, const f32x4 (&ac
           }
         }
       }
-      if (i + 1 < 8) {
+      if (EPI != G3_EPI_SLAB && i + 1 < 8) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) cur[j] = nxt[j];
       }
@@ -1182,14 +1177,11 @@ __device__ unsigned long long svae_rt[1024][2];   // per block: entry, exit (s_m
 #else
 #define G3_STAMP(k) ((void)0)
 #endif
-// internal instantiation: SVAE_EPI_F32_ACC whose fused bias-gradient row sums are weighted by k_weight (the
-// vocabulary head's dW, where the per-token weight r folds the softmax normalisation into the row sums)
-constexpr int G3_EPI_ACC_KW = 64;
-// internal: the split-K slab form of the same (each split stores its partial tile, slab_reduce adds them into C;
-// the k-weighted row sums of each split's K range go to a_rowsum by atomics as in every split-K row sum)
-constexpr int G3_EPI_F32_KW = 66;
 #ifndef SVAE_KW_FORM
 #define SVAE_KW_FORM 0
+#endif
+#ifndef SVAE_KW_PRE
+#define SVAE_KW_PRE 1   // form 0's weights loaded at the K-tile top by counted asm loads (0: at the use, no DMA stagger)
 #endif
 
 // Vector-memory operations every wave issues unconditionally in the epilogue of an interior 256 x 256 tile (stores
@@ -1215,9 +1207,8 @@ constexpr int g3_epi_vmem_ops() {
     case SVAE_EPI_DROPOUT_RESID:
     case G3_EPI_ACC_KW:
     case G3_EPI_F32_KW:
+    case G3_EPI_SLAB:
       return 8 * 4;                   // 8 fragment rows x 4 16-B f32 stores
-    case SVAE_EPI_F32_ATOMIC:
-      return 4 * 32;                  // staged: 4 passes x 32 atomics per lane
     default:
       return 0;
   }
@@ -1273,14 +1264,7 @@ __device__ __forceinline__ void gemm256_run(const GP& p, int blk, int nwg) {
       dma16_lds(kwr, skw + (stage * 8 + wave) * KW_SLOT, l < 16 && kk < kend ? kk * 4 : 0x7FFFFFF0);
     }
   };
-  G3Src sa, sb;
-  auto srcs = [&](const G3Tile& X, G3Src& xa, G3Src& xb) {
-    if constexpr (AT) xa = g3_src_mn(p.lda, X.m0, p.M, wave, lane);
-    else xa = g3_src_k(p.lda, X.m0, p.M, wave, lane);
-    if constexpr (BT) xb = g3_src_mn(p.ldb, X.n0, p.N, wave, lane);
-    else xb = g3_src_k(p.ldb, X.n0, p.N, wave, lane);
-  };
-  srcs(T, sa, sb);
+  const G3Src sa = g3_src<AT>(p.lda, wave, lane), sb = g3_src<BT>(p.ldb, wave, lane);
   int g = 0;   // K-tiles consumed so far by this block: the stage of K-tile g is g & 1
   if (T.nk > 0) {
     g3_issue<AT, BT>(p, T.A, T.B, sa, sb, T.m0, T.n0, T.kbeg, T.kend, ring, wave);
@@ -1301,6 +1285,8 @@ __device__ __forceinline__ void gemm256_run(const GP& p, int blk, int nwg) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
+    // the next tile's first K-tile is prefetched by the last K-tile of this one (8 DMA pieces per wave)
+    const bool next_dma = has_next && g3_tile(p, t3n).nk > 0;
     for (int kt = 0; kt < T.nk; ++kt, ++g) {
       // this wave's pieces of K-tile g landed (after an interior epilogue, up to G3_EPI_STORES younger stores may
       // still be in flight: vmcnt retires in issue order)
@@ -1315,18 +1301,33 @@ __device__ __forceinline__ void gemm256_run(const GP& p, int blk, int nwg) {
       // times -- wr 0 here, wr 1 after its first MFMA quadrant -- so one wave's DMA issue runs beside the other's MFMAs
       // (the k-weighted forms: form 0 loads the weights from global memory at the use, whose wait would also wait for
       // the late pieces, so no stagger; the LDS-slot diagnostic forms stagger)
-      const bool late = (!IS_KW || KW_FORM > 0) && p.dma_stagger && wr == 1 && kt + 1 < T.nk;   // (wave-uniform)
+      // ACC_KW form 0: the K-tile's 64 weights are loaded here, one dword per lane, BEFORE this K-tile's 8 DMA pieces
+      // (issued next, or after the first quadrant by a late wave; the block's very last K-tile issues 8 out-of-range
+      // pieces instead, so the count holds), by an asm buffer load the compiler does not track; the use waits vmcnt(8)
+      // -- those pieces may stay in flight, so the DMA stagger applies to the k-weighted GEMM too -- and takes each
+      // lane's 8 weights of a k-step by ds_bpermute (1 VGPR live across the quadrants instead of 8 or 16; a
+      // compiler-visible load made hipcc wait vmcnt(0), draining the DMA, and the wider live forms spilled)
+      const int ks0 = p.tn2 >= 2 ? T.bn : 0, ks1 = p.tn2 >= 2 ? T.bn + 1 : 2;
+      const bool kw_pre = IS_KW && KW_FORM == 0 && SVAE_KW_PRE && do_rs;   // (block-uniform)
+      float kw1 = 0.f;
+      if (kw_pre) {
+        const int kk = T.kbeg + kt * 64 + lane_id_fresh();
+        const int off = kk < T.kend ? kk * 4 : 0x7FFFFFF0;
+        const u32x4 kwr = buffer_rsrc(p.k_weight, 0x7FFFFFF0u);
+        asm volatile("s_nop 4\n\tbuffer_load_dword %0, %1, %2, 0 offen" : "=&v"(kw1) : "v"(off), "s"(kwr) : "memory");
+      }
+      const bool late = (!IS_KW || KW_FORM > 0 || kw_pre) && p.dma_stagger && wr == 1 && kt + 1 < T.nk;   // (uniform)
       if (kt + 1 < T.nk) {
         if (!late) g3_issue<AT, BT>(p, T.A, T.B, sa, sb, T.m0, T.n0, T.kbeg + (kt + 1) * 64, T.kend, nxt, wave);
         kw_issue(T.kbeg + (kt + 1) * 64, T.kend, (g + 1) & 1);   // (every wave here, late or not)
-      } else if (has_next) {   // the next tile's first K-tile, in flight during this tile's epilogue
+      } else if (next_dma) {   // the next tile's first K-tile, in flight during this tile's epilogue
         const G3Tile TN = g3_tile(p, t3n);
-        if (TN.nk > 0) {
-          G3Src xa, xb;
-          srcs(TN, xa, xb);
-          g3_issue<AT, BT>(p, TN.A, TN.B, xa, xb, TN.m0, TN.n0, TN.kbeg, TN.kend, nxt, wave);
-          kw_issue(TN.kbeg, TN.kend, (g + 1) & 1);
-        }
+        g3_issue<AT, BT>(p, TN.A, TN.B, sa, sb, TN.m0, TN.n0, TN.kbeg, TN.kend, nxt, wave);
+        kw_issue(TN.kbeg, TN.kend, (g + 1) & 1);
+      } else if (kw_pre) {   // (see kw_pre: 8 pieces that read nothing, into the idle stage)
+        const u32x4 rs = buffer_rsrc(p.A, 0x7FFFFFF0u);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) dma16_lds(rs, nxt + (wave * 8 + i) * 1024, 0x7FFFFFF0);
       }
       // Quadrant walk (mh, nh) = (0,0) (0,1) (1,1) (1,0): A fragments of a half reused by two quadrants, B
       // fragments of a half by the turn. The next quadrant's fragment reads are issued ahead of the current
@@ -1341,7 +1342,6 @@ __device__ __forceinline__ void gemm256_run(const GP& p, int blk, int nwg) {
       // forms 1-3 of SVAE_KW_FORM, kept for diagnostic builds) read stale weights now and then in the bit-exact test
       // (DESIGN §6); registers loaded a K-tile ahead spilled (34 VGPRs). The first two column tiles (blocks bn = 0, 1
       // hold the same A rows) split the work by k-step, so neither runs much longer than the blocks without row sums.
-      const int ks0 = p.tn2 >= 2 ? T.bn : 0, ks1 = p.tn2 >= 2 ? T.bn + 1 : 2;
       auto rowsum2 = [&](const bf16x8 (&x)[2], const bf16x8 (&y)[2]) {
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
@@ -1352,10 +1352,21 @@ __device__ __forceinline__ void gemm256_run(const GP& p, int blk, int nwg) {
             k0 = *(const f32x4*)kws;
             k1 = *(const f32x4*)(kws + 4);
           } else if constexpr (IS_KW) {
-            const int kk = T.kbeg + kt * 64 + 32 * ks + 8 * (lane >> 4);   // (K % 8 == 0: 8 inside or 8 past)
-            const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
-            k0 = kk < T.kend ? *(const f32x4*)(p.k_weight + kk) : z4;
-            k1 = kk < T.kend ? *(const f32x4*)(p.k_weight + kk + 4) : z4;
+            if (kw_pre) {   // (kw1 landed: the wait after the second quadrant)
+              const int src0 = (32 * ks + 8 * (lane_id_fresh() >> 4)) * 4;
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                k0[e] = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(src0 + 4 * e, __builtin_bit_cast(int, kw1)));
+                k1[e] = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(src0 + 16 + 4 * e, __builtin_bit_cast(int, kw1)));
+              }
+            } else {        // (SVAE_KW_PRE=0 builds: loads at the use, the wait drains the DMA too: no stagger)
+              const int kk = T.kbeg + kt * 64 + 32 * ks + 8 * (lane_id_fresh() >> 4);
+              const int off = kk < T.kend ? kk * 4 : 0x7FFFFFF0;
+              const u32x4 kwr = buffer_rsrc(p.k_weight, 0x7FFFFFF0u);
+              asm volatile("s_nop 4\n\tbuffer_load_dwordx4 %0, %2, %3, 0 offen\n\t"
+                           "buffer_load_dwordx4 %1, %2, %3, 0 offen offset:16\n\ts_waitcnt vmcnt(0)"
+                           : "=&v"(k0), "=&v"(k1) : "v"(off), "s"(kwr) : "memory");
+            }
           }
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
@@ -1401,6 +1412,8 @@ __device__ __forceinline__ void gemm256_run(const GP& p, int blk, int nwg) {
 #pragma unroll
           for (int j = 0; j < 2; ++j) acc[i][2 + j] = mfma16(b1[j][ks], a0[i][ks], acc[i][2 + j]);
       if constexpr (AT) {
+        // kw1's one wait, for every wave here (a wait per use site let hipcc copy kw1 before the data landed)
+        if (kw_pre) asm volatile("s_waitcnt vmcnt(8)" : "+v"(kw1) :: "memory");
         if (do_rs) {
           if (wc == 0) rowsum2(a0[0], a0[1]);
           else if (wc == 1) rowsum2(a0[2], a0[3]);
@@ -1466,11 +1479,10 @@ __device__ __forceinline__ void gemm256_run(const GP& p, int blk, int nwg) {
       g3_reg_epilogue_ld<EPI>(p, acc, sbias, T.m0, T.n0, T.batch, T.split, wr, wc, lane);
     else if constexpr (EPI == G3_EPI_ACC_KW)
       g3_reg_epilogue_ld<SVAE_EPI_F32_ACC>(p, acc, sbias, T.m0, T.n0, T.batch, T.split, wr, wc, lane);
-    else if constexpr (EPI == G3_EPI_F32_KW)
-      g3_reg_epilogue_ld<SVAE_EPI_F32>(p, acc, sbias, T.m0, T.n0, T.batch, T.split, wr, wc, lane);
+    else if constexpr (EPI == G3_EPI_F32_KW || EPI == G3_EPI_SLAB)
+      g3_reg_epilogue_ld<G3_EPI_SLAB>(p, acc, sbias, T.m0, T.n0, T.batch, T.split, wr, wc, lane);
     else
-      g3_epilogue<EPI>(p, ring + ((g + 1) & 1) * G3_STAGE, acc, sbias, slabel, T.m0, T.n0, T.bn, T.batch, T.split,
-                       wr, wc, tid, lane);
+      static_assert(EPI == G3_EPI_SLAB, "no gemm256 epilogue for this EPI");
     relaxed = p.relaxed && T.m0 + 256 <= p.M && T.n0 + 256 <= p.N;
     G3_STAMP(2);
     ++ntile;
@@ -1478,7 +1490,6 @@ __device__ __forceinline__ void gemm256_run(const GP& p, int blk, int nwg) {
     const bool prefetched = T.nk > 0;
     t3 = t3n;
     T = g3_tile(p, t3);
-    srcs(T, sa, sb);
     if (!prefetched && T.nk > 0) {   // (an empty split-K slice prefetched nothing)
       g3_issue<AT, BT>(p, T.A, T.B, sa, sb, T.m0, T.n0, T.kbeg, T.kend, ring + (g & 1) * G3_STAGE, wave);
       kw_issue(T.kbeg, T.kend, g & 1);
@@ -1509,9 +1520,11 @@ struct GP2 {
 
 template <bool AT, bool BT, int EPI>
 __global__ __launch_bounds__(512, 1) void gemm256_pair_kernel(GP2 q) {
+  // one inlined copy of the block program over the selected GEMM's parameters (two copies, one per GEMM, kept both
+  // parameter sets in SGPRs: 185 SGPR spills)
   const int b = blockIdx.x;
-  if (b < q.nb0) gemm256_run<AT, BT, EPI>(q.p[0], b, q.nb0);
-  else gemm256_run<AT, BT, EPI>(q.p[1], b - q.nb0, (int)gridDim.x - q.nb0);
+  const int sel = b < q.nb0 ? 0 : 1;
+  gemm256_run<AT, BT, EPI>(q.p[sel], sel ? b - q.nb0 : b, sel ? (int)gridDim.x - q.nb0 : q.nb0);
 }
 
 // ===================================================================================================
@@ -1822,7 +1835,12 @@ static int gemm_run(const svae_gemm_desc* d, svae_stream_t stream, bool* fused_d
     else return SVAE_EINVAL;
   }
   if (impl == 3 && !ok3) impl = 1;
+  // float-atomic split-K (no slab workspace) is not a gemm256 epilogue: its staged 4-pass atomics cost 67-88 spilled
+  // VGPRs there; the 128-tile kernels run it (the product's split-K weight gradients use the slab form)
+  if (impl == 3 && epi_run == SVAE_EPI_F32_ATOMIC) impl = (kslice <= 2048 && !(d->a_t && d->b_t)) ? 2 : 1;
   if (impl == 3) {
+    // the weight-gradient slab layout stores through the plain slab epilogue (other layouts keep SVAE_EPI_F32)
+    if (slab && epi_run == SVAE_EPI_F32 && d->a_t && d->b_t) epi_run = G3_EPI_SLAB;
     int kc3 = (d->K + d->splits - 1) / d->splits;
     p.kchunk = (kc3 + 63) / 64 * 64;
     // persistent above one block per CU (1 block of 8 waves fits a CU): blocks walk their tiles and prefetch the
@@ -1860,7 +1878,6 @@ static int gemm_run(const svae_gemm_desc* d, svae_stream_t stream, bool* fused_d
     else hipLaunchKernelGGL((gemm256_kernel<false, false, E>), grid3, dim3(512), 0, s, p);                   \
     break;
     switch (epi_run) {
-      SVAE_GEMM3_CASE(SVAE_EPI_F32_ATOMIC)
       SVAE_GEMM3_CASE(SVAE_EPI_BF16)
       SVAE_GEMM3_CASE(SVAE_EPI_F32)
       SVAE_GEMM3_CASE(SVAE_EPI_F32_ACC)
@@ -1872,6 +1889,9 @@ static int gemm_run(const svae_gemm_desc* d, svae_stream_t stream, bool* fused_d
       case G3_EPI_ACC_KW:
         if (d->b_t) hipLaunchKernelGGL((gemm256_kernel<true, true, G3_EPI_ACC_KW>), grid3, dim3(512), 0, s, p);
         else hipLaunchKernelGGL((gemm256_kernel<true, false, G3_EPI_ACC_KW>), grid3, dim3(512), 0, s, p);
+        break;
+      case G3_EPI_SLAB:
+        hipLaunchKernelGGL((gemm256_kernel<true, true, G3_EPI_SLAB>), grid3, dim3(512), 0, s, p);
         break;
       case G3_EPI_F32_KW:
         if (!d->b_t) return SVAE_EINVAL;
@@ -1970,7 +1990,7 @@ SVAE_EXPORT int svae_gemm_pair(const svae_gemm_desc* d0, const svae_gemm_desc* d
   }
   q.nb0 = (int)((nb[0] + 7) / 8 * 8);   // block ranges start on an XCD boundary (block id % 8)
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL((gemm256_pair_kernel<true, true, SVAE_EPI_F32>), dim3((unsigned)(q.nb0 + nb[1])), dim3(512), 0, s,
+  hipLaunchKernelGGL((gemm256_pair_kernel<true, true, G3_EPI_SLAB>), dim3((unsigned)(q.nb0 + nb[1])), dim3(512), 0, s,
                      q);
   SVAE_LAUNCH_CHECK();
   static const int two_env = [] { const char* e = getenv("SVAE_SLAB2"); return e ? atoi(e) : 1; }();

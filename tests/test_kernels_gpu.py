@@ -48,13 +48,15 @@ def test_gemm_split_k_atomic_and_acc():
     assert torch.equal(C, 1 + 2 * (A.t() @ B))
 
 
+@pytest.mark.parametrize('Kk,Nn', [(2048, 776), (2056, 200)])
 @pytest.mark.parametrize('b_t', [True, False])
-def test_gemm256_at_rowsum_k_weight_exact(b_t):
+def test_gemm256_at_rowsum_k_weight_exact(b_t, Kk, Nn):
     """a_t on the 256x256 kernel with both B layouts (the vocabulary head's dW: MN-contiguous B; or K-contiguous):
     f32 accumulate with plain and k-weighted row sums, bit-exact on integer data, repeated (the k-weighted sums once
-    mismatched in a DMA-order experiment)."""
+    mismatched in a DMA-order experiment). N 776: 64 x 4 = 256 tiles, ragged N, each of the first two column tiles
+    sums one k-step of every K-tile; N 200: one column tile summing both k-steps, and a K tail (2056 = 32 x 64 + 8)."""
     g = torch.Generator(device=dev).manual_seed(5)
-    Kk, M, Nn = 2048, 16384, 776   # 64 x 4 = 256 tiles (>= 192: gemm256 with and without k_weight), ragged N
+    M = 16384
     A = torch.randint(-2, 3, (Kk, M), device=dev, generator=g).float()
     B = torch.randint(-2, 3, (Kk, Nn), device=dev, generator=g).float()
     kw = torch.randint(-2, 3, (Kk,), device=dev, generator=g).float()
@@ -643,6 +645,62 @@ def test_attention_fwd_bwd(B, H, Lq, Lk, hd, causal, padded, learned):
     def unheads(t):
         return t.transpose(1, 2).reshape(t.shape[0], t.shape[2], d)
 
+    assert _rel(dq, unheads(qr.grad)) < 2e-2
+    assert _rel(dk, unheads(kr.grad)) < 2e-2
+    assert _rel(dv, unheads(vr.grad)) < 2e-2
+
+
+@pytest.mark.parametrize('hd,L,causal', [(64, 1024, True), (96, 1024, True), (128, 512, True), (64, 520, False)])
+def test_attention_bwd_row_constant_slots_repeatable(hd, L, causal):
+    """The backward kernels take each query tile's lse and delta rows through a per-wave LDS slot filled by LDS-DMA
+    (the protocol whose k-weighted GEMM form once read stale slots). Here the query tiles' lse and delta
+    differ by large factors (Q and dO scaled per 64-query tile), so a slot read one tile stale would move dQ / dK / dV
+    far past the tolerance; 20 repeated backwards must also be bit-identical (the kernels are deterministic: no float
+    atomics), which catches an intermittent stale read even where its effect is small."""
+    torch.manual_seed(hd + L)
+    B, H = 4, 3
+    d = H * hd
+    nt = (L + 63) // 64
+    f = torch.tensor([0.25, 2.0, 0.5, 3.0, 1.0, 0.35, 2.5, 0.7], device=dev).repeat(nt)[:nt].repeat_interleave(64)[:L]
+    q = (torch.randn(B, L, d, device=dev) * f[None, :, None]).bfloat16()
+    k = torch.randn(B, L, d, device=dev).bfloat16()
+    v = torch.randn(B, L, d, device=dev).bfloat16()
+    do = (torch.randn(B, L, d, device=dev) * f.flip(0)[None, :, None] * 4).bfloat16()
+    pad = None
+    if not causal:
+        pad = torch.zeros(B, L, device=dev, dtype=torch.uint8)
+        pad[:, L - 37:] = 1
+    o = torch.empty(B, L, d, device=dev, dtype=torch.bfloat16)
+    lse = torch.empty(B, H, L, device=dev)
+    o32 = torch.empty(B, L, d, device=dev)
+    common = dict(B=B, H=H, Lq=L, Lk=L, hd=hd, sq=d, bq=L * d, sk=d, sv=d, bk=L * d, bv=L * d, so=d, bo=L * d,
+                  key_pad=pad, causal=causal)
+    K.attention(q, k, v, o, lse, o32=o32, so32=d, bo32=L * d, **common)
+    runs = []
+    for _ in range(20):
+        dq = torch.empty(B, L, d, device=dev)
+        dk = torch.empty(B, L, d, device=dev, dtype=torch.bfloat16)
+        dv = torch.empty_like(dk)
+        delta = torch.empty(B, H, L, device=dev)
+        K.attention(q, k, v, o, lse, backward=True, dout=do, sdo=d, bdo=L * d, delta=delta, dq=dq, bdq=L * d,
+                    dk=dk, dv=dv, sdk=d, sdv=d, bdk=L * d, bdv=L * d, o32=o32, so32=d, bo32=L * d, **common)
+        runs.append((dq, dk, dv))
+    torch.cuda.synchronize()
+    for i, r in enumerate(runs[1:], 1):
+        for name, a, b in zip(('dq', 'dk', 'dv'), runs[0], r):
+            assert torch.equal(a, b), (i, name, (a.float() - b.float()).abs().max().item())
+
+    def heads(t):
+        return t.float().view(B, L, H, hd).transpose(1, 2)
+
+    qr, kr, vr = (heads(t).requires_grad_() for t in (q, k, v))
+    ref = _attn_ref(qr, kr, vr, pad, causal, hd ** -0.5).transpose(1, 2).reshape(B, L, d)
+    ref.backward(do.float())
+
+    def unheads(t):
+        return t.transpose(1, 2).reshape(B, L, d)
+
+    dq, dk, dv = runs[0]
     assert _rel(dq, unheads(qr.grad)) < 2e-2
     assert _rel(dk, unheads(kr.grad)) < 2e-2
     assert _rel(dv, unheads(vr.grad)) < 2e-2
