@@ -56,11 +56,17 @@ def record(s, n, t):
     wc = s.get('SQ_WAVE_CYCLES', 0.0)
     grbm = s.get('GRBM_GUI_ACTIVE', 0.0)
     rec = {'launches': n}
+    busy = s.get('SQ_VALU_MFMA_BUSY_CYCLES', 0.0)
+    if t:
+        # busy x 1024 = the MFMA flops (calibrated on the 8K^3 GEMM), over the trace duration at the 2.5 PF peak
+        rec['mfma_frac_of_peak'] = round(busy * 1024 / t / 2.5e15, 4)
+        rec['us_per_launch'] = round(t / n * 1e6, 1)
     if grbm:
-        rec['mfma_util'] = round(s.get('SQ_VALU_MFMA_BUSY_CYCLES', 0.0) / (SIMDS * grbm / 8), 4)
+        rec['mfma_util_active_cycles'] = round(busy / (SIMDS * grbm / 8), 4)
         if t:
             rec['effective_clock_ghz'] = round(grbm / 8 / t / 1e9, 3)
-            rec['us_per_launch'] = round(t / n * 1e6, 1)
+    if busy and 'SQ_VALU_MFMA_COEXEC_CYCLES' in s:
+        rec['coexec_over_mfma_busy'] = round(s['SQ_VALU_MFMA_COEXEC_CYCLES'] / busy, 4)
     for c in ('SQ_WAIT_ANY', 'SQ_WAIT_INST_ANY', 'SQ_ACTIVE_INST_ANY', 'SQ_LDS_BANK_CONFLICT'):
         if wc and c in s:
             rec[c.lower().replace('sq_', '') + '_frac'] = round(s[c] / wc, 4)
@@ -70,11 +76,18 @@ def record(s, n, t):
 def main():
     root, cfg = sys.argv[1], sys.argv[2]
     which = sys.argv[3] if len(sys.argv) > 3 else 'gemm'
-    out = {'source': f'rocprofv3 --kernel-trace --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_ANY '
-                     f'SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE (one pass) over bench.py '
-                     f'--config {cfg} --steps 3 --warmup 2 (scripts/pmc_gemm_sq.sh)',
-           'denominator': 'mfma_util = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8); the *_frac '
-                          'fields are fractions of SQ_WAVE_CYCLES (quad-cycles per wave, like the WAIT/ACTIVE counters)'}
+    out = {'source': f'rocprofv3 --kernel-trace --pmc SQ_WAVE_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_VALU_MFMA_COEXEC_CYCLES '
+                     f'SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE (one pass) '
+                     f'over bench.py --config {cfg} --steps 3 --warmup 2 (scripts/pmc_gemm_sq.sh)',
+           'denominator': 'mfma_frac_of_peak = SQ_VALU_MFMA_BUSY_CYCLES x 1024 flop / (kernel-trace duration x 2.5 PF/s): '
+                          'the FLOP-derived fraction of the dense bf16 peak (the calibration pass shows busy x 1024 = '
+                          '2 M N K exactly); mfma_util_active_cycles = MFMA_BUSY / (1024 SIMDs x GRBM_GUI_ACTIVE / 8), '
+                          'the busy share of the SIMD-cycles at the clock the chip actually ran (GRBM_GUI_ACTIVE also '
+                          'counts the profiler gaps around a short dispatch: effective_clock_ghz > 2.4 marks a launch '
+                          'where that share is understated); the *_frac fields are fractions of SQ_WAVE_CYCLES '
+                          '(quad-cycles per wave, like the WAIT/ACTIVE counters); coexec_over_mfma_busy = '
+                          'SQ_VALU_MFMA_COEXEC_CYCLES / MFMA_BUSY (cycles in which vector and matrix instructions '
+                          'execute together, per MFMA-busy cycle)'}
     cs, cn, ct = per_kernel(f'{root}/calib')
     for key, s in cs.items():
         n = len(cn[key])
@@ -83,12 +96,12 @@ def main():
         grbm = s.get('GRBM_GUI_ACTIVE', 0.0)
         cal = {'kernel': key, 'launches': n, 'flops': flops,
                'mfma_busy_x1024_over_flops': round(busy * 1024 / flops, 4) if flops else None,
-               'mfma_util_counter': round(busy / (SIMDS * grbm / 8), 4) if grbm else None,
-               'mfma_util_flops': round(flops / (SIMDS * 1024 * grbm / 8), 4) if grbm else None}
+               'mfma_util_active_cycles': round(busy / (SIMDS * grbm / 8), 4) if grbm else None}
         if ct[key]:
             cal['effective_clock_ghz'] = round(grbm / 8 / ct[key] / 1e9, 3)
             cal['tflops_wall'] = round(flops / ct[key] / 1e12, 1)
-            cal['util_vs_2p5PF'] = round(flops / ct[key] / 2.5e15, 4)
+            cal['flop_derived_frac_of_peak'] = round(flops / ct[key] / 2.5e15, 4)
+            cal['mfma_frac_of_peak_from_counter'] = round(busy * 1024 / ct[key] / 2.5e15, 4)
         out['calibration_8192_cubed'] = cal
     sums, disp, tdur = per_kernel(f'{root}/{cfg}')
     sel = (lambda k: 'gemm' in k) if which == 'gemm' else (lambda k: 'attn' in k)
