@@ -1918,7 +1918,7 @@ SVAE_EXPORT int svae_attn_fwd(const svae_attn_desc* d, svae_stream_t stream) {
   if (d->causal && d->Lq != d->Lk) return SVAE_EINVAL;
   dim3 grid((d->Lq + 127) / 128, d->H, d->B);
   hipStream_t s = (hipStream_t)stream;
-  // the 32x32-MFMA kernel for hd <= 96 (SVAE_ATTN_FWD32=0: the 16x16 kernels, for A/B runs); its padding bit mask holds
+  // the 32x32-MFMA kernel for hd <= 64 (hd 96 spilled; SVAE_ATTN_FWD32=0: the 16x16 kernels, for A/B runs); its padding bit mask holds
   // FWD32_MAXPAD keys and its DMA / store offsets are 32-bit byte offsets from a sequence's row 0
   static const int fwd32_env = [] { const char* e = getenv("SVAE_ATTN_FWD32"); return e ? atoi(e) : 1; }();
   static const int occ_env = [] { const char* e = getenv("SVAE_ATTN_FWD32_OCC"); return e ? atoi(e) : 3; }();
