@@ -662,10 +662,10 @@ __device__ __forceinline__ void g3_issue_one(const bf16* tile_base, const G3Src&
                                              int krem, char* dst, int wave) {
   const u32x4 rs = buffer_rsrc(tile_base, 0x7FFFFFF0u);
   if (full) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) dma16_lds(rs, dst + (wave * 4 + i) * 1024, src.off[i]);
+    dma16x4_lds(rs, dst + wave * 4 * 1024, src.off[0], src.off[1], src.off[2], src.off[3]);
   } else {
     const int lane = lane_id_fresh();
+    int o[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       int x, y, off;
@@ -679,8 +679,9 @@ __device__ __forceinline__ void g3_issue_one(const bf16* tile_base, const G3Src&
         ok = x < nrem && y * 8 < krem;
         off = (x * (int)ld + y * 8) * 2;
       }
-      dma16_lds(rs, dst + (wave * 4 + i) * 1024, ok ? off : 0x7FFFFFF0);
+      o[i] = ok ? off : 0x7FFFFFF0;
     }
+    dma16x4_lds(rs, dst + wave * 4 * 1024, o[0], o[1], o[2], o[3]);
   }
 }
 
