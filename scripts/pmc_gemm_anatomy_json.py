@@ -3,8 +3,9 @@
     python scripts/pmc_gemm_anatomy_json.py gpurun_out/<tag> > profiles/pmc_gemm_anatomy_c2.json
 
 SQ_ACTIVE_INST_* and SQ_WAIT_INST_LDS are quad-cycles per wave like SQ_WAVE_CYCLES (fractions of it); SQ_LDS_IDX_ACTIVE,
-TA_TA_BUSY, TD_TD_BUSY and the stall counters are cycles summed over the CUs' units, normalised here by the kernel's
-active cycles GRBM_GUI_ACTIVE / 8 (per XCD) x 32 CUs per XCD = one unit's busy share."""
+TA_TA_BUSY, TD_TD_BUSY and the stall counters are summed over the chip's 256 per-CU units, normalised here by the
+kernel's active cycles GRBM_GUI_ACTIVE / 8 (GRBM sums the 8 XCDs) x 256 = one unit's busy share (not calibrated against
+a known-rate kernel: read them relative to each other)."""
 import collections
 import csv
 import glob
@@ -12,7 +13,7 @@ import json
 import re
 import sys
 
-CUS_PER_XCD = 32
+UNITS = 256
 
 
 def per_kernel(root):
@@ -40,8 +41,8 @@ def main():
     for key in sorted(set(s1) & set(s2), key=lambda k: -s1[k].get('SQ_WAVE_CYCLES', 0)):
         a, b = s1[key], s2[key]
         wc = a.get('SQ_WAVE_CYCLES', 0.0)
-        g1 = a.get('GRBM_GUI_ACTIVE', 0.0) / 8 * CUS_PER_XCD
-        g2 = b.get('GRBM_GUI_ACTIVE', 0.0) / 8 * CUS_PER_XCD
+        g1 = a.get('GRBM_GUI_ACTIVE', 0.0) / 8 * UNITS
+        g2 = b.get('GRBM_GUI_ACTIVE', 0.0) / 8 * UNITS
         rec = {'launches': len(d1[key])}
         for c in ('SQ_ACTIVE_INST_VMEM', 'SQ_ACTIVE_INST_LDS', 'SQ_ACTIVE_INST_VALU', 'SQ_ACTIVE_INST_SCA',
                   'SQ_ACTIVE_INST_MISC', 'SQ_WAIT_INST_LDS'):
