@@ -2,13 +2,13 @@
 # Same-box A/B of bench.py step times: variants alternate (each variant = an env assignment list, e.g.
 # "SVAE_LIB=sparse-vae_amd/sparse_vae/libsvae_old.so" or "SVAE_GEMM_STAGGER=0"; "-" = defaults), optionally after a
 # GPU test subset run with the default library.
-#   TESTS="tests/test_kernels_gpu.py -k gemm" CFGS="c2 c4" ROUNDS=2 bash scripts/ab_bench.sh TAG VARIANT...
+#   TESTS="tests/test_kernels_gpu.py -k 'gemm or attention'" CFGS="c2 c4" ROUNDS=2 bash scripts/ab_bench.sh TAG VARIANT...
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 OUT=gpurun_out/${1:-ab}; shift
 mkdir -p "$OUT"
 if [ -n "${TESTS:-}" ]; then
-  timeout -k 10 600 python -u -m pytest $TESTS -x -q --timeout 150 --timeout-method thread > "$OUT/tests.log" 2>&1 \
+  eval "timeout -k 10 600 python -u -m pytest $TESTS -x -q --timeout 150 --timeout-method thread" > "$OUT/tests.log" 2>&1 \
     || { tail -30 "$OUT/tests.log"; exit 1; }
   tail -2 "$OUT/tests.log"
 fi
