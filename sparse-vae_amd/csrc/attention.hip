@@ -1537,17 +1537,28 @@ __device__ __forceinline__ void attn_bwd8_tile(const AP& p, char* smem, int kb, 
   auto fetch = [&](int qb, int buf) {
     char* base = QO + buf * 2 * R::BYTES;
     const int ln = lane_id_fresh();
+    // a wave's QO_PW pieces are consecutive pieces of ONE image (Q for waves 0-3, dO for 4-7: 2 R::PIECES split over
+    // 8 waves), issued in one statement
+    static_assert(R::PIECES % QO_PW == 0 && (QO_PW == 2 || QO_PW == 3), "a wave's pieces within one image");
+    const bool isq = w * QO_PW < R::PIECES;   // (wave-uniform)
+    const int pc0 = isq ? w * QO_PW : w * QO_PW - R::PIECES;
+    char* img = isq ? base : base + R::BYTES;
+    const long long ld = isq ? p.sq : p.sdo;
+    const u32x4 irs = isq ? qrs : ors;
+    int po[3];
 #pragma unroll
     for (int i = 0; i < QO_PW; ++i) {
-      const int pc = w * QO_PW + i;
-      if (pc < R::PIECES) dma_img_piece<HDC>(qrs, p.sq, qb, p.Lq, p.hd, base, pc, ln);
-      else dma_img_piece<HDC>(ors, p.sdo, qb, p.Lq, p.hd, base + R::BYTES, pc - R::PIECES, ln);
+      int r, c;
+      R::piece_src(pc0 + i, ln, r, c);
+      const bool ok = qb + r < p.Lq && c * 8 < p.hd;
+      po[i] = ok ? ((qb + r) * (int)ld + c * 8) * 2 : 0x7FFFFFF0;
     }
+    if constexpr (QO_PW == 2) dma16x2_lds(irs, img + pc0 * 1024, po[0], po[1]);
+    else dma16x3_lds(irs, img + pc0 * 1024, po[0], po[1], po[2]);
     const int qo = qb + lane < p.Lq ? (qb + lane) * 4 : 0x7FFFFFF0;
     // every wave DMAs the tile's lse and delta rows into its OWN slot; it reads them only after its own
     // end-of-tile vmcnt (+ the block barrier), so no wave depends on another wave's DMA count
-    dma4_lds(lser, cst + (buf * NWB + w) * 128, qo);
-    dma4_lds(der, cst + (buf * NWB + w) * 128 + 64, qo);
+    dma4x2_lds(lser, der, cst + (buf * NWB + w) * 128, qo, qo);
   };
   if (qt0 < nqt) fetch(qt0 * 64, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -103,6 +103,40 @@ __device__ __forceinline__ void dma16x4_lds(const u32x4& rsrc, const void* lds_b
                : "memory", "scc");
 }
 
+// Two / three consecutive 1-KiB pieces in one statement (as dma16x4_lds).
+__device__ __forceinline__ void dma16x2_lds(const u32x4& rsrc, const void* lds_base, int v0, int v1) {
+  const int m = __builtin_amdgcn_readfirstlane((int)(unsigned)(uintptr_t)lds_base);
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_nop 1\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
+               "buffer_load_dwordx4 %2, %4, 0 offen lds\n\ts_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"
+               "buffer_load_dwordx4 %3, %4, 0 offen lds\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "s"(m), "v"(v0), "v"(v1), "s"(rsrc)
+               : "memory", "scc");
+}
+__device__ __forceinline__ void dma16x3_lds(const u32x4& rsrc, const void* lds_base, int v0, int v1, int v2) {
+  const int m = __builtin_amdgcn_readfirstlane((int)(unsigned)(uintptr_t)lds_base);
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_nop 1\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
+               "buffer_load_dwordx4 %2, %5, 0 offen lds\n\ts_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"
+               "buffer_load_dwordx4 %3, %5, 0 offen lds\n\ts_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"
+               "buffer_load_dwordx4 %4, %5, 0 offen lds\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "s"(m), "v"(v0), "v"(v1), "v"(v2), "s"(rsrc)
+               : "memory", "scc");
+}
+// Two dword slots 256 B apart from two tensors (the attention backward's lse and delta rows of a query tile).
+__device__ __forceinline__ void dma4x2_lds(const u32x4& rs_a, const u32x4& rs_b, const void* lds_base, int va, int vb) {
+  const int m = __builtin_amdgcn_readfirstlane((int)(unsigned)(uintptr_t)lds_base);
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_nop 1\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
+               "buffer_load_dword %2, %4, 0 offen lds\n\ts_add_u32 m0, m0, 0x100\n\ts_nop 0\n\t"
+               "buffer_load_dword %3, %5, 0 offen lds\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "s"(m), "v"(va), "v"(vb), "s"(rs_a), "s"(rs_b)
+               : "memory", "scc");
+}
+
 // 4 B per lane (buffer_load_dword ... lds) into lds_base + 4 * lane, same conventions as dma16_lds.
 __device__ __forceinline__ void dma4_lds(const u32x4& rsrc, const void* lds_base, int voff) {
   const int m = __builtin_amdgcn_readfirstlane((int)(unsigned)(uintptr_t)lds_base);
