@@ -184,8 +184,21 @@ __device__ __forceinline__ void dma_tile(const RowImg<HDC>*, const bf16* g, long
   static_assert(PW * 4 == RowImg<HDC>::PIECES, "pieces split over the 4 waves");
   const u32x4 rs = buffer_rsrc(g, 0x7FFFFFF0u);
   const int ln = lane_id_fresh();   // (offsets recomputed here, not kept live across the key loop)
+  if constexpr (PW == 2 || PW == 3) {   // the wave's consecutive pieces in one statement
+    int o[3];
 #pragma unroll
-  for (int i = 0; i < PW; ++i) dma_img_piece<HDC>(rs, ld, row0, nrows, hd, lds, w * PW + i, ln);
+    for (int i = 0; i < PW; ++i) {
+      int r, c;
+      RowImg<HDC>::piece_src(w * PW + i, ln, r, c);
+      const bool ok = row0 + r < nrows && c * 8 < hd;
+      o[i] = ok ? ((row0 + r) * (int)ld + c * 8) * 2 : 0x7FFFFFF0;
+    }
+    if constexpr (PW == 2) dma16x2_lds(rs, lds + w * PW * 1024, o[0], o[1]);
+    else dma16x3_lds(rs, lds + w * PW * 1024, o[0], o[1], o[2]);
+  } else {
+#pragma unroll
+    for (int i = 0; i < PW; ++i) dma_img_piece<HDC>(rs, ld, row0, nrows, hd, lds, w * PW + i, ln);
+  }
 }
 template <int HDP>
 constexpr int tile_pieces(const Tile<HDP>*) { return 64 * Tile<HDP>::PITCH / 1024; }
