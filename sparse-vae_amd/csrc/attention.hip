@@ -691,13 +691,27 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd32_kernel(AP p) {
     const int kn = (it2 == 0 ? 0 : kt1 + it2 - 1) * 64;
     char* kb = smem + (it2 % NS) * 2 * I::BYTES;
     const int ln = lane_id_fresh();   // (offsets recomputed at the issue, never kept live across the key loop)
+    if constexpr (PW == 2) {   // K's two pieces in one statement, V's in another
+      int ko[2], vo[2];
 #pragma unroll
-    for (int i = 0; i < PW; ++i) {
-      int r, c;
-      I::piece_src(w * PW + i, ln, r, c);
-      const bool ok = kn + r < p.Lk && c * 8 < p.hd;
-      dma16_lds(krs, kb + (w * PW + i) * 1024, ok ? ((kn + r) * (int)p.sk + c * 8) * 2 : 0x7FFFFFF0);
-      dma16_lds(vrs, kb + I::BYTES + (w * PW + i) * 1024, ok ? ((kn + r) * (int)p.sv + c * 8) * 2 : 0x7FFFFFF0);
+      for (int i = 0; i < 2; ++i) {
+        int r, c;
+        I::piece_src(w * PW + i, ln, r, c);
+        const bool ok = kn + r < p.Lk && c * 8 < p.hd;
+        ko[i] = ok ? ((kn + r) * (int)p.sk + c * 8) * 2 : 0x7FFFFFF0;
+        vo[i] = ok ? ((kn + r) * (int)p.sv + c * 8) * 2 : 0x7FFFFFF0;
+      }
+      dma16x2_lds(krs, kb + w * PW * 1024, ko[0], ko[1]);
+      dma16x2_lds(vrs, kb + I::BYTES + w * PW * 1024, vo[0], vo[1]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < PW; ++i) {
+        int r, c;
+        I::piece_src(w * PW + i, ln, r, c);
+        const bool ok = kn + r < p.Lk && c * 8 < p.hd;
+        dma16_lds(krs, kb + (w * PW + i) * 1024, ok ? ((kn + r) * (int)p.sk + c * 8) * 2 : 0x7FFFFFF0);
+        dma16_lds(vrs, kb + I::BYTES + (w * PW + i) * 1024, ok ? ((kn + r) * (int)p.sv + c * 8) * 2 : 0x7FFFFFF0);
+      }
     }
   };
 #pragma unroll

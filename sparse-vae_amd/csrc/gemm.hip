@@ -459,6 +459,7 @@ __device__ __forceinline__ void issue_tile2(const bf16* __restrict__ g, long lon
                                             int kend, char* lds_tile, int wave, int lane) {
   const bf16* base = TRANS ? g + (long long)k0 * ld + row0 : g + (long long)row0 * ld + k0;
   const u32x4 rsrc = buffer_rsrc(base, 0x7FFFFFF0u);
+  int o[G2_PIECES];
 #pragma unroll
   for (int j = 0; j < G2_PIECES; ++j) {
     const int inst = wave * G2_PIECES + j;
@@ -476,7 +477,13 @@ __device__ __forceinline__ void issue_tile2(const bf16* __restrict__ g, long lon
       off = (kr * (int)ld + v * 8) * 2;
       ok = (k0 + kr < kend) && (row0 + v * 8 < nrows);
     }
-    dma16_lds(rsrc, lds_tile + inst * 1024, ok ? off : 0x7FFFFFF0);
+    o[j] = ok ? off : 0x7FFFFFF0;
+  }
+  // the wave's consecutive pieces in one statement
+  if constexpr (G2_PIECES == 2) dma16x2_lds(rsrc, lds_tile + wave * G2_PIECES * 1024, o[0], o[1]);
+  else {
+#pragma unroll
+    for (int j = 0; j < G2_PIECES; ++j) dma16_lds(rsrc, lds_tile + (wave * G2_PIECES + j) * 1024, o[j]);
   }
 }
 
