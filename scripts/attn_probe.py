@@ -2,6 +2,8 @@
 some neighbours, and the C4 decoder shape (L=1024, hd=96).
 
     python scripts/attn_probe.py
+ATTN_PROBE_ONLY: hd96 | c2c4 | c2c4c5 (adds the C5 decoder shape B=32, L=2048, hd 96); ATTN_PROBE_ROT=1: the backward
+with the inverse rotary fused (bf16 dQ with rotary, as the engine runs it).
 """
 import os
 import sys
@@ -10,6 +12,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, 'sparse-vae_amd'))
 import torch  # noqa: E402
 from sparse_vae import kernels as K  # noqa: E402
+from sparse_vae.engine import rotary_table  # noqa: E402
 
 dev = torch.device('cuda', 0)
 
@@ -30,11 +33,16 @@ def timeit(fn, reps=20):
 def main():
     only = os.environ.get('ATTN_PROBE_ONLY')   # e.g. 'hd96': only the C4 decoder shape
     cases = [(64, 512, True, 64), (64, 512, False, 64), (16, 512, True, 64), (256, 512, True, 64), (64, 1024, True, 64),
-             (64, 1024, True, 96)]
+             (64, 1024, True, 96), (32, 2048, True, 96)]
+    rot_on = os.environ.get('ATTN_PROBE_ROT') == '1'
     for B, L, causal, hd in cases:
       if only == 'hd96' and hd != 96:
           continue
       if only == 'c2c4' and (B, L, causal, hd) not in ((64, 512, True, 64), (64, 1024, True, 96)):
+          continue
+      if only == 'c2c4c5' and (B, L, causal, hd) not in ((64, 512, True, 64), (64, 1024, True, 96), (32, 2048, True, 96)):
+          continue
+      if not only and L == 2048:
           continue
       for with_o32 in (True, 'olo', False):
         H = 8
@@ -56,9 +64,10 @@ def main():
         dqkv = torch.empty(B * L, 3 * d, device=dev).bfloat16()
         delta = torch.empty(B, H, L, device=dev)
         part = torch.empty(K.attn_dq_part_elems(B, H, L, L, hd), device=dev)
+        rkw = dict(rot=rotary_table(L, d).to(dev), rot_d=d) if rot_on else {}
         bwd = lambda: K.attention(qkv, qkv[:, d:], qkv[:, 2 * d:], o, lse, backward=True, dout=dout, sdo=d, bdo=L * d,
                                   delta=delta, dq_bf=dqkv, ldq_bf=3 * d, dk=dqkv[:, d:], dv=dqkv[:, 2 * d:], sdk=3 * d,
-                                  sdv=3 * d, bdk=L * 3 * d, bdv=L * 3 * d, dq_part=part, **kw)
+                                  sdv=3 * d, bdk=L * 3 * d, bdv=L * 3 * d, dq_part=part, **rkw, **kw)
         if not with_o32:
             print(f'B={B:4d} L={L:5d} hd={hd:3d} causal={int(causal)} no-o32 fwd {t:8.1f} us', flush=True)
             continue

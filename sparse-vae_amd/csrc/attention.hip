@@ -41,7 +41,7 @@ struct AP {
   bf16* olo; long long solo, bolo;   // bf16 residual O - bf16(O) (alternative to o32)
   int window;        // > 0: causal sliding window of `window` 32-key blocks plus key block 0 (SparseAttention)
   int kblk;          // backward: keys per dQ partial (the key block of the kernel that wrote dq_part)
-  int dq_direct;     // backward (attn_bwd8, causal): key block 0 stores the final dQ of queries < 256 itself
+  int dq_direct;     // backward (attn_bwd8, causal): the final dQ of queries < dq_direct is stored by attn_bwd8 itself
 };
 
 // Block-sparse sliding window of SparseAttention (sparse_attention.py:39-60, causal, block 32): query q sees
@@ -1479,8 +1479,8 @@ __device__ unsigned long long svae_bwd8_stamps[1024][8][8];
 #define BWD8_ACC(k, a, b) (st_acc[k] += (b) - (a))
 #endif
 
-template <int HDC>
-__device__ __forceinline__ void attn_bwd8_tile(const AP& p, char* smem, int kb, int h, int b) {
+template <int HDC, int NSUB, bool RMW>
+__device__ __forceinline__ void attn_bwd8_tile(const AP& p, char* smem, int kb, int h, int b, int nsub) {
   using R = RowImg<HDC>;
   using TS = Tile<64>;          // dS^T [256 keys][64 queries]
   constexpr int NKK = HDC / 32, NT = HDC / 16;
@@ -1491,6 +1491,10 @@ __device__ __forceinline__ void attn_bwd8_tile(const AP& p, char* smem, int kb, 
   char* dSs = Ks + 4 * R::BYTES;
   float* cst = (float*)(dSs + 4 * TS::BYTES);   // [buf][wave][lse, delta][64] (DMA'd with the tile)
   constexpr int NWB = 8;
+  char* rslots = (char*)(cst + 2 * NWB * 128);    // [wave][DQ_NT KiB]: the first sub-block's dQ partial (see rmw)
+  // [wave][DQ_NT KiB]: the direct tiles' rotary cos / sin. hd 96 has no LDS left for a second slot array: there the
+  // direct tiles are key block 0's (queries < 256, never rmw) and share the rmw slots (the host's dq_direct limit)
+  char* cslots = HDC == 64 && NSUB == 2 ? rslots + NWB * (HDC / 32) * 1024 : rslots;
   // LDS-DMA pieces per wave: one query tile's Q + dO images, and the K tile
   constexpr int QO_PW = 2 * R::PIECES / NW;
   constexpr int K_PW = 4 * R::PIECES / NW;
@@ -1544,14 +1548,22 @@ __device__ __forceinline__ void attn_bwd8_tile(const AP& p, char* smem, int kb, 
   const int q_end = (p.window > 0 && k0 > 0) ? min(p.Lq, k0 + BWD8_KEYS - SBLK + SBLK * p.window) : p.Lq;
   const int nqt = (q_end + 63) / 64;
   const int band_end = p.window > 0 && kw >= SBLK ? kw + SBLK * p.window : 0x7FFFFFFF;   // first query past kw's band
-  float* part = p.dq_part + ((long long)kb * p.B + b) * p.Lq * p.H * p.hd + (long long)h * p.hd;
+  // dQ partial plane pk: nsub = 2 consecutive 256-key sub-blocks (kb = 2 pk, 2 pk + 1) share one plane, swept one
+  // after the other by the same workgroup; the second adds the first's partial (read back by LDS-DMA into its own
+  // per-wave slot, `rmw`) before storing, so the planes -- and attn_dq_reduce's reads of them -- halve
+  const int pk = nsub == 2 ? kb >> 1 : kb;
+  constexpr bool rmw = RMW;   // (the second sub-block: kb odd, NSUB = nsub = 2)
+  // query tiles the first sub-block (keys k0 - 256 ..) stored: every tile from its qt0 (<= this qt0) to its q_end
+  const int nqt_prev = !rmw ? 0
+                       : (((p.window > 0 && k0 - BWD8_KEYS > 0)
+                               ? min(p.Lq, k0 - SBLK + SBLK * p.window) : p.Lq) + 63) >> 6;
+  float* part = p.dq_part + ((long long)pk * p.B + b) * p.Lq * p.H * p.hd + (long long)h * p.hd;
   const long long ldp = (long long)p.H * p.hd;
   const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc((void*)part, 0, 0x7FFFFFF0, 0x00020000);
   // final dQ of the direct tiles (see the dQ stores): row 0 of this (batch, head) in dq_bf (bf16) or dq (f32)
   void* dbase = p.dq_bf ? (void*)((bf16*)p.dq_bf + (long long)b * p.Lq * p.ldq_bf + (long long)h * p.hd)
                         : (void*)(p.dq + b * p.bdq + (long long)h * p.hd);
   const __amdgpu_buffer_rsrc_t drs = __builtin_amdgcn_make_buffer_rsrc(dbase, 0, 0x7FFFFFF0, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.rot, 0, 0x7FFFFFF0, 0x00020000);
   // dQ partial of a query tile (64 queries x HDC dims): wave w owns queries 16 (w & 3) .. + 15 and dims
   // (w >> 2) HDC / 2 .. + HDC / 2 - 1, i.e. NT / 2 fragments, stored as NT / 2 16-B buffer stores per lane (a fixed
   // count: the end-of-tile wait leaves exactly those in flight)
@@ -1582,7 +1594,7 @@ __device__ __forceinline__ void attn_bwd8_tile(const AP& p, char* smem, int kb, 
     }
     if constexpr (QO_PW == 2) dma16x2_lds(irs, img + pc0 * 1024, po[0], po[1]);
     else dma16x3_lds(irs, img + pc0 * 1024, po[0], po[1], po[2]);
-    const int qo = qb + lane < p.Lq ? (qb + lane) * 4 : 0x7FFFFFF0;
+    const int qo = qb + ln < p.Lq ? (qb + ln) * 4 : 0x7FFFFFF0;
     // every wave DMAs the tile's lse and delta rows into its OWN slot; it reads them only after its own
     // end-of-tile vmcnt (+ the block barrier), so no wave depends on another wave's DMA count
     dma4x2_lds(lser, der, cst + (buf * NWB + w) * 128, qo, qo);
@@ -1590,6 +1602,13 @@ __device__ __forceinline__ void attn_bwd8_tile(const AP& p, char* smem, int kb, 
   if (qt0 < nqt) fetch(qt0 * 64, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  // the V fragments' loads counted as complete here (an empty statement reading them: the compiler's own wait lands
+  // in front of it): left pending into the loop they got a vmcnt(0) before their first MFMA inside it (the second
+  // sub-block's instance), which waited for the next tile's DMA on every tile
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int kk = 0; kk < NKK; ++kk) asm volatile("" : "+v"(vf[j][kk]));
 
 #ifdef SVAE_STAMPS
   { BWD8_T(t1); BWD8_ACC(0, t_start, t1); }
@@ -1604,6 +1623,47 @@ __device__ __forceinline__ void attn_bwd8_tile(const AP& p, char* smem, int kb, 
     const char* Qs = QO + buf * 2 * R::BYTES;
     const char* dOs = Qs + R::BYTES;
     const float* nl = cst + (buf * NWB + w) * 128;
+    const bool rmw_t = rmw && qt < nqt_prev;   // (wave-uniform)
+    if (rmw_t) {
+      // this wave's dQ fragments of the first sub-block's partial (the layout of the stores below: piece u, lane l =
+      // query 16 dq_q16 + (l & 15), dims 16 (dq_u0 + u) + 4 (l >> 4) .. + 3) into its own slot; issued before the next
+      // tile's DMA, so the dQ phase's counted wait covers it. The first sub-block's stores were drained by the
+      // workgroup barrier between the sub-blocks.
+      const int lf = lane_id_fresh();
+      const bool qok = qb + 16 * dq_q16 + (lf & 15) < p.Lq;
+      const int qrow = (qb + 16 * dq_q16 + (lf & 15)) * (int)ldp + 4 * (lf >> 4);
+      const u32x4 prs4 = buffer_rsrc(part, 0x7FFFFFF0u);
+      int ro[DQ_NT];
+#pragma unroll
+      for (int u = 0; u < DQ_NT; ++u) {
+        const int d = 16 * (dq_u0 + u);
+        ro[u] = (qok && d + 4 * (lf >> 4) < p.hd) ? (qrow + d) * 4 : 0x7FFFFFF0;
+      }
+      static_assert(DQ_NT == 2 || DQ_NT == 3, "dQ fragments per wave");
+      if constexpr (DQ_NT == 2) dma16x2_lds(prs4, rslots + w * DQ_NT * 1024, ro[0], ro[1]);
+      else dma16x3_lds(prs4, rslots + w * DQ_NT * 1024, ro[0], ro[1], ro[2]);
+    }
+    // direct tiles (see the dQ stores): plane 0 (its sub-blocks hold every key of these causal queries), below the
+    // host's limit dq_direct, and below this sub-block's last key (a later sub-block of the plane adds to the others)
+    // (hd 96: dq_direct <= 256, so the second sub-block has no direct tiles)
+    const bool direct_t = !(RMW && HDC == 96) && pk == 0 && qb + 64 <= p.dq_direct && qb + 64 <= k0 + BWD8_KEYS;
+    const bool rot_t = direct_t && p.dq_bf && p.rot;
+    if (rot_t) {
+      // the inverse rotary's cos / sin of this wave's dQ fragments (query, dim pair 2 j, 2 j + 1 per 16 B), by
+      // LDS-DMA with the tile: a plain load at the use waited for it (and for the next tile's DMA) in the dQ phase
+      const int lf = lane_id_fresh();
+      const int q = qb + 16 * dq_q16 + (lf & 15);
+      const bool qok = q < p.Lq;
+      const u32x4 crs = buffer_rsrc(p.rot, 0x7FFFFFF0u);
+      int co[DQ_NT];
+#pragma unroll
+      for (int u = 0; u < DQ_NT; ++u) {
+        const int d = 16 * (dq_u0 + u) + 4 * (lf >> 4);
+        co[u] = (qok && d < p.hd) ? (q * (p.rot_d / 2) + (h * p.hd + d) / 2) * 8 : 0x7FFFFFF0;
+      }
+      if constexpr (DQ_NT == 2) dma16x2_lds(crs, cslots + w * DQ_NT * 1024, co[0], co[1]);
+      else dma16x3_lds(crs, cslots + w * DQ_NT * 1024, co[0], co[1], co[2]);
+    }
     if (qt + 1 < nqt) fetch(qb + 64, buf ^ 1);
     const bool live = (!p.causal || kw <= qb + 63) && qb < band_end && kw < p.Lk;
 #ifdef SVAE_STAMPS
@@ -1749,8 +1809,19 @@ __device__ __forceinline__ void attn_bwd8_tile(const AP& p, char* smem, int kb, 
         }
       }
     }
-    if (p.dq_direct && qb + 64 <= BWD8_KEYS) {
-      // causal, key block 0, queries < 256: this block holds every key these queries see, so dQ is final here
+    if (rmw_t || rot_t) {
+      // the slot DMAs landed once only the next tile's DMA (its QO_PW + 2 loads, issued after them) can be in flight
+      if (qt + 1 < nqt) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(QO_PW + 2) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    if (rmw_t) {
+      const lds_char* sl = lds_ptr(rslots + w * DQ_NT * 1024) + 16 * lane_id_fresh();
+#pragma unroll
+      for (int u = 0; u < DQ_NT; ++u) dq[u] += *(const f32x4*)(sl + 1024 * u);
+    }
+    if (direct_t) {
+      // causal, plane 0, queries below this sub-block's last key: plane 0's sub-blocks hold every key these queries
+      // see (the first sub-block's share added above), so dQ is final here
       // (scale, inverse rotary, bf16 or f32 out) -- no partial plane, and attn_dq_reduce skips these rows. The same
       // number of store instructions as the partial path (out-of-range offsets for masked lanes): the end-of-tile wait
       // counts them.
@@ -1766,18 +1837,16 @@ __device__ __forceinline__ void attn_bwd8_tile(const AP& p, char* smem, int kb, 
         f32x4 v = dq[u] * p.scale;
         if (p.dq_bf) {
           if (p.rot) {
-            // 32-bit buffer offsets (a masked lane's load returns 0 and its store is dropped): the 64-bit per-fragment
-            // addresses of a plain load were hoisted out of the q-tile loop and spilled (hd 96: 3 reloads per tile)
-            const f32x4 cs = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                rrs, ok ? (q * (p.rot_d / 2) + (h * p.hd + d) / 2) * 8 : 0x7FFFFFF0, 0, 0));
+            // (the tile's cos / sin slot; a masked lane's DMA wrote zeros and its store is dropped)
+            const f32x4 cs = *(const f32x4*)(lds_ptr(cslots + w * DQ_NT * 1024) + 16 * lf + 1024 * u);
             const float a0 = v[0], b0 = v[1], a1 = v[2], b1 = v[3];
             v[0] = a0 * cs[0] + b0 * cs[1];
             v[1] = -a0 * cs[1] + b0 * cs[0];
             v[2] = a1 * cs[2] + b1 * cs[3];
             v[3] = -a1 * cs[3] + b1 * cs[2];
           }
-          const bf16x4 pk = {f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
-          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, pk), drs,
+          const bf16x4 pd = {f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, pd), drs,
                                                 ok ? (q * (int)p.ldq_bf + d) * 2 : 0x7FFFFFF0, 0, 0);
         } else {
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), drs, ok ? (q * (int)ldp + d) * 4 : 0x7FFFFFF0,
@@ -1853,12 +1922,27 @@ __device__ __forceinline__ void attn_bwd8_tile(const AP& p, char* smem, int kb, 
 #endif
 }
 
-template <int HDC>
+template <int HDC, int NSUB>
 __global__ __launch_bounds__(512, 1) void attn_bwd8_kernel(AP p) {
-  __shared__ __attribute__((aligned(16))) char smem[8 * RowImg<HDC>::BYTES + 4 * Tile<64>::BYTES + 2 * 8 * 128 * 4];
+  // + the per-wave dQ slots of the second sub-block (8 waves x HDC / 32 KiB: hd 96 fills the CU's 160 KiB exactly)
+  // and, hd 64, the rotary slots of the direct tiles
+  __shared__ __attribute__((aligned(16))) char smem[8 * RowImg<HDC>::BYTES + 4 * Tile<64>::BYTES + 2 * 8 * 128 * 4 +
+                                                    (HDC == 64 && NSUB == 2 ? 2 : 1) * 8 * (HDC / 32) * 1024];
   int kb, h, b;
   xcd_block(kb, h, b, p.causal ? 2 : 0);
-  attn_bwd8_tile<HDC>(p, smem, kb, h, b);
+  // NSUB 256-key sub-blocks per workgroup and dQ plane (1, or 2 as two instances of the sweep: the loop form spilled
+  // 42 VGPRs into the q-tile loop at hd 96; nsub = p.kblk / 256 = NSUB, a run-time value on purpose -- the
+  // compile-time one changed the register allocation and spilled inside the hd 96 loop)
+  if constexpr (NSUB == 1) {
+    attn_bwd8_tile<HDC, 1, false>(p, smem, kb, h, b, 1);
+  } else {
+    const int nsub = p.kblk / BWD8_KEYS;
+    attn_bwd8_tile<HDC, 2, false>(p, smem, nsub * kb, h, b, nsub);
+    if (nsub == 2 && (2 * kb + 1) * BWD8_KEYS < p.Lk) {
+      __syncthreads();   // the first sub-block's LDS reads done and its dQ plane stores drained (vmcnt(0))
+      attn_bwd8_tile<HDC, 2, true>(p, smem, 2 * kb + 1, h, b, 2);
+    }
+  }
 }
 
 // One key block per workgroup. (Pairing key blocks x and nkb - 1 - x per workgroup, to even out the causal
@@ -1889,7 +1973,7 @@ __global__ __launch_bounds__(256) void attn_dq_reduce_kernel(AP p) {
   const int nkb = (p.Lk + KB - 1) / KB;
   const long long plane = (long long)rows * D;
   const int nk = p.causal ? min(nkb, q / KB + 1) : nkb;
-  if (p.dq_direct && q < KB) return;   // written final by attn_bwd8 (causal: key block 0 is the only contributor)
+  if (q < p.dq_direct) return;   // written final by attn_bwd8 (causal: plane 0 holds every key these queries see)
   // sliding window: key block k >= 1 wrote partials only for the query tiles it swept (see attn_bwd_kernel)
   int k1 = 1;
   if (p.window > 0)
@@ -1999,11 +2083,23 @@ SVAE_EXPORT int svae_attn_bwd(const svae_attn_desc* d, svae_stream_t stream) {
   // SVAE_ATTN_DQ_DIRECT=0: every query tile through the partial planes (A/B runs)
   static const int direct_env = [] { const char* e = getenv("SVAE_ATTN_DQ_DIRECT"); return e ? atoi(e) : 1; }();
   if (bwd8_env && d->hd <= 96) {
-    p.kblk = BWD8_KEYS;
-    p.dq_direct = (d->causal && direct_env) ? 1 : 0;
-    dim3 grid8((d->Lk + BWD8_KEYS - 1) / BWD8_KEYS, d->H, d->B);
-    if (d->hd <= 64) hipLaunchKernelGGL(attn_bwd8_kernel<64>, grid8, dim3(512), 0, s, p);
-    else hipLaunchKernelGGL(attn_bwd8_kernel<96>, grid8, dim3(512), 0, s, p);
+    // two 256-key sub-blocks per workgroup and dQ plane for >= 512 queries; fewer query tiles per key block (the
+    // encoder's latent queries) keep one: there the two serial sweeps of one workgroup cost more than the halved
+    // planes save. SVAE_BWD8_SUB=1: one everywhere (A/B runs)
+    static const int sub_env = [] { const char* e = getenv("SVAE_BWD8_SUB"); return e && atoi(e) == 1 ? 1 : 2; }();
+    const int nsub = sub_env == 2 && d->Lq >= 512 ? 2 : 1;
+    p.kblk = BWD8_KEYS * nsub;
+    // causal: attn_bwd8 stores the final dQ of the queries below dq_direct itself (hd 96: key block 0's, < 256;
+    // hd 64 with two sub-blocks: plane 0's, < 512)
+    p.dq_direct = (d->causal && direct_env) ? (nsub == 2 && d->hd <= 64 ? 2 : 1) * BWD8_KEYS : 0;
+    dim3 grid8((d->Lk + p.kblk - 1) / p.kblk, d->H, d->B);
+    if (d->hd <= 64) {
+      if (nsub == 2) hipLaunchKernelGGL((attn_bwd8_kernel<64, 2>), grid8, dim3(512), 0, s, p);
+      else hipLaunchKernelGGL((attn_bwd8_kernel<64, 1>), grid8, dim3(512), 0, s, p);
+    } else {
+      if (nsub == 2) hipLaunchKernelGGL((attn_bwd8_kernel<96, 2>), grid8, dim3(512), 0, s, p);
+      else hipLaunchKernelGGL((attn_bwd8_kernel<96, 1>), grid8, dim3(512), 0, s, p);
+    }
   } else {
     p.kblk = BWD_KEYS;
     dim3 grid((d->Lk + BWD_KEYS - 1) / BWD_KEYS, d->H, d->B);
@@ -2012,7 +2108,9 @@ SVAE_EXPORT int svae_attn_bwd(const svae_attn_desc* d, svae_stream_t stream) {
     else hipLaunchKernelGGL(attn_bwd_kernel<128>, grid, dim3(256), 0, s, p);
   }
   const long long work = (long long)d->B * d->Lq * (d->H * d->hd / 4);
-  hipLaunchKernelGGL(attn_dq_reduce_kernel, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, s, p);
+  // (causal with every query below kblk: attn_bwd8 stored the whole dQ itself)
+  if (d->Lq > p.dq_direct)
+    hipLaunchKernelGGL(attn_dq_reduce_kernel, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, s, p);
   SVAE_LAUNCH_CHECK();
   return SVAE_OK;
 }

@@ -606,6 +606,8 @@ def _attn_ref(q, k, v, pad, causal, scale):
     (1, 2, 1024, 1024, 96, True, True, False),     # C4 decoder head dim: 4 key blocks of 256, ragged padding
     (2, 2, 600, 600, 96, True, False, False),      # hd 96, last key block partial (600 = 2 x 256 + 88)
     (2, 4, 64, 520, 64, False, True, True),        # learned queries over 3 key blocks (the encoder's first layer)
+    (1, 2, 1536, 1536, 64, True, False, False),    # 3 dQ planes of two 256-key sub-blocks each
+    (1, 2, 256, 1300, 96, False, True, False),     # non-causal hd 96: 6 sub-blocks, the last partial, 3 planes
 ])
 def test_attention_fwd_bwd(B, H, Lq, Lk, hd, causal, padded, learned):
     torch.manual_seed(Lq * 7 + hd)
@@ -828,7 +830,8 @@ def test_attention_sliding_window_fwd_bwd(B, H, L, hd, window, padded):
 
 @pytest.mark.parametrize('B,H,L,hd', [
     (2, 4, 256, 64),     # every query < 256: dQ written final by key block 0 (no partial planes)
-    (2, 2, 640, 96),     # queries < 256 direct, the rest through the partial planes and the reduce
+    (2, 2, 640, 96),     # hd 96: queries < 256 direct, the rest through the partial planes and the reduce
+    (2, 2, 1100, 64),    # hd 64, two sub-blocks per plane: queries < 512 direct (with the first's partial added)
 ])
 def test_attention_bwd_fused_dq_rotary(B, H, L, hd):
     """bf16 dQ with inverse rotary (from key block 0 directly, or from the partial-sum reduce) == f32 dQ followed by
