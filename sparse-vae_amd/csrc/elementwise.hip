@@ -747,6 +747,7 @@ __global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ g,
 }
 
 // scal: {lr_eff, bcm, bcv, rho_ok, beta1, beta2, eps, wd, max_norm}
+template <int U, bool NTIN>
 __global__ __launch_bounds__(256) void radam_kernel(float* __restrict__ p, bf16* __restrict__ pbf, const float* __restrict__ g,
                                                     float* __restrict__ m, float* __restrict__ v, long long n,
                                                     const float* __restrict__ part, int nblk, const float* __restrict__ scal,
@@ -786,19 +787,24 @@ __global__ __launch_bounds__(256) void radam_kernel(float* __restrict__ p, bf16*
     ((f32x4*)p)[i] = pi;
     if (pbf) ((bf16x4*)pbf)[i] = (bf16x4){f2bf(pi[0]), f2bf(pi[1]), f2bf(pi[2]), f2bf(pi[3])};
   };
-  // two vectors per thread per iteration: all eight 16-B loads issued before the first update
+  // U vectors per thread per iteration: all 4 U 16-B loads issued before the first update (NTIN: the gradient and
+  // parameter loads nontemporal too)
   const long long stride = (long long)gridDim.x * 256;
   long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-  for (; i + stride < n4; i += 2 * stride) {
-    const long long j = i + stride;
-    const f32x4 ga = ((const f32x4*)g)[i], gb = ((const f32x4*)g)[j];
-    const f32x4 ma = __builtin_nontemporal_load((const f32x4*)m + i), mb = __builtin_nontemporal_load((const f32x4*)m + j);
-    const f32x4 va = __builtin_nontemporal_load((const f32x4*)v + i), vb = __builtin_nontemporal_load((const f32x4*)v + j);
-    const f32x4 pa = ((const f32x4*)p)[i], pb = ((const f32x4*)p)[j];
-    update(i, ga, ma, va, pa);
-    update(j, gb, mb, vb, pb);
+  for (; i + (U - 1) * stride < n4; i += U * stride) {
+    f32x4 gg[U], mm[U], vv[U], pp[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long j = i + u * stride;
+      gg[u] = NTIN ? __builtin_nontemporal_load((const f32x4*)g + j) : ((const f32x4*)g)[j];
+      mm[u] = __builtin_nontemporal_load((const f32x4*)m + j);
+      vv[u] = __builtin_nontemporal_load((const f32x4*)v + j);
+      pp[u] = NTIN ? __builtin_nontemporal_load((const f32x4*)p + j) : ((const f32x4*)p)[j];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) update(i + u * stride, gg[u], mm[u], vv[u], pp[u]);
   }
-  if (i < n4)
+  for (; i < n4; i += stride)
     update(i, ((const f32x4*)g)[i], ((const f32x4*)m)[i], ((const f32x4*)v)[i], ((const f32x4*)p)[i]);
 }
 
@@ -1316,8 +1322,17 @@ SVAE_EXPORT int svae_radam(float* p, void* pbf, const float* g, float* m, float*
                            int32_t nblk, const float* scal, float* norm_out, svae_stream_t stream) {
   if (!p || !g || !m || !v || !part || !scal || n <= 0 || n % 4 || nblk <= 0) return SVAE_EINVAL;
   if (((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15 || ((uintptr_t)pbf & 7)) return SVAE_EINVAL;
-  hipLaunchKernelGGL(radam_kernel, dim3(grid_for(n / 4, 256, 2048)), dim3(256), 0, (hipStream_t)stream, p, (bf16*)pbf, g, m,
-                     v, n, part, nblk, scal, norm_out);
+  // the gradient and parameter loads nontemporal as well (C2's 45 M parameters 263 -> 223-227 us; at C4's 162 M all
+  // variants run 4.6-5.0 TB/s: profiles/r05ra_radam_variants.log). SVAE_RADAM_U / _NT / _GRID: A/B variants
+  static const int u_env = [] { const char* e = getenv("SVAE_RADAM_U"); return e ? atoi(e) : 2; }();
+  static const int nt_env = [] { const char* e = getenv("SVAE_RADAM_NT"); return e ? atoi(e) : 1; }();
+  static const int grid_env = [] { const char* e = getenv("SVAE_RADAM_GRID"); return e ? atoi(e) : 2048; }();
+  const dim3 grid(grid_for(n / 4, 256, grid_env)), blk(256);
+  hipStream_t s = (hipStream_t)stream;
+  if (u_env == 4 && nt_env) hipLaunchKernelGGL((radam_kernel<4, true>), grid, blk, 0, s, p, (bf16*)pbf, g, m, v, n, part, nblk, scal, norm_out);
+  else if (u_env == 4) hipLaunchKernelGGL((radam_kernel<4, false>), grid, blk, 0, s, p, (bf16*)pbf, g, m, v, n, part, nblk, scal, norm_out);
+  else if (nt_env) hipLaunchKernelGGL((radam_kernel<2, true>), grid, blk, 0, s, p, (bf16*)pbf, g, m, v, n, part, nblk, scal, norm_out);
+  else hipLaunchKernelGGL((radam_kernel<2, false>), grid, blk, 0, s, p, (bf16*)pbf, g, m, v, n, part, nblk, scal, norm_out);
   SVAE_LAUNCH_CHECK();
   return SVAE_OK;
 }
