@@ -2082,7 +2082,12 @@ SVAE_EXPORT int svae_attn_bwd(const svae_attn_desc* d, svae_stream_t stream) {
   static const int bwd8_env = [] { const char* e = getenv("SVAE_ATTN_BWD8"); return e ? atoi(e) : 1; }();
   // SVAE_ATTN_DQ_DIRECT=0: every query tile through the partial planes (A/B runs)
   static const int direct_env = [] { const char* e = getenv("SVAE_ATTN_DQ_DIRECT"); return e ? atoi(e) : 1; }();
-  if (bwd8_env && d->hd <= 96) {
+  // one query tile (the encoder's 64 latent / learned queries) at hd <= 64: the 4-wave 128-key kernel, two workgroups per
+  // CU, hides more of the per-workgroup prologue / epilogue that such a sweep is made of (C2 encoder shape 64 -> 58 us,
+  // C4's 180 -> 171 us: profiles/r05enc_attn_bwd_smallq_probe.log). SVAE_ATTN_BWD_SMALLQ=0: the 8-wave kernel there too
+  static const int smallq_env = [] { const char* e = getenv("SVAE_ATTN_BWD_SMALLQ"); return e ? atoi(e) : 1; }();
+  const bool smallq = smallq_env && d->Lq <= 64 && d->hd <= 64;
+  if (bwd8_env && d->hd <= 96 && !smallq) {
     // two 256-key sub-blocks per workgroup and dQ plane for >= 512 queries; fewer query tiles per key block (the
     // encoder's latent queries) keep one: there the two serial sweeps of one workgroup cost more than the halved
     // planes save. SVAE_BWD8_SUB=1: one everywhere (A/B runs)
