@@ -15,6 +15,11 @@ Checks, per kernel:
   * M0_HAZARD        an LDS-DMA whose m0 write is not followed by >= 1 wait state;
   * M0_FOREIGN       a compiler instruction outside our asm that touches m0 in a kernel that also issues our DMA
                      (our statements save and restore m0, so this is informational: it should stay empty);
+  * ASYNC_EARLY_USE  a register-destination load issued inside our asm (the k-weighted GEMM's one dword per lane,
+                     gemm.hip `kw_pre`; the compiler takes the value as ready when the statement ends) whose
+                     destination VGPR is read, copied or overwritten before the first `s_waitcnt vmcnt(n <= 8)` after
+                     it (in program order): a v_mov of a live-range split placed there would copy a value that has not
+                     landed (silently wrong bias gradients);
   * spills           .vgpr_spill_count / .sgpr_spill_count from the kernel metadata, and how many scratch
                      instructions sit in each kernel, and how many of those sit inside a loop (a spill reload's
                      compiler vmcnt(0) inside a K-tile / q-tile loop drains the hand-counted DMA ring).
@@ -131,6 +136,33 @@ def loop_scratch(body):
     return inloop, inner
 
 
+VREG = re.compile(r'\bv\[(\d+):(\d+)\]|\bv(\d+)\b')
+
+
+def vregs(text):
+    out = set()
+    for m in VREG.finditer(text):
+        if m.group(3) is not None:
+            out.add(int(m.group(3)))
+        else:
+            out.update(range(int(m.group(1)), int(m.group(2)) + 1))
+    return out
+
+
+def async_early_use(body, i, dst):
+    """First instruction after the asm load at body[i] that touches VGPR dst before a vmcnt(<= 8) wait, or None."""
+    for j in range(i + 1, len(body)):
+        kind, text = body[j]
+        if kind != 'ins':
+            continue
+        m = re.match(r'^s_waitcnt\b.*vmcnt\((\d+)\)', text)
+        if m and int(m.group(1)) <= 8:
+            return None
+        if dst in vregs(text):
+            return j, text
+    return None
+
+
 def audit_kernel(name, body):
     issues = []
     in_asm = False
@@ -150,6 +182,12 @@ def audit_kernel(name, body):
             scratch += 1
         if not in_asm and kernel_has_dma and re.search(r'(^|[\s,])m0([\s,]|$)', text):
             issues.append(('M0_FOREIGN', i, text))
+        if in_asm and re.match(r'^buffer_load_dword$', op) and not text.rstrip().endswith('lds'):
+            dst = vregs(text.split(',')[0])
+            for r in dst:
+                hit = async_early_use(body, i, r)
+                if hit:
+                    issues.append(('ASYNC_EARLY_USE', i, f'{text!r}: v{r} touched by {hit[1]!r} before its wait'))
         if re.match(r'^buffer_load_\w+', op) and text.rstrip().endswith('lds'):
             ops = [o.strip() for o in text[len(op):].split(',')]
             srsrc = sregs(ops[1]) if len(ops) > 1 else set()
@@ -206,10 +244,12 @@ def main():
             issues, scratch = audit_kernel(name, body)
             vsp, ssp, vg = meta.get(name, (-1, -1, -1))
             ndma = sum(1 for k, t in body if k == 'ins' and t.endswith(' lds'))
+            nasync = sum(1 for k, t in body if k == 'ins' and t.split()[0] == 'buffer_load_dword' and
+                         not t.endswith('lds') and re.search(r'\boffen$', t))
             if issues:
                 bad += len(issues)
             inloop, inner = loop_scratch(body)
-            report[name] = dict(dma=ndma, vgpr=vg, vgpr_spill=vsp, sgpr_spill=ssp, scratch=scratch,
+            report[name] = dict(dma=ndma, async_loads=nasync, vgpr=vg, vgpr_spill=vsp, sgpr_spill=ssp, scratch=scratch,
                                 scratch_in_loops=inloop, scratch_in_mfma_loops=inner, hazards=len(issues))
             if issues or not args.quiet and (ndma or vsp > 0 or ssp > 0):
                 print(f'{os.path.basename(f)} {name}: {ndma} LDS-DMA, vgpr {vg}, spills v{vsp}/s{ssp}, '

@@ -2046,7 +2046,8 @@ SVAE_EXPORT int svae_attn_fwd(const svae_attn_desc* d, svae_stream_t stream) {
   static const int occ_env = [] { const char* e = getenv("SVAE_ATTN_FWD32_OCC"); return e ? atoi(e) : 3; }();
   static const int ns_env = [] { const char* e = getenv("SVAE_ATTN_FWD32_NS"); return e ? atoi(e) : 2; }();
   const bool fit32 = ((long long)d->Lk + 64) * std::max(d->sk, d->sv) * 2 < 0x7FFFFFF0LL &&
-                     ((long long)d->Lq + 128) * d->so * 2 < 0x7FFFFFF0LL && (!d->key_pad || d->Lk <= FWD32_MAXPAD);
+                     ((long long)d->Lq + 128) * d->so * 2 < 0x7FFFFFF0LL && (!d->key_pad || d->Lk <= FWD32_MAXPAD) &&
+                     (!d->o_lo || ((long long)d->Lq + 128) * d->so_lo * 2 < 0x7FFFFFF0LL);   // (o_lo's 32-bit offsets too)
   if (fwd32_env && fit32 && d->hd <= 64) {
     if (ns_env == 3) hipLaunchKernelGGL((attn_fwd32_kernel<64, 3, 3>), grid, dim3(256), 0, s, p);
     else if (occ_env == 4) hipLaunchKernelGGL((attn_fwd32_kernel<64, 4, 2>), grid, dim3(256), 0, s, p);
