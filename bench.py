@@ -44,24 +44,35 @@ CONFIGS = {
     'c5': dict(layers=12, d=768, heads=8, L=2048, B=32),
     # the C2 model with the reference's default decoder attention (sparse_self_attention, attn_window_size 4)
     'c2s': dict(layers=6, d=512, heads=8, L=512, B=64, window=4),
+    # the same model and tokens per batch at the sparse presets' sequence lengths (hparam_presets.py:122-171): 2 x 16384
+    'c2s16k': dict(layers=6, d=512, heads=8, L=16384, B=2, window=4),
 }
 V, NLAT = 32768, 64
 PEAK_BF16_TFLOPS = 2500.0      # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, chip-level parameters)
 
 
-def flops_per_token(nl, d, L, V=V, N=NLAT):
-    """F_train = 3 * F_fwd (dense count, verified against torch.utils.flop_counter)."""
+def _dec_keys(L, window):
+    """Keys per decoder query the count prices: all L (dense), or the sliding window's band -- window 32-key blocks
+    plus the [CLS] block (sparse_attention.py:39-60) -- which the window kernels visit."""
+    return L if not window else min(L, 32 * (window + 1))
+
+
+def flops_per_token(nl, d, L, V=V, N=NLAT, window=0):
+    """F_train = 3 * F_fwd (dense count, verified against torch.utils.flop_counter); window mode
+    prices the decoder's scores and P.V over the band's keys instead of all L."""
     f_enc = (4 * d * d + 4 * N * d + 18 * d * d * N / L) \
         + (nl // 2 - 2) * (4 * d * d + 4 * N * d + (28 * d * d * N + 4 * N * N * d) / L) \
         + (4 * d * d * N + 4 * N * d + 18 * d * d) / L
-    f_fwd = nl * (24 * d * d + 4 * L * d) + 2 * d * d + 2 * d * V + f_enc
+    f_fwd = nl * (24 * d * d + 4 * _dec_keys(L, window) * d) + 2 * d * d + 2 * d * V + f_enc
     return 3 * f_fwd
 
 
-def flops_per_token_causal(nl, d, L, V=V, N=NLAT):
-    """The causal-useful count: the dense count less the masked half of the decoder's causal
-    attention scores and P.V products, nl * 2 * L * d per token forward."""
-    return flops_per_token(nl, d, L, V, N) - 3 * nl * 2 * L * d
+def flops_per_token_causal(nl, d, L, V=V, N=NLAT, window=0):
+    """The causal-useful count: the dense count less the masked decoder attention: the upper half
+    (nl * 2 * L * d per token forward), or in window mode everything past the keys a query actually sees (on average
+    window - 1 full blocks, half its own block and the [CLS] block: 32 (window - 1) + 48)."""
+    useful = L / 2 if not window else min(L / 2, 32 * (window - 1) + 48)
+    return flops_per_token(nl, d, L, V, N, window) - 3 * nl * 4 * (_dec_keys(L, window) - useful) * d
 
 
 def build(cfg, device):
@@ -108,6 +119,9 @@ def cpu_baseline(cfg):
     """The oracle's fp32 fwd+bwd on the host cores on the config's own batch: one warm-up step at
     batch 2 (thread pool, allocator), then ONE timed step at the full per-GPU batch (C2: 64 x 512 tokens, ~10-30
     s on 8-16 cores)."""
+    if cfg['L'] > 4096:
+        # (the oracle's attention is dense: at 16 K tokens its autograd keeps ~100 GB of [L, L] probabilities)
+        return {'skipped': f'seq {cfg["L"]}: the dense CPU oracle does not fit a bounded sample'}
     import oracle
     from oracle.params import portable_ids
     threads = host_cores()
@@ -324,8 +338,8 @@ def main():
     ms = dt / args.steps * 1e3
     tokens = cfg['B'] * cfg['L'] * world * args.steps
     value = tokens / dt
-    fpt = flops_per_token(cfg['layers'], cfg['d'], cfg['L'])
-    fpt_causal = flops_per_token_causal(cfg['layers'], cfg['d'], cfg['L'])
+    fpt = flops_per_token(cfg['layers'], cfg['d'], cfg['L'], window=cfg.get('window', 0))
+    fpt_causal = flops_per_token_causal(cfg['layers'], cfg['d'], cfg['L'], window=cfg.get('window', 0))
     loss = model.logged.get('train_nll')
 
     scaling = None

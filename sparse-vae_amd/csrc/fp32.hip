@@ -83,8 +83,10 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__
   }
 }
 
-// One wave per (batch, head, query); scores for every key in LDS, softmax, then o[d] = sum_j p_j v[j][d].
-__global__ __launch_bounds__(256) void attn_fwd_f32_kernel(const float* __restrict__ q, const float* __restrict__ k,
+// One wave per (batch, head, query); scores for every key in LDS, softmax, then o[d] = sum_j p_j v[j][d]. WPB waves
+// (queries) per block: 4 up to 8192 keys, fewer beyond (each wave's score row is Lk floats of the 160 KiB LDS).
+template <int WPB>
+__global__ __launch_bounds__(64 * WPB) void attn_fwd_f32_kernel(const float* __restrict__ q, const float* __restrict__ k,
                                                            const float* __restrict__ v, float* __restrict__ o,
                                                            long long sq, long long sk, long long sv, long long so,
                                                            long long bq, long long bk, long long bv, long long bo,
@@ -93,7 +95,7 @@ __global__ __launch_bounds__(256) void attn_fwd_f32_kernel(const float* __restri
                                                            float scale) {
   extern __shared__ float sc[];   // [4 waves][Lk]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const long long gid_raw = (long long)blockIdx.x * 4 + wave;
+  const long long gid_raw = (long long)blockIdx.x * WPB + wave;
   const bool valid = gid_raw < (long long)B * H * Lq;
   const long long gid = valid ? gid_raw : 0;
   const int qi = (int)(gid % Lq), h = (int)((gid / Lq) % H), b = (int)(gid / ((long long)Lq * H));
@@ -166,12 +168,19 @@ SVAE_EXPORT int svae_attn_fwd_f32(const float* q, const float* k, const float* v
                                   int64_t sv, int64_t so, int64_t bq, int64_t bk, int64_t bv, int64_t bo,
                                   const uint8_t* key_pad, int32_t B, int32_t H, int32_t Lq, int32_t Lk, int32_t hd,
                                   int32_t causal, int32_t window, float scale, svae_stream_t stream) {
-  if (!q || !k || !v || !o || B <= 0 || H <= 0 || Lq <= 0 || Lk <= 0 || hd <= 0 || Lk > 8192) return SVAE_EINVAL;
+  if (!q || !k || !v || !o || B <= 0 || H <= 0 || Lq <= 0 || Lk <= 0 || hd <= 0 || Lk > 32768) return SVAE_EINVAL;
   if (window < 0 || (window > 0 && !causal)) return SVAE_EINVAL;
   const long long n = (long long)B * H * Lq;
-  hipLaunchKernelGGL(attn_fwd_f32_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 4 * Lk * sizeof(float),
-                     (hipStream_t)stream, q, k, v, o, sq, sk, sv, so, bq, bk, bv, bo, key_pad, B, H, Lq, Lk, hd, causal,
-                     window, scale);
+  hipStream_t st = (hipStream_t)stream;
+  if (Lk <= 8192)
+    hipLaunchKernelGGL(attn_fwd_f32_kernel<4>, dim3((unsigned)((n + 3) / 4)), dim3(256), 4 * Lk * sizeof(float), st, q, k,
+                       v, o, sq, sk, sv, so, bq, bk, bv, bo, key_pad, B, H, Lq, Lk, hd, causal, window, scale);
+  else if (Lk <= 16384)
+    hipLaunchKernelGGL(attn_fwd_f32_kernel<2>, dim3((unsigned)((n + 1) / 2)), dim3(128), 2 * Lk * sizeof(float), st, q, k,
+                       v, o, sq, sk, sv, so, bq, bk, bv, bo, key_pad, B, H, Lq, Lk, hd, causal, window, scale);
+  else
+    hipLaunchKernelGGL(attn_fwd_f32_kernel<1>, dim3((unsigned)n), dim3(64), Lk * sizeof(float), st, q, k, v, o, sq, sk,
+                       sv, so, bq, bk, bv, bo, key_pad, B, H, Lq, Lk, hd, causal, window, scale);
   SVAE_LAUNCH_CHECK();
   return SVAE_OK;
 }

@@ -191,3 +191,45 @@ def test_mutual_info_in_kernel_draws():
     assert torch.isfinite(ours).all() and ours.std() > 0
     se = ((ours.var() + theirs.var()) / 300).sqrt().item()
     assert abs(ours.mean().item() - theirs.mean().item()) < 6 * se + 1e-6, (ours.mean(), theirs.mean(), se)
+
+
+def test_sparse_step_long_sequence_matches_oracle():
+    """The sliding-window decoder at a long sequence (SparseAttention's lengths: hparam_presets.py:122-171 run
+    50 K / 100 K tokens per sample): 4 layers, d 256, 4 heads, L 4096 in window mode (window 4 x 32), one row padded
+    (so the decoder's padded-key forward takes the 16x16 kernel past FWD32_MAXPAD, and the backward's window key
+    blocks sweep only their band over 8 dQ planes), against the oracle's dense restatement of the block-sparse mask;
+    the bars of test_step_matches_oracle. The model's weights come from the oracle's portable generator (no golden
+    fixture: this is GPU-vs-oracle parity, the oracle being pinned by the other fixtures)."""
+    torch.set_num_threads(min(16, os.cpu_count()))
+    hp = oracle.HParams(d_model=256, num_heads=4, num_layers=4, latent_depth=64, kl_weight=0.7, attn_window=4)
+    params = oracle.init_params(hp, 4096)
+    B, L = 2, 4096
+    rng = np.random.default_rng(4096)
+    ids_np = rng.integers(3, hp.vocab_size, size=(B, L), dtype=np.int64)
+    ids_np[:, 0] = 1
+    lens = np.array([L, 3500])
+    for b, n in enumerate(lens):
+        ids_np[b, n - 1] = 2
+        ids_np[b, n:] = 0
+    ids = torch.from_numpy(ids_np)
+    ntok = torch.from_numpy(lens)
+    eps = torch.from_numpy(rng.standard_normal((B, 1, 64)).astype(np.float32))
+    kw = hp.kl_weight
+    p = {k: v.clone().requires_grad_(True) for k, v in params.items()}
+    ref = oracle.training_step(p, hp, ids, ntok, eps, kl_weight=kw)
+    ref['loss'].backward()
+
+    flat, eng = _build(hp, params)
+    assert eng.window == 4
+    out = eng.forward(ids.cuda(), ntok.cuda(), eps=eps.cuda(), dropout=0.0, kl_weight=kw)
+    flat.grad.zero_()
+    eng.backward(torch.ones((), device='cuda'), kw)
+    torch.cuda.synchronize()
+    loss, nll, kl = out['loss'].item(), out['nll'].item(), out['kl'].item()
+    assert abs(loss - ref['loss'].item()) / abs(ref['loss'].item()) < 1e-3
+    elbo_ref = -(ref['nll'].item() + ref['kl'].item())
+    assert abs(-(nll + kl) - elbo_ref) / abs(elbo_ref) < 1e-3
+    worst = _grad_report(flat, p)
+    msg = '\n'.join(f'{c:.5f} {r:.4f} {n}' for c, r, n in worst[:8])
+    print(f'[L4096 w4] loss {loss:.6f} ref {ref["loss"].item():.6f}\n' + msg)
+    _grad_bars(worst, msg)

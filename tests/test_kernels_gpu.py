@@ -781,6 +781,11 @@ def test_attention_fwd_running_max_growth(hd, L, causal, order):
     (1, 2, 640, 64, 1, False),      # window 1: diagonal block + [CLS] block only
     (2, 2, 256, 64, 8, False),      # window wider than the sequence: plain causal
     (1, 3, 1184, 32, 3, True),      # ragged tail (1184 = 37 blocks of 32), small head dim
+    # the lengths the reference's sparse presets run (hparam_presets.py:122-171: 50 K / 100 K tokens per sample): past
+    # 4096 padded keys the forward leaves the one-query-per-lane kernel for the 16x16 one (FWD32_MAXPAD), and the
+    # backward's sliding-window key blocks sweep only their band (q_end) over 32 / 64 dQ planes
+    (1, 2, 8192, 64, 4, True),
+    (1, 2, 16384, 64, 4, True),
 ])
 def test_attention_sliding_window_fwd_bwd(B, H, L, hd, window, padded):
     """window mode (SparseAttention's causal band + [CLS] block) vs a dense fp32 reference with the oracle's
