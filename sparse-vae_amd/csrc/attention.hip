@@ -42,6 +42,12 @@ struct AP {
   int window;        // > 0: causal sliding window of `window` 32-key blocks plus key block 0 (SparseAttention)
   int kblk;          // backward: keys per dQ partial (the key block of the kernel that wrote dq_part)
   int dq_direct;     // backward (attn_bwd8, causal): the final dQ of queries < dq_direct is stored by attn_bwd8 itself
+  // backward, sliding window (attn_bwd8 path): queries >= cls_q0 see nothing of dQ plane 0 but the [CLS] block (keys
+  // 0-31); plane 0's key blocks sweep only the queries below it, attn_bwd_cls_kernel takes the rest, and the [CLS]
+  // keys' dK / dV go as f32 partial slabs into cls_part (slab 0 from attn_bwd8) summed by attn_cls_finalize_kernel.
+  // 0 = off.
+  int cls_q0;
+  float* cls_part;
 };
 
 // Block-sparse sliding window of SparseAttention (sparse_attention.py:39-60, causal, block 32): query q sees
@@ -1479,6 +1485,26 @@ __device__ unsigned long long svae_bwd8_stamps[1024][8][8];
 #define BWD8_ACC(k, a, b) (st_acc[k] += (b) - (a))
 #endif
 
+// The [CLS] keys' f32 dK / dV partials of one wave (keys 16 j + li, dims 16 u + 4 g ..): slab layout [2][B][32][H hd]
+// (dK, then dV), unscaled and before the inverse rotary (attn_cls_finalize_kernel applies both to the slabs' sum)
+template <int NT>
+__device__ __forceinline__ void bwd_cls_store_slab(const AP& p, float* slab, int b, int h, const f32x4 (&dk)[2][NT],
+                                                   const f32x4 (&dv)[2][NT]) {
+  const int lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15;
+  const long long D = (long long)p.H * p.hd, half = (long long)p.B * 32 * D;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    float* row = slab + ((long long)b * 32 + 16 * j + li) * D + (long long)h * p.hd;
+#pragma unroll
+    for (int u = 0; u < NT; ++u) {
+      const int d = 16 * u + 4 * g;
+      if (d >= p.hd) continue;
+      *(f32x4*)(row + d) = dk[j][u];
+      *(f32x4*)(row + half + d) = dv[j][u];
+    }
+  }
+}
+
 template <int HDC, int NSUB, bool RMW>
 __device__ __forceinline__ void attn_bwd8_tile(const AP& p, char* smem, int kb, int h, int b, int nsub) {
   using R = RowImg<HDC>;
@@ -1545,7 +1571,9 @@ __device__ __forceinline__ void attn_bwd8_tile(const AP& p, char* smem, int kb, 
 
   const float inv_scale = 1.0f / p.scale, c = p.scale * LOG2E;
   const int qt0 = p.causal ? k0 / 64 : 0;
-  const int q_end = (p.window > 0 && k0 > 0) ? min(p.Lq, k0 + BWD8_KEYS - SBLK + SBLK * p.window) : p.Lq;
+  // (key block 0 in window mode: every query sees its [CLS] keys; with the [CLS] split it stops at cls_q0)
+  const int q_end = (p.window > 0 && k0 > 0) ? min(p.Lq, k0 + BWD8_KEYS - SBLK + SBLK * p.window)
+                                             : (p.cls_q0 > 0 ? min(p.Lq, p.cls_q0) : p.Lq);
   const int nqt = (q_end + 63) / 64;
   const int band_end = p.window > 0 && kw >= SBLK ? kw + SBLK * p.window : 0x7FFFFFFF;   // first query past kw's band
   // dQ partial plane pk: nsub = 2 consecutive 256-key sub-blocks (kb = 2 pk, 2 pk + 1) share one plane, swept one
@@ -1881,6 +1909,11 @@ __device__ __forceinline__ void attn_bwd8_tile(const AP& p, char* smem, int kb, 
 #endif
 
   // epilogue: dK (scaled, inverse rotary) and dV for key = kw + 16j + li, dims 16u + 4g + (0..3)
+  if (p.cls_q0 > 0 && kw == 0) {
+    // the [CLS] keys with the window's [CLS] split: their dK / dV so far (queries < cls_q0) as slab 0 of the f32
+    // partials attn_cls_finalize_kernel sums (unscaled, before the inverse rotary)
+    bwd_cls_store_slab<NT>(p, p.cls_part, b, h, dk, dv);
+  } else {
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int key = kw + 16 * j + li;
@@ -1907,6 +1940,7 @@ __device__ __forceinline__ void attn_bwd8_tile(const AP& p, char* smem, int kb, 
       *(bf16x4*)(DK + d) = (bf16x4){f2bf(x[0]), f2bf(x[1]), f2bf(x[2]), f2bf(x[3])};
       *(bf16x4*)(DV + d) = (bf16x4){f2bf(dv[j][u][0]), f2bf(dv[j][u][1]), f2bf(dv[j][u][2]), f2bf(dv[j][u][3])};
     }
+  }
   }
 #ifdef SVAE_STAMPS
   {
@@ -1943,6 +1977,213 @@ __global__ __launch_bounds__(512, 1) void attn_bwd8_kernel(AP p) {
       attn_bwd8_tile<HDC, 2, true>(p, smem, 2 * kb + 1, h, b, 2);
     }
   }
+}
+
+
+// ===================================================================================== backward, sliding window: [CLS]
+// With SparseAttention's window every query sees the [CLS] block (keys 0-31, sparse_attention.py:39-60 include_cls), so
+// key block 0 of attn_bwd8 would sweep ALL Lq / 64 query tiles while every other key block sweeps the ~6 of its band:
+// at 2 x 16384 tokens that one workgroup per (batch, head) took 810 us of 6 layers' 17 ms step
+// (profiles/r06i_c2s16k_kernel_summary.txt). With cls_q0 set, plane 0's key blocks stop at cls_q0 (past it they hold
+// nothing but the [CLS] keys for any query) and this kernel takes the queries >= cls_q0 against the 32 [CLS] keys:
+// 4 independent waves per workgroup, each sweeping CLS_TW query tiles with the bwd8 wave program for one 32-key slice
+// (key on the MFMA lane; its own Q / dO / lse / delta LDS images and its own dS^T image, so no workgroup barrier in
+// the loop), dQ of its tiles straight into plane 0 (no other writer there), dK / dV of the [CLS] keys into its own f32
+// slab; attn_cls_finalize_kernel sums the slabs in a fixed order (deterministic).
+constexpr int CLS_TW = 8;   // query tiles per wave
+
+template <int HDC>
+__global__ __launch_bounds__(256, 1) void attn_bwd_cls_kernel(AP p) {
+  using R = RowImg<HDC>;
+  using TS = Tile<64>;
+  constexpr int NKK = HDC / 32, NT = HDC / 16;
+  constexpr int WAVE_LDS = 2 * R::BYTES + 32 * TS::PITCH + 512;
+  __shared__ __attribute__((aligned(16))) char smem[R::BYTES + 4 * WAVE_LDS];
+  const int chunk = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  const int lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  char* Ks = smem;   // the [CLS] keys' K rows (rows 32-63 read as zeros)
+  char* Qs = smem + R::BYTES + w * WAVE_LDS;
+  char* dOs = Qs + R::BYTES;
+  char* dSs = dOs + R::BYTES;                  // dS^T [32 keys][64 queries]
+  float* nl = (float*)(dSs + 32 * TS::PITCH);  // [lse 64 | delta 64]
+  const long long hc = (long long)h * p.hd;
+  const bf16* Q = p.q + b * p.bq + hc;
+  const bf16* K = p.k + b * p.bk + hc;
+  const bf16* V = p.v + b * p.bv + hc;
+  const bf16* dO = p.dout + b * p.bdo + hc;
+  const float* lse = p.lse + ((long long)b * p.H + h) * p.Lq;
+  const float* delta = p.delta + ((long long)b * p.H + h) * p.Lq;
+  const int nk = min(p.Lk, 32);
+  {  // K image: the 4 waves split its pieces
+    const u32x4 krs = buffer_rsrc(K, 0x7FFFFFF0u);
+    for (int i = w; i < R::PIECES; i += 4) dma_img_piece<HDC>(krs, p.sk, 0, nk, p.hd, Ks, i, lane);
+  }
+  bool key_ok[2];
+  bf16x8 vf[2][NKK];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int key = 16 * j + li;
+    key_ok[j] = key < nk && !(p.pad && p.pad[(long long)b * p.Lk + key]);
+#pragma unroll
+    for (int kk = 0; kk < NKK; ++kk) {
+      const int d = 32 * kk + 8 * g;
+      u32x4 c = {0u, 0u, 0u, 0u};
+      if (key < nk && d < p.hd) c = *(const u32x4*)(V + (long long)key * p.sv + d);
+      vf[j][kk] = __builtin_bit_cast(bf16x8, c);
+    }
+  }
+  const bool keys_all_ok = __builtin_amdgcn_ballot_w64(!(key_ok[0] && key_ok[1])) == 0;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  f32x4 dk[2][NT], dv[2][NT];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int t = 0; t < NT; ++t) { dk[j][t] = (f32x4){0.f, 0.f, 0.f, 0.f}; dv[j][t] = dk[j][t]; }
+  const float inv_scale = 1.0f / p.scale, c = p.scale * LOG2E;
+  const int ntile = (p.Lq + 63) / 64;
+  const int t0 = p.cls_q0 / 64 + (chunk * 4 + w) * CLS_TW, t1 = min(ntile, t0 + CLS_TW);
+  float* part = p.dq_part + (long long)b * p.Lq * p.H * p.hd + hc;   // dQ plane 0
+  const long long ldp = (long long)p.H * p.hd;
+  const u32x4 qrs = buffer_rsrc(Q, 0x7FFFFFF0u), ors = buffer_rsrc(dO, 0x7FFFFFF0u);
+  const u32x4 lser = buffer_rsrc(lse, (unsigned)p.Lq * 4u), der = buffer_rsrc(delta, (unsigned)p.Lq * 4u);
+  for (int qt = t0; qt < t1; ++qt) {
+    const int qb = qt * 64;
+    for (int i = 0; i < R::PIECES; ++i) {
+      dma_img_piece<HDC>(qrs, p.sq, qb, p.Lq, p.hd, Qs, i, lane);
+      dma_img_piece<HDC>(ors, p.sdo, qb, p.Lq, p.hd, dOs, i, lane);
+    }
+    const int qo = qb + lane < p.Lq ? (qb + lane) * 4 : 0x7FFFFFF0;
+    dma4x2_lds(lser, der, nl, qo, qo);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // every query of the tile is past the [CLS] keys (qb >= cls_q0 > 31) and inside their window: masks only for
+    // padded keys and the ragged end
+    const bool edge = !keys_all_ok || qb + 64 > p.Lq;
+    const int qlim = p.Lq - qb;
+    constexpr int TPP = 2;
+#pragma unroll
+    for (int pass = 0; pass < 4 / TPP; ++pass) {
+      bf16x8 kf[2][NKK];
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int kk = 0; kk < NKK; ++kk) kf[j][kk] = *(const bf16x8*)(Ks + R::off(16 * j + li, g + 4 * kk));
+      f32x4 s[2][TPP], dp[2][TPP];
+#pragma unroll
+      for (int th = 0; th < TPP; ++th) {
+        const int t = pass * TPP + th;
+        const f32x4 sl = *(const f32x4*)(nl + 16 * t + 4 * g) * -inv_scale;
+        const f32x4 dl = -*(const f32x4*)(nl + 64 + 16 * t + 4 * g);
+        s[0][th] = sl; s[1][th] = sl;
+        dp[0][th] = dl; dp[1][th] = dl;
+        if (edge) {
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const unsigned kbad = key_ok[j] ? 0u : 1u;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int ql = 16 * t + 4 * g + r;
+              s[j][th][r] = (kbad | (unsigned)(ql >= qlim)) ? -INFINITY : s[j][th][r];
+            }
+          }
+        }
+#pragma unroll
+        for (int k2 = 0; k2 < NKK; ++k2) {
+          const bf16x8 qa = *(const bf16x8*)(Qs + R::off(16 * t + li, g + 4 * k2));
+          const bf16x8 oa = *(const bf16x8*)(dOs + R::off(16 * t + li, g + 4 * k2));
+          s[0][th] = mfma16(qa, kf[0][k2], s[0][th]);
+          s[1][th] = mfma16(qa, kf[1][k2], s[1][th]);
+          dp[0][th] = mfma16(oa, vf[0][k2], dp[0][th]);
+          dp[1][th] = mfma16(oa, vf[1][k2], dp[1][th]);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int th = 0; th < TPP; ++th)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float pr = __builtin_amdgcn_exp2f(s[j][th][r] * c);
+            s[j][th][r] = pr;
+            dp[j][th][r] = pr * dp[j][th][r];
+          }
+#pragma unroll
+      for (int k2 = 0; k2 < TPP / 2; ++k2) {
+        const int kk = pass * (TPP / 2) + k2;
+        const bf16x8 pf0 = pack8(s[0][2 * k2], s[0][2 * k2 + 1]), pf1 = pack8(s[1][2 * k2], s[1][2 * k2 + 1]);
+        const bf16x8 df0 = pack8(dp[0][2 * k2], dp[0][2 * k2 + 1]), df1 = pack8(dp[1][2 * k2], dp[1][2 * k2 + 1]);
+        const int rq = 4 * g + (li >> 2);
+#pragma unroll
+        for (int u = 0; u < NT; ++u) {
+          const int uu = 4 * u + (li & 3);
+          const int pitch = 16 * u < 64 ? 128 : 64;
+          const lds_char* po = lds_ptr(dOs) + R::uoff(rq, uu) + 32 * kk * pitch;
+          const lds_char* pq = lds_ptr(Qs) + R::uoff(rq, uu) + 32 * kk * pitch;
+          const bf16x8 ao = cat44(lds_read_tr3(po), lds_read_tr3(po + 16 * pitch));
+          dv[0][u] = mfma16(ao, pf0, dv[0][u]);
+          dv[1][u] = mfma16(ao, pf1, dv[1][u]);
+          const bf16x8 aq = cat44(lds_read_tr3(pq), lds_read_tr3(pq + 16 * pitch));
+          dk[0][u] = mfma16(aq, df0, dk[0][u]);
+          dk[1][u] = mfma16(aq, df1, dk[1][u]);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int th = 0; th < TPP; ++th)
+          *(bf16x4*)(dSs + TS::uoff(16 * j + li, 4 * (pass * TPP + th) + g)) =
+              (bf16x4){f2bf(dp[j][th][0]), f2bf(dp[j][th][1]), f2bf(dp[j][th][2]), f2bf(dp[j][th][3])};
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // (the wave's own dS^T writes, read back below)
+    // dQ of the tile over the 32 [CLS] keys: query 16 q16 + li, dims 16 u + 4 g .. (plane 0, unscaled)
+    const int q4 = 8 * g + (li >> 2);
+#pragma unroll
+    for (int q16 = 0; q16 < 4; ++q16) {
+      const int uq = 4 * q16 + (li & 3);
+      const bf16x8 a = cat44(lds_read_tr3(lds_ptr(dSs) + TS::uoff(q4, uq)), lds_read_tr3(lds_ptr(dSs) + TS::uoff(q4 + 4, uq)));
+      const int q = qb + 16 * q16 + li;
+#pragma unroll
+      for (int u = 0; u < NT; ++u) {
+        const int uk = 4 * u + (li & 3);
+        const bf16x8 bk = cat44(lds_read_tr3(lds_ptr(Ks) + R::uoff(q4, uk)), lds_read_tr3(lds_ptr(Ks) + R::uoff(q4 + 4, uk)));
+        const f32x4 dq = mfma16(bk, a, (f32x4){0.f, 0.f, 0.f, 0.f});
+        const int d = 16 * u + 4 * g;
+        if (q < p.Lq && d < p.hd) *(f32x4*)(part + (long long)q * ldp + d) = dq;
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // (the LDS reads done before the next tile's DMA)
+  }
+  bwd_cls_store_slab<NT>(p, p.cls_part + (long long)(1 + chunk * 4 + w) * 2 * p.B * 32 * p.H * p.hd, b, h, dk, dv);
+}
+
+// dK / dV of the [CLS] keys = the sum of the nslab f32 slabs (slab 0 from attn_bwd8's key block 0, the rest from
+// attn_bwd_cls_kernel) in a fixed order; dK scaled and inverse-rotated (pos = key) like attn_bwd8's epilogue
+__global__ __launch_bounds__(256) void attn_cls_finalize_kernel(AP p, int nslab) {
+  const int D = p.H * p.hd, D4 = D / 4;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= p.B * 32 * D4) return;
+  const int row = i / D4, c4 = i - row * D4;   // row = b * 32 + key
+  const int b = row / 32, key = row - b * 32;
+  if (key >= p.Lk) return;
+  const long long half = (long long)p.B * 32 * D;
+  const float* src = p.cls_part + (long long)row * D + 4 * c4;
+  f32x4 k4 = {0.f, 0.f, 0.f, 0.f}, v4 = k4;
+  for (int s = 0; s < nslab; ++s) {
+    k4 += *(const f32x4*)(src + s * 2 * half);
+    v4 += *(const f32x4*)(src + s * 2 * half + half);
+  }
+  k4 *= p.scale;
+  if (p.rot) {
+    const f32x4 cs = *(const f32x4*)(p.rot + ((long long)key * (p.rot_d / 2) + 2 * c4) * 2);
+    const float a0 = k4[0], b0 = k4[1], a1 = k4[2], b1 = k4[3];
+    k4[0] = a0 * cs[0] + b0 * cs[1];
+    k4[1] = -a0 * cs[1] + b0 * cs[0];
+    k4[2] = a1 * cs[2] + b1 * cs[3];
+    k4[3] = -a1 * cs[3] + b1 * cs[2];
+  }
+  *(bf16x4*)(p.dk + b * p.bdk + (long long)key * p.sdk + 4 * c4) = (bf16x4){f2bf(k4[0]), f2bf(k4[1]), f2bf(k4[2]), f2bf(k4[3])};
+  *(bf16x4*)(p.dv + b * p.bdv + (long long)key * p.sdv + 4 * c4) = (bf16x4){f2bf(v4[0]), f2bf(v4[1]), f2bf(v4[2]), f2bf(v4[3])};
 }
 
 // One key block per workgroup. (Pairing key blocks x and nkb - 1 - x per workgroup, to even out the causal
@@ -2027,6 +2268,8 @@ bool fill(const svae_attn_desc* d, AP& p) {
   if (p.olo && ((p.solo | p.bolo) % 8)) return false;
   p.kblk = BWD_KEYS;
   p.dq_direct = 0;
+  p.cls_q0 = 0;
+  p.cls_part = nullptr;
   if (p.window < 0 || (p.window > 0 && !p.causal)) return false;
   if (p.o32 && ((p.so32 | p.bo32) % 4)) return false;
   return true;
@@ -2098,6 +2341,16 @@ SVAE_EXPORT int svae_attn_bwd(const svae_attn_desc* d, svae_stream_t stream) {
     // causal: attn_bwd8 stores the final dQ of the queries below dq_direct itself (hd 96: key block 0's, < 256;
     // hd 64 with two sub-blocks: plane 0's, < 512)
     p.dq_direct = (d->causal && direct_env) ? (nsub == 2 && d->hd <= 64 ? 2 : 1) * BWD8_KEYS : 0;
+    // sliding window: queries from cls_q0 on see nothing of dQ plane 0 but the [CLS] block -> attn_bwd_cls_kernel
+    // (SVAE_ATTN_CLS_SPLIT=0: key block 0 sweeps every query, A/B runs)
+    static const int cls_env = [] { const char* e = getenv("SVAE_ATTN_CLS_SPLIT"); return e ? atoi(e) : 1; }();
+    if (cls_env && d->window > 0 && d->causal && (!d->rot_tab || d->rot_d == d->H * d->hd)) {
+      const int q0 = (std::min(d->Lq, p.kblk - SBLK + SBLK * d->window) + 63) / 64 * 64;
+      if (q0 < d->Lq) {
+        p.cls_q0 = q0;
+        p.cls_part = d->dq_part + (long long)((d->Lk + BWD_KEYS - 1) / BWD_KEYS) * d->B * d->Lq * d->H * d->hd;
+      }
+    }
     dim3 grid8((d->Lk + p.kblk - 1) / p.kblk, d->H, d->B);
     if (d->hd <= 64) {
       if (nsub == 2) hipLaunchKernelGGL((attn_bwd8_kernel<64, 2>), grid8, dim3(512), 0, s, p);
@@ -2113,6 +2366,14 @@ SVAE_EXPORT int svae_attn_bwd(const svae_attn_desc* d, svae_stream_t stream) {
     else if (d->hd <= 96) hipLaunchKernelGGL((attn_bwd_kernel<128, 96>), grid, dim3(256), 0, s, p);
     else hipLaunchKernelGGL(attn_bwd_kernel<128>, grid, dim3(256), 0, s, p);
   }
+  if (p.cls_q0 > 0) {
+    const int nfar = (d->Lq + 63) / 64 - p.cls_q0 / 64, nchunk = (nfar + 4 * CLS_TW - 1) / (4 * CLS_TW);
+    const dim3 gc(nchunk, d->H, d->B);
+    if (d->hd <= 64) hipLaunchKernelGGL(attn_bwd_cls_kernel<64>, gc, dim3(256), 0, s, p);
+    else hipLaunchKernelGGL(attn_bwd_cls_kernel<96>, gc, dim3(256), 0, s, p);
+    const long long nf = (long long)d->B * 32 * (d->H * d->hd / 4);
+    hipLaunchKernelGGL(attn_cls_finalize_kernel, dim3((unsigned)((nf + 255) / 256)), dim3(256), 0, s, p, 1 + 4 * nchunk);
+  }
   const long long work = (long long)d->B * d->Lq * (d->H * d->hd / 4);
   // (causal with every query below kblk: attn_bwd8 stored the whole dQ itself)
   if (d->Lq > p.dq_direct)
@@ -2123,7 +2384,10 @@ SVAE_EXPORT int svae_attn_bwd(const svae_attn_desc* d, svae_stream_t stream) {
 
 SVAE_EXPORT int64_t svae_attn_dq_part_elems(int32_t B, int32_t H, int32_t Lq, int32_t Lk, int32_t hd) {
   if (B <= 0 || H <= 0 || Lq <= 0 || Lk <= 0 || hd <= 0) return 0;
-  return (int64_t)((Lk + BWD_KEYS - 1) / BWD_KEYS) * B * Lq * H * hd;
+  // + the sliding window's [CLS] dK / dV slabs (attn_bwd_cls_kernel): at most 1 + 4 ceil(tiles / (4 CLS_TW)) of
+  // [2][B][32][H hd]
+  const int64_t nslab = 1 + 4 * (((Lq + 63) / 64 + 4 * CLS_TW - 1) / (4 * CLS_TW));
+  return (int64_t)((Lk + BWD_KEYS - 1) / BWD_KEYS) * B * Lq * H * hd + nslab * 2 * B * 32 * H * hd;
 }
 
 #ifdef SVAE_STAMPS

@@ -786,10 +786,12 @@ def test_attention_fwd_running_max_growth(hd, L, causal, order):
     # backward's sliding-window key blocks sweep only their band (q_end) over 32 / 64 dQ planes
     (1, 2, 8192, 64, 4, True),
     (1, 2, 16384, 64, 4, True),
+    (1, 2, 1024, 96, 4, True),      # hd 96 (two 256-key sub-blocks per plane): queries >= 640 through the [CLS] kernel
 ])
 def test_attention_sliding_window_fwd_bwd(B, H, L, hd, window, padded):
     """window mode (SparseAttention's causal band + [CLS] block) vs a dense fp32 reference with the oracle's
-    sparse mask; also the f32 kernel mode's forward."""
+    sparse mask; also the f32 kernel mode's forward. Past the band of dQ plane 0 (L >= 576 here) the [CLS] keys'
+    share of the far queries runs in attn_bwd_cls_kernel (dK / dV through its f32 slabs)."""
     torch.manual_seed(L + window)
     d = H * hd
     q, k, v = (torch.randn(B, L, d, device=dev).bfloat16() for _ in range(3))
