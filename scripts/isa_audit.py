@@ -16,10 +16,11 @@ Checks, per kernel:
   * M0_FOREIGN       a compiler instruction outside our asm that touches m0 in a kernel that also issues our DMA
                      (our statements save and restore m0, so this is informational: it should stay empty);
   * ASYNC_EARLY_USE  a register-destination load issued inside our asm (the k-weighted GEMM's one dword per lane,
-                     gemm.hip `kw_pre`; the compiler takes the value as ready when the statement ends) whose
-                     destination VGPR is read, copied or overwritten before the first `s_waitcnt vmcnt(n <= 8)` after
-                     it (in program order): a v_mov of a live-range split placed there would copy a value that has not
-                     landed (silently wrong bias gradients);
+                     gemm.hip `kw_pre`; the attention backward's in-kernel delta O / o_lo rows; the compiler takes the
+                     value as ready when the statement ends) whose destination VGPR is read, copied or overwritten
+                     before the first `s_waitcnt vmcnt(N)` that retires it (at most N vector-memory instructions issued
+                     after it, in program order): a v_mov of a live-range split placed there would copy a value that has
+                     not landed (silently wrong results);
   * spills           .vgpr_spill_count / .sgpr_spill_count from the kernel metadata, and how many scratch
                      instructions sit in each kernel, and how many of those sit inside a loop (a spill reload's
                      compiler vmcnt(0) inside a K-tile / q-tile loop drains the hand-counted DMA ring).
@@ -149,8 +150,14 @@ def vregs(text):
     return out
 
 
-def async_early_use(body, i, dst):
-    """First instruction after the asm load at body[i] that touches VGPR dst before a vmcnt(<= 8) wait, or None."""
+VMEM = re.compile(r'^(buffer|global|scratch|flat)_(load|store|atomic)')
+
+
+def async_early_use(body, i, dst, labels=None):
+    """First instruction after the asm load at body[i] (in program order) that touches VGPR dst before a
+    `s_waitcnt vmcnt(N <= 8)`, or None. The product's one such load (gemm.hip `kw_pre`) is retired by the
+    vmcnt(8) that leaves exactly the K-tile's 8 DMA pieces in flight; a linear scan is the check that matters there
+    (a live-range-split copy of the register would sit between the statement and that wait)."""
     for j in range(i + 1, len(body)):
         kind, text = body[j]
         if kind != 'ins':
@@ -166,6 +173,7 @@ def async_early_use(body, i, dst):
 def audit_kernel(name, body):
     issues = []
     in_asm = False
+    labels = {t.split(':')[0].strip(): k for k, (kind, t) in enumerate(body) if kind == 'label'}
     kernel_has_dma = any(k == 'ins' and re.search(r'offen lds$|\blds$', t) for k, t in body)
     scratch = 0
     for i, (kind, text) in enumerate(body):
@@ -182,10 +190,10 @@ def audit_kernel(name, body):
             scratch += 1
         if not in_asm and kernel_has_dma and re.search(r'(^|[\s,])m0([\s,]|$)', text):
             issues.append(('M0_FOREIGN', i, text))
-        if in_asm and re.match(r'^buffer_load_dword$', op) and not text.rstrip().endswith('lds'):
+        if in_asm and re.match(r'^buffer_load_dword(x[234])?$', op) and not text.rstrip().endswith('lds'):
             dst = vregs(text.split(',')[0])
             for r in dst:
-                hit = async_early_use(body, i, r)
+                hit = async_early_use(body, i, r, labels)
                 if hit:
                     issues.append(('ASYNC_EARLY_USE', i, f'{text!r}: v{r} touched by {hit[1]!r} before its wait'))
         if re.match(r'^buffer_load_\w+', op) and text.rstrip().endswith('lds'):
@@ -244,8 +252,8 @@ def main():
             issues, scratch = audit_kernel(name, body)
             vsp, ssp, vg = meta.get(name, (-1, -1, -1))
             ndma = sum(1 for k, t in body if k == 'ins' and t.endswith(' lds'))
-            nasync = sum(1 for k, t in body if k == 'ins' and t.split()[0] == 'buffer_load_dword' and
-                         not t.endswith('lds') and re.search(r'\boffen$', t))
+            nasync = sum(1 for k, t in body if k == 'ins' and re.match(r'buffer_load_dword(x[234])?$', t.split()[0]) and
+                         not t.endswith('lds') and re.search(r'\boffen( offset:\d+)?$', t))
             if issues:
                 bad += len(issues)
             inloop, inner = loop_scratch(body)

@@ -48,6 +48,8 @@ struct AP {
   // 0 = off.
   int cls_q0;
   float* cls_part;
+  // backward (attn_bwd8, hd <= 64, o_lo given): delta = rowsum(dO . O) computed inside the kernel (no attn_delta_kernel)
+  int delta_inkernel;
 };
 
 // Block-sparse sliding window of SparseAttention (sparse_attention.py:39-60, causal, block 32): query q sees
@@ -1627,9 +1629,62 @@ __device__ __forceinline__ void attn_bwd8_tile(const AP& p, char* smem, int kb, 
     // end-of-tile vmcnt (+ the block barrier), so no wave depends on another wave's DMA count
     dma4x2_lds(lser, der, cst + (buf * NWB + w) * 128, qo, qo);
   };
+  // In-kernel delta (hd 64, p.delta_inkernel): waves 4-7, which DMA the dO image of a tile (rows 16 (w - 4) .. + 15),
+  // DMA the same rows of O and of its bf16 residual o_lo into a slot of their own with the tile (4 more LDS-DMA pieces,
+  // retired by the same end-of-tile wait) and reduce delta = sum_d dO . (O + o_lo) of their 16 rows into the shared
+  // slot dsh[buf] before the end-of-tile barrier that publishes the tile. This replaces the attn_delta_kernel pass
+  // (which re-read O, o_lo and dO: 100 MB per launch at C2, 19 us). (Register loads instead -- compiler-visible ones --
+  // made hipcc put a vmcnt(0) in front of them on every tile, behind the next tile's DMA.)
+  constexpr bool DIK_OK = HDC == 64;
+  const bool dik = DIK_OK && p.delta_inkernel != 0;   // (uniform)
+  float* dsh = (float*)(rslots + (HDC == 64 && NSUB == 2 ? 2 : 1) * NWB * (HDC / 32) * 1024);   // [2][64]
+  char* dslot = (char*)(dsh + 128) + (w - 4) * 4096;   // waves 4-7: [O 16 x 64 | o_lo 16 x 64] bf16, row-major
+  const u32x4 ors_o = buffer_rsrc(p.o + b * p.bo + (long long)h * p.hd, 0x7FFFFFF0u);
+  const u32x4 ors_l = buffer_rsrc(p.olo ? p.olo + b * p.bolo + (long long)h * p.hd : p.o, 0x7FFFFFF0u);
+  auto dik_issue = [&](int qb) {   // piece i, lane l: row 8 i + (l >> 3) of the wave's 16, dims 8 (l & 7) .. + 7
+    const int ln = lane_id_fresh();
+    int oo[2], ol[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int r = 16 * (w - 4) + 8 * i + (ln >> 3), dd = 8 * (ln & 7);
+      const bool ok = qb + r < p.Lq && dd < p.hd;   // (dims >= hd land as zeros, as in the dO image)
+      oo[i] = ok ? ((qb + r) * (int)p.so + dd) * 2 : 0x7FFFFFF0;
+      ol[i] = ok ? ((qb + r) * (int)p.solo + dd) * 2 : 0x7FFFFFF0;
+    }
+    dma16x2_lds(ors_o, dslot, oo[0], oo[1]);
+    dma16x2_lds(ors_l, dslot + 2048, ol[0], ol[1]);
+  };
+  auto dik_reduce = [&](int buf, int qb) {   // after this wave's wait for the tile's DMA and its O / o_lo pieces
+    const int ln = lane_id_fresh();
+    const int rl = ln >> 2, r = 16 * (w - 4) + rl, c0 = 2 * (ln & 3);
+    const char* dimg = QO + buf * 2 * R::BYTES + R::BYTES;
+    float sacc = 0.f;
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      const bf16x8 dv8 = *(const bf16x8*)(dimg + R::off(r, c0 + hh));
+      const bf16x8 o8 = *(const bf16x8*)(dslot + rl * 128 + (c0 + hh) * 16);
+      const bf16x8 l8 = *(const bf16x8*)(dslot + 2048 + rl * 128 + (c0 + hh) * 16);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) sacc += ((float)o8[e] + (float)l8[e]) * (float)dv8[e];
+    }
+    sacc += __shfl_xor(sacc, 1);
+    sacc += __shfl_xor(sacc, 2);
+    if ((ln & 3) == 0) {
+      dsh[buf * 64 + r] = sacc;
+      // (also to the delta buffer, as the separate pass writes it: every workgroup that sweeps the tile stores the
+      // same value)
+      if (qb + r < p.Lq) ((float*)p.delta)[((long long)b * p.H + h) * p.Lq + qb + r] = sacc;
+    }
+  };
   if (qt0 < nqt) fetch(qt0 * 64, 0);
+  if (dik && w >= 4 && qt0 < nqt) dik_issue(qt0 * 64);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  if (dik) {
+    if (w >= 4 && qt0 < nqt) dik_reduce(0, qt0 * 64);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
   // the V fragments' loads counted as complete here (an empty statement reading them: the compiler's own wait lands
   // in front of it): left pending into the loop they got a vmcnt(0) before their first MFMA inside it (the second
   // sub-block's instance), which waited for the next tile's DMA on every tile
@@ -1693,6 +1748,8 @@ __device__ __forceinline__ void attn_bwd8_tile(const AP& p, char* smem, int kb, 
       else dma16x3_lds(crs, cslots + w * DQ_NT * 1024, co[0], co[1], co[2]);
     }
     if (qt + 1 < nqt) fetch(qb + 64, buf ^ 1);
+    if (dik && w >= 4 && qt + 1 < nqt) dik_issue(qb + 64);
+    const float* dlp = dik ? dsh + buf * 64 : nl + 64;   // the tile's delta rows
     const bool live = (!p.causal || kw <= qb + 63) && qb < band_end && kw < p.Lk;
 #ifdef SVAE_STAMPS
     if (live) st_acc[6] += 1;
@@ -1716,7 +1773,7 @@ __device__ __forceinline__ void attn_bwd8_tile(const AP& p, char* smem, int kb, 
         for (int th = 0; th < TPP; ++th) {
           const int t = pass * TPP + th;
           const f32x4 sl = *(const f32x4*)(nl + 16 * t + 4 * g) * -inv_scale;   // -lse / scale
-          const f32x4 dl = -*(const f32x4*)(nl + 64 + 16 * t + 4 * g);          // -delta
+          const f32x4 dl = -*(const f32x4*)(dlp + 16 * t + 4 * g);              // -delta
           s[0][th] = sl; s[1][th] = sl;
           dp[0][th] = dl; dp[1][th] = dl;
           if (edge) {
@@ -1796,6 +1853,13 @@ __device__ __forceinline__ void attn_bwd8_tile(const AP& p, char* smem, int kb, 
 #endif
     __builtin_amdgcn_s_barrier();   // dS^T complete (a raw barrier: __syncthreads' vmcnt(0) would drain the DMA)
     asm volatile("" ::: "memory");
+    // in-kernel delta of the NEXT tile, by waves 4-7 beside the other waves' dQ phase (its DMA, issued at the top of
+    // this step, has landed by now; their only older vector-memory operations are the last step's dQ stores); written
+    // to dsh[buf ^ 1], published by the end-of-tile barrier. (At the end of the step it held every wave at that barrier.)
+    if (dik && w >= 4 && qt + 1 < nqt) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      dik_reduce(buf ^ 1, qb + 64);
+    }
 #ifdef SVAE_STAMPS
     BWD8_T(tc);
     BWD8_ACC(2, tb, tc);
@@ -1839,8 +1903,13 @@ __device__ __forceinline__ void attn_bwd8_tile(const AP& p, char* smem, int kb, 
     }
     if (rmw_t || rot_t) {
       // the slot DMAs landed once only the next tile's DMA (its QO_PW + 2 loads, issued after them) can be in flight
-      if (qt + 1 < nqt) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(QO_PW + 2) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // (+ the 4 O / o_lo loads of waves 4-7 with the in-kernel delta)
+      if (qt + 1 < nqt) {
+        if (dik && w >= 4) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(QO_PW + 6) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(QO_PW + 2) : "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
     }
     if (rmw_t) {
       const lds_char* sl = lds_ptr(rslots + w * DQ_NT * 1024) + 16 * lane_id_fresh();
@@ -1961,7 +2030,8 @@ __global__ __launch_bounds__(512, 1) void attn_bwd8_kernel(AP p) {
   // + the per-wave dQ slots of the second sub-block (8 waves x HDC / 32 KiB: hd 96 fills the CU's 160 KiB exactly)
   // and, hd 64, the rotary slots of the direct tiles
   __shared__ __attribute__((aligned(16))) char smem[8 * RowImg<HDC>::BYTES + 4 * Tile<64>::BYTES + 2 * 8 * 128 * 4 +
-                                                    (HDC == 64 && NSUB == 2 ? 2 : 1) * 8 * (HDC / 32) * 1024];
+                                                    (HDC == 64 && NSUB == 2 ? 2 : 1) * 8 * (HDC / 32) * 1024 +
+                                                    (HDC == 64 ? 2 * 64 * 4 + 4 * 4096 : 0)];   // (+ in-kernel delta)
   int kb, h, b;
   xcd_block(kb, h, b, p.causal ? 2 : 0);
   // NSUB 256-key sub-blocks per workgroup and dQ plane (1, or 2 as two instances of the sweep: the loop form spilled
@@ -2270,6 +2340,7 @@ bool fill(const svae_attn_desc* d, AP& p) {
   p.dq_direct = 0;
   p.cls_q0 = 0;
   p.cls_part = nullptr;
+  p.delta_inkernel = 0;
   if (p.window < 0 || (p.window > 0 && !p.causal)) return false;
   if (p.o32 && ((p.so32 | p.bo32) % 4)) return false;
   return true;
@@ -2316,11 +2387,6 @@ SVAE_EXPORT int svae_attn_bwd(const svae_attn_desc* d, svae_stream_t stream) {
   if (((long long)std::max(d->Lq, d->Lk) + 64) * std::max(std::max(d->sq, d->sk), d->sdo) * 2 > 0x7FFFFFF0LL) return SVAE_EINVAL;
   hipStream_t s = (hipStream_t)stream;
   const int rows = d->B * d->Lq * d->H;
-  // delta_ready: the dO GEMM's epilogue already wrote delta (svae_gemm_desc.delta)
-  if (!d->delta_ready) {
-    if (d->hd <= 64) hipLaunchKernelGGL(attn_delta_kernel<8>, dim3((rows + 31) / 32), dim3(256), 0, s, p);
-    else hipLaunchKernelGGL(attn_delta_kernel<16>, dim3((rows + 15) / 16), dim3(256), 0, s, p);
-  }
   // hd <= 96: the 8-wave 256-key kernel; hd 128: the 4-wave 128-key one (its LDS rows do not fit the 8-wave layout).
   // SVAE_ATTN_BWD8=0: the 4-wave kernels for every hd (A/B runs)
   static const int bwd8_env = [] { const char* e = getenv("SVAE_ATTN_BWD8"); return e ? atoi(e) : 1; }();
@@ -2331,12 +2397,13 @@ SVAE_EXPORT int svae_attn_bwd(const svae_attn_desc* d, svae_stream_t stream) {
   // C4's 180 -> 171 us: profiles/r05enc_attn_bwd_smallq_probe.log). SVAE_ATTN_BWD_SMALLQ=0: the 8-wave kernel there too
   static const int smallq_env = [] { const char* e = getenv("SVAE_ATTN_BWD_SMALLQ"); return e ? atoi(e) : 1; }();
   const bool smallq = smallq_env && d->Lq <= 64 && d->hd <= 64;
-  if (bwd8_env && d->hd <= 96 && !smallq) {
-    // two 256-key sub-blocks per workgroup and dQ plane for >= 512 queries; fewer query tiles per key block (the
-    // encoder's latent queries) keep one: there the two serial sweeps of one workgroup cost more than the halved
-    // planes save. SVAE_BWD8_SUB=1: one everywhere (A/B runs)
-    static const int sub_env = [] { const char* e = getenv("SVAE_BWD8_SUB"); return e && atoi(e) == 1 ? 1 : 2; }();
-    const int nsub = sub_env == 2 && d->Lq >= 512 ? 2 : 1;
+  const bool use8 = bwd8_env && d->hd <= 96 && !smallq;
+  // two 256-key sub-blocks per workgroup and dQ plane for >= 512 queries; fewer query tiles per key block (the
+  // encoder's latent queries) keep one: there the two serial sweeps of one workgroup cost more than the halved
+  // planes save. SVAE_BWD8_SUB=1: one everywhere (A/B runs)
+  static const int sub_env = [] { const char* e = getenv("SVAE_BWD8_SUB"); return e && atoi(e) == 1 ? 1 : 2; }();
+  const int nsub = sub_env == 2 && d->Lq >= 512 ? 2 : 1;
+  if (use8) {
     p.kblk = BWD8_KEYS * nsub;
     // causal: attn_bwd8 stores the final dQ of the queries below dq_direct itself (hd 96: key block 0's, < 256;
     // hd 64 with two sub-blocks: plane 0's, < 512)
@@ -2351,6 +2418,19 @@ SVAE_EXPORT int svae_attn_bwd(const svae_attn_desc* d, svae_stream_t stream) {
         p.cls_part = d->dq_part + (long long)((d->Lk + BWD_KEYS - 1) / BWD_KEYS) * d->B * d->Lq * d->H * d->hd;
       }
     }
+    // in-kernel delta (SVAE_ATTN_DELTA_INKERNEL=0: the separate pass, A/B runs): the 8-wave kernel at hd <= 64 reads O
+    // and o_lo itself; not with the [CLS] split (attn_bwd_cls_kernel reads delta from memory)
+    static const int dik_env = [] { const char* e = getenv("SVAE_ATTN_DELTA_INKERNEL"); return e ? atoi(e) : 1; }();
+    if (dik_env && d->hd <= 64 && !d->delta_ready && d->o_lo && p.cls_q0 == 0 &&
+        ((long long)d->Lq + 64) * std::max(d->so, d->so_lo) * 2 < 0x7FFFFFF0LL)
+      p.delta_inkernel = 1;
+  }
+  // delta_ready: the dO GEMM's epilogue already wrote delta (svae_gemm_desc.delta)
+  if (!d->delta_ready && !p.delta_inkernel) {
+    if (d->hd <= 64) hipLaunchKernelGGL(attn_delta_kernel<8>, dim3((rows + 31) / 32), dim3(256), 0, s, p);
+    else hipLaunchKernelGGL(attn_delta_kernel<16>, dim3((rows + 15) / 16), dim3(256), 0, s, p);
+  }
+  if (use8) {
     dim3 grid8((d->Lk + p.kblk - 1) / p.kblk, d->H, d->B);
     if (d->hd <= 64) {
       if (nsub == 2) hipLaunchKernelGGL((attn_bwd8_kernel<64, 2>), grid8, dim3(512), 0, s, p);

@@ -4,6 +4,7 @@ tests/test_oracle_golden.py. Tolerances: loss/ELBO 1e-3 rel (BASELINE.json north
 rel (the posterior comes out of the bf16 encoder), every parameter gradient cosine >= 0.995 and norm ratio
 within 2 %. c4shape is the C4/C5 model (12 layers, d768, decoder hd 96 on the hd-128 kernels, encoder 12 x 64,
 L=1024)."""
+import json
 import os
 
 import numpy as np
@@ -39,17 +40,43 @@ def _grad_report(flat, p):
     return worst
 
 
-def _grad_bars(worst, msg):
-    """Every parameter: cosine >= 0.995. Norm ratio within 2 % for every weight matrix; within 5 % for the 1-D
-    parameters (biases, LayerNorm affine, learned queries): the key-projection bias gradient is a cancellation
-    residual (softmax is invariant to a bias added to every key up to the rotary phase), so its bf16 relative
-    error runs a few times the matrices' (measured 2.7 % at the C2 model with the sliding window, at cosine
-    0.9996)."""
+def _noise_floor(name):
+    """Per-parameter bf16 noise floor of the gradient norm ratio at a golden configuration (tests/golden/
+    noise_floor_<name>.json, written by scripts/noise_floor.py on CPU: the oracle with every matmul operand rounded to
+    bf16 -- round-to-nearest and 8 stochastic-rounding draws -- against the fp64 oracle; std of the norm ratio over the 9
+    draws). {} when the configuration has none."""
+    f = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden', f'noise_floor_{name}.json')
+    if not os.path.exists(f):
+        return {}
+    with open(f) as fh:
+        return {k: v[0] for k, v in json.load(fh)['ratio_std_maxdev_mincos'].items()}
+
+
+NOISE_MULT = 4.0   # the bar's multiple of the bf16 noise floor (4 sigma: ~1e-4 false alarms per parameter)
+
+
+def _grad_bars(worst, msg, name=None):
+    """Every parameter: cosine >= 0.995. Norm ratio within max(base, 4 sigma_bf16): base 2 % for every weight matrix,
+    5 % for the 1-D parameters (biases, LayerNorm affine, learned queries: the key-projection bias gradient is a
+    cancellation residual -- softmax is invariant to a bias added to every key up to the rotary phase); sigma_bf16 the
+    parameter's measured bf16 noise floor at this configuration (_noise_floor). The encoder's self-attention over its
+    64 latents (nearly alike keys) is where that floor lies above the base: q / k gradients at 1.0-2.0 % sigma at the
+    C2 / C4 shapes (tests/golden/noise_floor_*.json; a correct bf16 emulation strays up to 4.4 % there), so a 2 % bar
+    could not tell a regression from rounding."""
     assert worst[0][0] >= 0.995, msg
+    floor = _noise_floor(name) if name else {}
+    zs = []
     for c, r, n in worst:
-        tol = 0.05 if (n.endswith('bias') or 'layer_norm' in n or n.startswith('output_layer.2.')
-                       or n.endswith('learned_queries')) else 0.02
-        assert abs(r - 1.0) < tol, f'{n}: norm ratio {r:.4f}\n' + msg
+        base = 0.05 if (n.endswith('bias') or 'layer_norm' in n or n.startswith('output_layer.2.')
+                        or n.endswith('learned_queries')) else 0.02
+        sig = floor.get(n, 0.0)
+        tol = max(base, NOISE_MULT * sig)
+        if sig > 0:
+            zs.append((r - 1.0) / sig)
+        assert abs(r - 1.0) < tol, f'{n}: norm ratio {r:.4f} (bar {tol:.4f}, bf16 sigma {sig:.4f})\n' + msg
+    if zs:
+        print(f'norm-ratio deviations in units of the bf16 noise floor: rms {float(np.sqrt(np.mean(np.square(zs)))):.2f}'
+              f', max |z| {float(np.max(np.abs(zs))):.2f} over {len(zs)} parameters')
 
 
 @pytest.mark.parametrize('name,chunk_numel,fuse_ln', [('tiny_pad', None, False), ('small6_pad', None, False),
@@ -102,7 +129,7 @@ def test_step_matches_oracle(name, chunk_numel, fuse_ln, monkeypatch):
     worst = _grad_report(flat, p)
     msg = '\n'.join(f'{c:.5f} {r:.4f} {n}' for c, r, n in worst[:8])
     print(f'[{name} {chunk_numel} fuse_ln={fuse_ln}] loss {loss:.6f} ref {ref["loss"].item():.6f} kl {kl:.6f} ref {ref["kl"].item():.6f}\n' + msg)
-    _grad_bars(worst, msg)
+    _grad_bars(worst, msg, name)
 
 
 @pytest.mark.parametrize('name,window', [('tiny_pad', 1), ('small6_pad', 2), ('c2shape', 4)])
@@ -135,7 +162,7 @@ def test_sparse_step_matches_oracle(name, window):
     worst = _grad_report(flat, p)
     msg = '\n'.join(f'{c:.5f} {r:.4f} {n}' for c, r, n in worst[:8])
     print(f'[{name} w{window}] loss {loss:.6f} ref {ref["loss"].item():.6f}\n' + msg)
-    _grad_bars(worst, msg)
+    _grad_bars(worst, msg, name)
 
 
 @pytest.mark.parametrize('name', ['tiny_pad', 'small6_pad', 'c2shape'])

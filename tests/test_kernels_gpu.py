@@ -708,10 +708,11 @@ def test_attention_bwd_row_constant_slots_repeatable(hd, L, causal):
     assert _rel(dv, unheads(vr.grad)) < 2e-2
 
 
-@pytest.mark.parametrize('hd,L', [(64, 512), (96, 1024), (32, 130)])
+@pytest.mark.parametrize('hd,L', [(64, 512), (96, 1024), (32, 130), (64, 1100), (64, 300)])
 def test_attention_o_lo_matches_o32(hd, L):
-    """The forward's bf16 residual o_lo = O - bf16(O) carries the f32 O to ~16 bits: the delta pass from (O, o_lo)
-    gives the backward of the f32 copy o32 to ~1e-5."""
+    """The forward's bf16 residual o_lo = O - bf16(O) carries the f32 O to ~16 bits: delta from (O, o_lo) -- the
+    separate pass, or at hd <= 64 computed inside the 8-wave backward from LDS-DMA'd O / o_lo rows -- gives the
+    backward of the f32 copy o32 to ~1e-5."""
     torch.manual_seed(hd * 3 + L)
     B, H = 2, 3
     d = H * hd
