@@ -46,6 +46,8 @@ CONFIGS = {
     'c2s': dict(layers=6, d=512, heads=8, L=512, B=64, window=4),
     # the same model and tokens per batch at the sparse presets' sequence lengths (hparam_presets.py:122-171): 2 x 16384
     'c2s16k': dict(layers=6, d=512, heads=8, L=16384, B=2, window=4),
+    # the pg19 preset's shape (hparam_presets.py:150-171: one 102,400-token sample per batch, attn_window_size 6)
+    'c2s100k': dict(layers=6, d=512, heads=8, L=102400, B=1, window=6),
 }
 V, NLAT = 32768, 64
 PEAK_BF16_TFLOPS = 2500.0      # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, chip-level parameters)

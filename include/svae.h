@@ -212,8 +212,12 @@ typedef struct svae_attn_desc {
 
 int svae_attn_fwd(const svae_attn_desc* d, svae_stream_t stream);
 int svae_attn_bwd(const svae_attn_desc* d, svae_stream_t stream);
-/* floats of the dq_part workspace: ceil(Lk / 128) * B * Lq * H * hd */
+/* floats of the dq_part workspace: ceil(Lk / 128) * B * Lq * H * hd (+ the sliding window's [CLS] slabs) -- enough for
+   every mode */
 int64_t svae_attn_dq_part_elems(int32_t B, int32_t H, int32_t Lq, int32_t Lk, int32_t hd);
+/* the same for a given sliding window (0 = dense): in window mode the 8-wave backward keeps dQ planes >= 1 to their
+   band's rows, O(Lq) floats instead of O(Lq^2 / 512) (2 x 16384 tokens at hd 64: 36 MB instead of 8.6 GB) */
+int64_t svae_attn_dq_part_elems_w(int32_t B, int32_t H, int32_t Lq, int32_t Lk, int32_t hd, int32_t window);
 /* dq f32 [rows][H*hd] -> bf16 out (row stride ldo) with optional inverse rotary (pos = row % seq). */
 int svae_dq_finalize(const float* dq, void* out, int64_t ldo, int32_t rows, int32_t D, const float* rot_tab,
                      int32_t seq, svae_stream_t stream);

@@ -50,7 +50,20 @@ struct AP {
   float* cls_part;
   // backward (attn_bwd8, hd <= 64, o_lo given): delta = rowsum(dO . O) computed inside the kernel (no attn_delta_kernel)
   int delta_inkernel;
+  // backward, sliding window on the attn_bwd8 path: dQ planes pk >= 1 hold only their band's wrows query rows
+  // (queries pk kblk .. + wrows - 1), after plane 0's B x Lq rows: O(L) instead of O(L^2 / kblk) floats. 0 = dense.
+  int wrows;
 };
+
+// Start of the (batch b) partial dQ of plane pk, indexed by ABSOLUTE query row: plane 0 and the dense layout [pk][B][Lq][D];
+// the window's compact planes [pk - 1][B][wrows][D] after plane 0 (rows pk kblk .. ; the returned base is offset back by
+// pk kblk rows, so base + q D addresses query q of the band)
+__device__ __forceinline__ float* dq_plane(const AP& p, int pk, int b) {
+  const long long D = (long long)p.H * p.hd;
+  if (p.wrows > 0 && pk > 0)
+    return p.dq_part + (long long)p.B * p.Lq * D + ((long long)(pk - 1) * p.B + b) * p.wrows * D - (long long)pk * p.kblk * D;
+  return p.dq_part + ((long long)pk * p.B + b) * p.Lq * D;
+}
 
 // Block-sparse sliding window of SparseAttention (sparse_attention.py:39-60, causal, block 32): query q sees
 // key k <= q iff k < 32 (the [CLS] block, layout[:, 0] = 1) or k / 32 >= q / 32 - (window - 1).
@@ -1587,7 +1600,7 @@ __device__ __forceinline__ void attn_bwd8_tile(const AP& p, char* smem, int kb, 
   const int nqt_prev = !rmw ? 0
                        : (((p.window > 0 && k0 - BWD8_KEYS > 0)
                                ? min(p.Lq, k0 - SBLK + SBLK * p.window) : p.Lq) + 63) >> 6;
-  float* part = p.dq_part + ((long long)pk * p.B + b) * p.Lq * p.H * p.hd + (long long)h * p.hd;
+  float* part = dq_plane(p, pk, b) + (long long)h * p.hd;
   const long long ldp = (long long)p.H * p.hd;
   const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc((void*)part, 0, 0x7FFFFFF0, 0x00020000);
   // final dQ of the direct tiles (see the dQ stores): row 0 of this (batch, head) in dq_bf (bf16) or dq (f32)
@@ -2292,6 +2305,10 @@ __global__ __launch_bounds__(256) void attn_dq_reduce_kernel(AP p) {
   const float* src = p.dq_part + (long long)row * D + 4 * c4;
   f32x4 acc = *(const f32x4*)src;
   int k = k1;
+  if (p.wrows > 0) {   // the window's compact planes (a query sees at most a few)
+    for (; k < nk; ++k) acc += *(const f32x4*)(dq_plane(p, k, b) + (long long)q * D + 4 * c4);
+    k = nk;
+  }
   for (; k + 4 <= nk; k += 4) {
     const f32x4 v0 = *(const f32x4*)(src + k * plane), v1 = *(const f32x4*)(src + (k + 1) * plane);
     const f32x4 v2 = *(const f32x4*)(src + (k + 2) * plane), v3 = *(const f32x4*)(src + (k + 3) * plane);
@@ -2341,9 +2358,56 @@ bool fill(const svae_attn_desc* d, AP& p) {
   p.cls_q0 = 0;
   p.cls_part = nullptr;
   p.delta_inkernel = 0;
+  p.wrows = 0;
   if (p.window < 0 || (p.window > 0 && !p.causal)) return false;
   if (p.o32 && ((p.so32 | p.bo32) % 4)) return false;
   return true;
+}
+
+// The backward's kernel choice and dQ-partial layout for a shape (svae_attn_bwd and the workspace-size queries agree on
+// it). hd <= 96: the 8-wave 256-key kernel, two 256-key sub-blocks per dQ plane from 512 queries on; hd 128 and the
+// encoder's <= 64 latent queries at hd <= 64: the 4-wave 128-key one. Environment switches (A/B runs only):
+// SVAE_ATTN_BWD8=0 (the 4-wave kernels everywhere), SVAE_ATTN_BWD_SMALLQ=0 (the 8-wave kernel for <= 64 queries too),
+// SVAE_BWD8_SUB=1 (one sub-block per plane), SVAE_ATTN_WINDOW_COMPACT=0 (dense planes in window mode).
+struct BwdLayout {
+  bool use8;
+  int nsub, kblk, wrows;
+  long long plane_elems;   // floats of the dQ partial planes (the [CLS] slabs follow them)
+};
+BwdLayout bwd_layout(int B, int H, int Lq, int Lk, int hd, bool causal, int window) {
+  static const int bwd8_env = [] { const char* e = getenv("SVAE_ATTN_BWD8"); return e ? atoi(e) : 1; }();
+  // one query tile (the encoder's 64 latent / learned queries) at hd <= 64: the 4-wave 128-key kernel, two workgroups
+  // per CU, hides more of the per-workgroup prologue / epilogue that such a sweep is made of (C2 encoder shape 64 -> 58
+  // us, C4's 180 -> 171 us: profiles/r05enc_attn_bwd_smallq_probe.log)
+  static const int smallq_env = [] { const char* e = getenv("SVAE_ATTN_BWD_SMALLQ"); return e ? atoi(e) : 1; }();
+  // two 256-key sub-blocks per workgroup and dQ plane for >= 512 queries; fewer query tiles per key block (the
+  // encoder's latent queries) keep one: there the two serial sweeps of one workgroup cost more than the halved planes
+  static const int sub_env = [] { const char* e = getenv("SVAE_BWD8_SUB"); return e && atoi(e) == 1 ? 1 : 2; }();
+  static const int compact_env = [] { const char* e = getenv("SVAE_ATTN_WINDOW_COMPACT"); return e ? atoi(e) : 1; }();
+  BwdLayout l;
+  l.use8 = bwd8_env && hd <= 96 && !(smallq_env && Lq <= 64 && hd <= 64);
+  l.nsub = l.use8 && sub_env == 2 && Lq >= 512 ? 2 : 1;
+  l.kblk = l.use8 ? BWD8_KEYS * l.nsub : BWD_KEYS;
+  const long long D = (long long)H * hd;
+  l.wrows = 0;
+  l.plane_elems = (long long)((Lk + BWD_KEYS - 1) / BWD_KEYS) * B * Lq * D;   // dense: the 128-key planes (either kernel)
+  if (l.use8 && window > 0 && causal && compact_env) {
+    // a plane's band: its keys pk kblk .. + kblk - 1 are seen by queries up to pk kblk + kblk - 32 + 32 window (whole
+    // query tiles); plane 0 keeps every row (the [CLS] keys are seen by all queries)
+    const int R = (std::min(Lq, l.kblk - SBLK + SBLK * window) + 63) / 64 * 64;
+    const int np = (Lk + l.kblk - 1) / l.kblk;
+    if (np > 1 && R < Lq) {
+      l.wrows = R;
+      l.plane_elems = (long long)B * Lq * D + (long long)(np - 1) * B * R * D;
+    }
+  }
+  return l;
+}
+
+// floats of the [CLS] split's dK / dV slabs: at most 1 + 4 ceil(tiles / (4 CLS_TW)) of [2][B][32][H hd]
+long long cls_slab_elems(int B, int H, int Lq, int hd) {
+  const long long nslab = 1 + 4 * (((Lq + 63) / 64 + 4 * CLS_TW - 1) / (4 * CLS_TW));
+  return nslab * 2 * B * 32 * H * hd;
 }
 
 }  // namespace
@@ -2387,24 +2451,14 @@ SVAE_EXPORT int svae_attn_bwd(const svae_attn_desc* d, svae_stream_t stream) {
   if (((long long)std::max(d->Lq, d->Lk) + 64) * std::max(std::max(d->sq, d->sk), d->sdo) * 2 > 0x7FFFFFF0LL) return SVAE_EINVAL;
   hipStream_t s = (hipStream_t)stream;
   const int rows = d->B * d->Lq * d->H;
-  // hd <= 96: the 8-wave 256-key kernel; hd 128: the 4-wave 128-key one (its LDS rows do not fit the 8-wave layout).
-  // SVAE_ATTN_BWD8=0: the 4-wave kernels for every hd (A/B runs)
-  static const int bwd8_env = [] { const char* e = getenv("SVAE_ATTN_BWD8"); return e ? atoi(e) : 1; }();
+  const BwdLayout lay = bwd_layout(d->B, d->H, d->Lq, d->Lk, d->hd, d->causal != 0, d->window);
+  const bool use8 = lay.use8;
+  const int nsub = lay.nsub;
   // SVAE_ATTN_DQ_DIRECT=0: every query tile through the partial planes (A/B runs)
   static const int direct_env = [] { const char* e = getenv("SVAE_ATTN_DQ_DIRECT"); return e ? atoi(e) : 1; }();
-  // one query tile (the encoder's 64 latent / learned queries) at hd <= 64: the 4-wave 128-key kernel, two workgroups per
-  // CU, hides more of the per-workgroup prologue / epilogue that such a sweep is made of (C2 encoder shape 64 -> 58 us,
-  // C4's 180 -> 171 us: profiles/r05enc_attn_bwd_smallq_probe.log). SVAE_ATTN_BWD_SMALLQ=0: the 8-wave kernel there too
-  static const int smallq_env = [] { const char* e = getenv("SVAE_ATTN_BWD_SMALLQ"); return e ? atoi(e) : 1; }();
-  const bool smallq = smallq_env && d->Lq <= 64 && d->hd <= 64;
-  const bool use8 = bwd8_env && d->hd <= 96 && !smallq;
-  // two 256-key sub-blocks per workgroup and dQ plane for >= 512 queries; fewer query tiles per key block (the
-  // encoder's latent queries) keep one: there the two serial sweeps of one workgroup cost more than the halved
-  // planes save. SVAE_BWD8_SUB=1: one everywhere (A/B runs)
-  static const int sub_env = [] { const char* e = getenv("SVAE_BWD8_SUB"); return e && atoi(e) == 1 ? 1 : 2; }();
-  const int nsub = sub_env == 2 && d->Lq >= 512 ? 2 : 1;
   if (use8) {
-    p.kblk = BWD8_KEYS * nsub;
+    p.kblk = lay.kblk;
+    p.wrows = lay.wrows;
     // causal: attn_bwd8 stores the final dQ of the queries below dq_direct itself (hd 96: key block 0's, < 256;
     // hd 64 with two sub-blocks: plane 0's, < 512)
     p.dq_direct = (d->causal && direct_env) ? (nsub == 2 && d->hd <= 64 ? 2 : 1) * BWD8_KEYS : 0;
@@ -2415,7 +2469,7 @@ SVAE_EXPORT int svae_attn_bwd(const svae_attn_desc* d, svae_stream_t stream) {
       const int q0 = (std::min(d->Lq, p.kblk - SBLK + SBLK * d->window) + 63) / 64 * 64;
       if (q0 < d->Lq) {
         p.cls_q0 = q0;
-        p.cls_part = d->dq_part + (long long)((d->Lk + BWD_KEYS - 1) / BWD_KEYS) * d->B * d->Lq * d->H * d->hd;
+        p.cls_part = d->dq_part + lay.plane_elems;
       }
     }
     // in-kernel delta (SVAE_ATTN_DELTA_INKERNEL=0: the separate pass, A/B runs): the 8-wave kernel at hd <= 64 reads O
@@ -2464,10 +2518,13 @@ SVAE_EXPORT int svae_attn_bwd(const svae_attn_desc* d, svae_stream_t stream) {
 
 SVAE_EXPORT int64_t svae_attn_dq_part_elems(int32_t B, int32_t H, int32_t Lq, int32_t Lk, int32_t hd) {
   if (B <= 0 || H <= 0 || Lq <= 0 || Lk <= 0 || hd <= 0) return 0;
-  // + the sliding window's [CLS] dK / dV slabs (attn_bwd_cls_kernel): at most 1 + 4 ceil(tiles / (4 CLS_TW)) of
-  // [2][B][32][H hd]
-  const int64_t nslab = 1 + 4 * (((Lq + 63) / 64 + 4 * CLS_TW - 1) / (4 * CLS_TW));
-  return (int64_t)((Lk + BWD_KEYS - 1) / BWD_KEYS) * B * Lq * H * hd + nslab * 2 * B * 32 * H * hd;
+  // the dense planes (enough for any mode) + the sliding window's [CLS] dK / dV slabs (attn_bwd_cls_kernel)
+  return (int64_t)((Lk + BWD_KEYS - 1) / BWD_KEYS) * B * Lq * H * hd + cls_slab_elems(B, H, Lq, hd);
+}
+
+SVAE_EXPORT int64_t svae_attn_dq_part_elems_w(int32_t B, int32_t H, int32_t Lq, int32_t Lk, int32_t hd, int32_t window) {
+  if (B <= 0 || H <= 0 || Lq <= 0 || Lk <= 0 || hd <= 0 || window < 0) return 0;
+  return bwd_layout(B, H, Lq, Lk, hd, window > 0, window).plane_elems + cls_slab_elems(B, H, Lq, hd);
 }
 
 #ifdef SVAE_STAMPS

@@ -103,6 +103,7 @@ _SIGS = {
     'svae_attn_fwd': [ctypes.POINTER(AttnDesc), c_void_p],
     'svae_attn_bwd': [ctypes.POINTER(AttnDesc), c_void_p],
     'svae_attn_dq_part_elems': [c_int32, c_int32, c_int32, c_int32, c_int32],
+    'svae_attn_dq_part_elems_w': [c_int32, c_int32, c_int32, c_int32, c_int32, c_int32],
     'svae_transpose_blocks': [c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p],
     'svae_dq_finalize': [c_void_p, c_void_p, c_int64, c_int32, c_int32, c_void_p, c_int32, c_void_p],
     'svae_embedding_fwd': [c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p],
@@ -175,7 +176,8 @@ def _load():
     for name, argtypes in _SIGS.items():
         fn = getattr(lib, name)
         fn.argtypes = argtypes
-        fn.restype = {'svae_version': ctypes.c_char_p, 'svae_attn_dq_part_elems': c_int64}.get(name, ctypes.c_int)
+        fn.restype = {'svae_version': ctypes.c_char_p, 'svae_attn_dq_part_elems': c_int64,
+                      'svae_attn_dq_part_elems_w': c_int64}.get(name, ctypes.c_int)
     return lib
 
 

@@ -527,9 +527,10 @@ class VAEEngine:
             return dict(o32=self.ws.get(tag + '32', (rows_q, d), f32), so32=d, bo32=Lq * d)
         return dict(o_lo=self.ws.get(tag + 'lo', (rows_q, d)), so_lo=d, bo_lo=Lq * d)
 
-    def _dq_part(self, B, H, Lq, Lk, hd):
-        """f32 workspace for the attention backward's per-key-block dQ partials (shared by all layers)."""
-        n = K.attn_dq_part_elems(B, H, Lq, Lk, hd)
+    def _dq_part(self, B, H, Lq, Lk, hd, window=0):
+        """f32 workspace for the attention backward's per-key-block dQ partials (shared by all layers; window mode: the
+        compact band planes, O(L) instead of O(L^2)))."""
+        n = K.attn_dq_part_elems(B, H, Lq, Lk, hd, window)
         t = self.ws.bufs.get('b.dqpart')
         return t if t is not None and t.numel() >= n else self.ws.get('b.dqpart', (n,), f32)
 
@@ -622,7 +623,7 @@ class VAEEngine:
                         sdo=d, bdo=Lq * d,
                         delta=delta, delta_ready=self.delta_fused, dq_bf=dqkv, ldq_bf=3 * d, dk=dqkv[:, d:], dv=dqkv[:, 2 * d:], sdk=3 * d,
                         sdv=3 * d, bdk=Sx * 3 * d, bdv=Sx * 3 * d, rot=rot, rot_d=d, **st['Ox'],
-                        dq_part=self._dq_part(B, heads, Lq, Sx, hd))
+                        dq_part=self._dq_part(B, heads, Lq, Sx, hd, st['window']))
             self._dw_pair(wo_dw, (dqkv, st['h'], a + 'q_linear.weight', rows_x, 3 * d, d, None, None,
                                   a + 'q_linear.bias'))
             dh = ws.get('b.dh', (rows_x, d))

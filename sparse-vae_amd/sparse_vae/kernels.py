@@ -290,8 +290,8 @@ def attention(q, k, v, o, lse, *, B, H, Lq, Lk, hd, sq, sk, sv, so, bq, bk, bv, 
         d.dk, d.dv, d.sdk, d.sdv, d.bdk, d.bdv = dk.data_ptr(), dv.data_ptr(), sdk, sdv, bdk, bdv
         d.rot_tab, d.rot_d = ptr(rot), rot_d
         if dq_part is None:
-            dq_part = torch.empty(attn_dq_part_elems(B, H, Lq, Lk, hd), device=q.device, dtype=torch.float32)
-        assert dq_part.numel() >= attn_dq_part_elems(B, H, Lq, Lk, hd) and dq_part.dtype == torch.float32
+            dq_part = torch.empty(attn_dq_part_elems(B, H, Lq, Lk, hd, window), device=q.device, dtype=torch.float32)
+        assert dq_part.numel() >= attn_dq_part_elems(B, H, Lq, Lk, hd, window) and dq_part.dtype == torch.float32
         d.dq_part, d.dq_bf, d.ldq_bf = dq_part.data_ptr(), ptr(dq_bf), ldq_bf
         d.dq = ptr(dq)
         check(lib.svae_attn_bwd(ctypes.byref(d), stream()), 'svae_attn_bwd')
@@ -300,8 +300,10 @@ def attention(q, k, v, o, lse, *, B, H, Lq, Lk, hd, sq, sk, sv, so, bq, bk, bv, 
         check(lib.svae_attn_fwd(ctypes.byref(d), stream()), 'svae_attn_fwd')
 
 
-def attn_dq_part_elems(B, H, Lq, Lk, hd):
-    return lib.svae_attn_dq_part_elems(B, H, Lq, Lk, hd)
+def attn_dq_part_elems(B, H, Lq, Lk, hd, window=0):
+    """Floats of the backward's dQ-partial workspace for this shape (window > 0: the sliding window's compact band
+    planes)."""
+    return lib.svae_attn_dq_part_elems_w(B, H, Lq, Lk, hd, int(window))
 
 
 def dq_finalize(dq, out, ldo, rows, D, rot=None, seq=0):
