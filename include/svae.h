@@ -208,9 +208,16 @@ typedef struct svae_attn_desc {
      O to ~16 significant bits, where the f32-accumulated O itself carries ~19 */
   void* o_lo;
   int64_t so_lo, bo_lo;
+  /* forward, few queries over many keys (<= 128 queries, non-causal, >= 2048 keys, < 128 query tiles in all): optional
+     f32 workspace of svae_attn_fwd_ws_elems floats (16-B aligned); when given, the keys are cut into slices run as
+     separate problems and combined (split-KV), so a long key sequence fills the chip. NULL: one pass. */
+  float* fwd_ws;
+  int64_t fwd_ws_elems;
 } svae_attn_desc;
 
 int svae_attn_fwd(const svae_attn_desc* d, svae_stream_t stream);
+/* floats of the split-KV forward's workspace for a shape (0: that shape runs in one pass) */
+int64_t svae_attn_fwd_ws_elems(int32_t B, int32_t H, int32_t Lq, int32_t Lk, int32_t hd, int32_t causal, int32_t window);
 int svae_attn_bwd(const svae_attn_desc* d, svae_stream_t stream);
 /* floats of the dq_part workspace: ceil(Lk / 128) * B * Lq * H * hd (+ the sliding window's [CLS] slabs) -- enough for
    every mode */

@@ -27,7 +27,7 @@ namespace {
 struct AP {
   const bf16* q; const bf16* k; const bf16* v; bf16* o;
   long long sq, sk, sv, so, bq, bk, bv, bo;
-  const unsigned char* pad;
+  const unsigned char* pad; long long ldpad;   // key_pad [B][ldpad] (a key slice of a longer row: ldpad > Lk)
   float* lse;
   int B, H, Lq, Lk, hd, causal;
   float scale;
@@ -332,7 +332,7 @@ __device__ __forceinline__ void attn_fwd_tile(const AP& p, char* smem, int bx, i
   const bf16* Q = p.q + b * p.bq + (long long)h * p.hd;
   const bf16* K = p.k + b * p.bk + (long long)h * p.hd;
   const bf16* V = p.v + b * p.bv + (long long)h * p.hd;
-  const unsigned char* pad = p.pad ? p.pad + (long long)b * p.Lk : nullptr;
+  const unsigned char* pad = p.pad ? p.pad + b * p.ldpad : nullptr;
   // key-padding ring: one dword per key (LDS-DMA writes a dword slot per lane; the byte is its low 8 bits), one ring
   // per wave ([wave][NS][64]): every wave DMAs the bytes it reads itself (no wave reads another wave's DMA)
   unsigned* pm = (unsigned*)(smem + NS * 2 * T::BYTES);
@@ -692,7 +692,7 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd32_kernel(AP p) {
   }
   // key padding as a bit mask in LDS (bit k of word k / 64), built once per block by ballots: plain loads, read after
   // the first tile's barrier (no per-tile DMA ring, no wave reading another wave's DMA)
-  const unsigned char* pad = p.pad ? p.pad + (long long)b * p.Lk : nullptr;
+  const unsigned char* pad = p.pad ? p.pad + b * p.ldpad : nullptr;
   unsigned long long* pbits = (unsigned long long*)(smem + NS * 2 * I::BYTES);
   if (pad) {
     for (int k0 = 64 * w; k0 < p.Lk; k0 += 256) {
@@ -1040,7 +1040,7 @@ __device__ __forceinline__ void attn_bwd_tile(const AP& p, char* smem, int kb, i
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int key = kw + 16 * j + li;
-    key_ok[j] = key < p.Lk && !(p.pad && p.pad[(long long)b * p.Lk + key]);
+    key_ok[j] = key < p.Lk && !(p.pad && p.pad[b * p.ldpad + key]);
 #pragma unroll
     for (int kk = 0; kk < NKK; ++kk) {
       const int d = 32 * kk + 8 * g;
@@ -1285,7 +1285,7 @@ __device__ __forceinline__ void attn_bwd_tile_wide(const AP& p, char* smem, int 
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int key = kw + 16 * j + li;
-    key_ok[j] = key < p.Lk && !(p.pad && p.pad[(long long)b * p.Lk + key]);
+    key_ok[j] = key < p.Lk && !(p.pad && p.pad[b * p.ldpad + key]);
 #pragma unroll
     for (int kk = 0; kk < NKK; ++kk) {
       const int d = 32 * kk + 8 * g;
@@ -1560,7 +1560,7 @@ __device__ __forceinline__ void attn_bwd8_tile(const AP& p, char* smem, int kb, 
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int key = kw + 16 * j + li;
-    key_ok[j] = key < p.Lk && !(p.pad && p.pad[(long long)b * p.Lk + key]);
+    key_ok[j] = key < p.Lk && !(p.pad && p.pad[b * p.ldpad + key]);
 #pragma unroll
     for (int kk = 0; kk < NKK; ++kk) {
       const int d = 32 * kk + 8 * g;
@@ -2107,7 +2107,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_cls_kernel(AP p) {
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int key = 16 * j + li;
-    key_ok[j] = key < nk && !(p.pad && p.pad[(long long)b * p.Lk + key]);
+    key_ok[j] = key < nk && !(p.pad && p.pad[b * p.ldpad + key]);
 #pragma unroll
     for (int kk = 0; kk < NKK; ++kk) {
       const int d = 32 * kk + 8 * g;
@@ -2341,7 +2341,7 @@ bool fill(const svae_attn_desc* d, AP& p) {
   p.q = (const bf16*)d->q; p.k = (const bf16*)d->k; p.v = (const bf16*)d->v; p.o = (bf16*)d->o;
   p.sq = d->sq; p.sk = d->sk; p.sv = d->sv; p.so = d->so;
   p.bq = d->bq; p.bk = d->bk; p.bv = d->bv; p.bo = d->bo;
-  p.pad = d->key_pad; p.lse = d->lse;
+  p.pad = d->key_pad; p.ldpad = d->Lk; p.lse = d->lse;
   p.B = d->B; p.H = d->H; p.Lq = d->Lq; p.Lk = d->Lk; p.hd = d->hd; p.causal = d->causal;
   p.scale = d->scale;
   p.dout = (const bf16*)d->dout; p.sdo = d->sdo; p.bdo = d->bdo;
@@ -2412,27 +2412,135 @@ long long cls_slab_elems(int B, int H, int Lq, int hd) {
 
 }  // namespace
 
+namespace {
+
+// the forward's kernel choice for the (possibly key-sliced) problem p
+void launch_fwd(const AP& p, hipStream_t s) {
+  dim3 grid((p.Lq + 127) / 128, p.H, p.B);
+  // the 32x32-MFMA kernel for hd <= 64 (hd 96 spilled; SVAE_ATTN_FWD32=0: the 16x16 kernels, for A/B runs); its padding
+  // bit mask holds FWD32_MAXPAD keys and its DMA / store offsets are 32-bit byte offsets from a sequence's row 0
+  static const int fwd32_env = [] { const char* e = getenv("SVAE_ATTN_FWD32"); return e ? atoi(e) : 1; }();
+  static const int occ_env = [] { const char* e = getenv("SVAE_ATTN_FWD32_OCC"); return e ? atoi(e) : 3; }();
+  static const int ns_env = [] { const char* e = getenv("SVAE_ATTN_FWD32_NS"); return e ? atoi(e) : 2; }();
+  const bool fit32 = ((long long)p.Lk + 64) * std::max(p.sk, p.sv) * 2 < 0x7FFFFFF0LL &&
+                     ((long long)p.Lq + 128) * p.so * 2 < 0x7FFFFFF0LL && (!p.pad || p.Lk <= FWD32_MAXPAD) &&
+                     (!p.olo || ((long long)p.Lq + 128) * p.solo * 2 < 0x7FFFFFF0LL);   // (o_lo's 32-bit offsets too)
+  if (fwd32_env && fit32 && p.hd <= 64) {
+    if (ns_env == 3) hipLaunchKernelGGL((attn_fwd32_kernel<64, 3, 3>), grid, dim3(256), 0, s, p);
+    else if (occ_env == 4) hipLaunchKernelGGL((attn_fwd32_kernel<64, 4, 2>), grid, dim3(256), 0, s, p);
+    else hipLaunchKernelGGL((attn_fwd32_kernel<64, 3, 2>), grid, dim3(256), 0, s, p);
+  } else if (p.hd <= 64) hipLaunchKernelGGL(attn_fwd_kernel<64>, grid, dim3(256), 0, s, p);
+  else if (p.hd <= 96) hipLaunchKernelGGL((attn_fwd_kernel<128, 96>), grid, dim3(256), 0, s, p);
+  else hipLaunchKernelGGL(attn_fwd_kernel<128>, grid, dim3(256), 0, s, p);
+}
+
+// Split-KV forward for few queries over many keys (the encoder's 64 learned / latent queries against a long sequence:
+// at 2 x 16384 tokens one 128-query tile per (batch, head) gave 16 workgroups for the whole chip, 312 us per launch,
+// profiles/r06i_c2s16k_kernel_summary.txt): the keys are cut into nsplit slices of kc keys, each slice's attention runs
+// as its own problem into the workspace (O in bf16 + its bf16 residual, lse), and this kernel combines them:
+// lse = log sum_s exp(lse_s), O = sum_s exp(lse_s - lse) O_s (a slice whose keys are all padding has lse_s = -inf and no
+// weight). One thread per 4 dims of one (batch, query, head).
+__global__ __launch_bounds__(256) void attn_fwd_combine_kernel(AP p, const bf16* so_hi, const bf16* so_lo,
+                                                              const float* slse, int nsplit) {
+  const int D4 = p.hd / 4;
+  const long long n = (long long)p.B * p.Lq * p.H * D4;
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int c4 = (int)(i % D4);
+  const long long r = i / D4;                 // ((b * Lq + q) * H + h)
+  const int h = (int)(r % p.H), q = (int)((r / p.H) % p.Lq), b = (int)(r / ((long long)p.H * p.Lq));
+  const long long D = (long long)p.H * p.hd;
+  const long long slice_o = (long long)p.B * p.Lq * D, slice_l = (long long)p.B * p.H * p.Lq;
+  const long long lrow = ((long long)b * p.H + h) * p.Lq + q;
+  float m = -INFINITY;
+  for (int sl = 0; sl < nsplit; ++sl) {
+    const float l = slse[sl * slice_l + lrow];
+    if (l > m) m = l;   // (NaN / -inf slices never raise it)
+  }
+  float wsum = 0.f;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  const long long orow = ((long long)b * p.Lq + q) * D + (long long)h * p.hd + 4 * c4;
+  for (int sl = 0; sl < nsplit; ++sl) {
+    const float l = slse[sl * slice_l + lrow];
+    if (!(l > -INFINITY)) continue;           // all-padding slice (or none): no weight, its O is 0 / 0
+    const float wgt = __expf(l - m);
+    const bf16x4 hi = *(const bf16x4*)(so_hi + sl * slice_o + orow), lo = *(const bf16x4*)(so_lo + sl * slice_o + orow);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) acc[e] += wgt * ((float)hi[e] + (float)lo[e]);
+    wsum += wgt;
+  }
+  const float inv = wsum > 0.f ? 1.0f / wsum : 0.f;
+  acc *= inv;
+  const bf16x4 oh = {f2bf(acc[0]), f2bf(acc[1]), f2bf(acc[2]), f2bf(acc[3])};
+  const long long od = (long long)q * p.so + (long long)h * p.hd + 4 * c4;
+  *(bf16x4*)(p.o + b * p.bo + od) = oh;
+  if (p.olo) {
+    const long long ol = (long long)q * p.solo + (long long)h * p.hd + 4 * c4;
+    *(bf16x4*)(p.olo + b * p.bolo + ol) = (bf16x4){f2bf(acc[0] - (float)oh[0]), f2bf(acc[1] - (float)oh[1]),
+                                                   f2bf(acc[2] - (float)oh[2]), f2bf(acc[3] - (float)oh[3])};
+  }
+  if (p.o32) *(f32x4*)(p.o32 + b * p.bo32 + (long long)q * p.so32 + (long long)h * p.hd + 4 * c4) = acc;
+  if (c4 == 0) p.lse[lrow] = m + __logf(wsum);
+}
+
+// the split for a shape: slices of kc keys (a multiple of 64), nsplit of them; 1 = no split
+void fwd_split(int B, int H, int Lq, int Lk, bool causal, int window, int& nsplit, int& kc) {
+  static const int env = [] { const char* e = getenv("SVAE_ATTN_FWD_SPLIT"); return e ? atoi(e) : 1; }();
+  nsplit = 1;
+  kc = Lk;
+  const long long nwg = (long long)((Lq + 127) / 128) * H * B;
+  if (!env || causal || window > 0 || Lq > 128 || nwg >= 128 || Lk < 2048) return;
+  int sp = (int)std::min<long long>((512 + nwg - 1) / nwg, (Lk + 511) / 512);
+  if (sp < 2) return;
+  kc = ((Lk + sp - 1) / sp + 63) / 64 * 64;
+  nsplit = (Lk + kc - 1) / kc;
+}
+
+}  // namespace
+
+SVAE_EXPORT int64_t svae_attn_fwd_ws_elems(int32_t B, int32_t H, int32_t Lq, int32_t Lk, int32_t hd, int32_t causal,
+                                           int32_t window) {
+  if (B <= 0 || H <= 0 || Lq <= 0 || Lk <= 0 || hd <= 0) return 0;
+  int nsplit, kc;
+  fwd_split(B, H, Lq, Lk, causal != 0, window, nsplit, kc);
+  if (nsplit <= 1) return 0;
+  // per slice: O and its residual, bf16 [B][Lq][H hd] each (one float per element for both), lse f32 [B][H][Lq]
+  return (int64_t)nsplit * ((int64_t)B * Lq * H * hd + (int64_t)B * H * Lq);
+}
+
 SVAE_EXPORT int svae_attn_fwd(const svae_attn_desc* d, svae_stream_t stream) {
   AP p;
   if (!fill(d, p)) return SVAE_EINVAL;
   if (d->causal && d->Lq != d->Lk) return SVAE_EINVAL;
-  dim3 grid((d->Lq + 127) / 128, d->H, d->B);
   hipStream_t s = (hipStream_t)stream;
-  // the 32x32-MFMA kernel for hd <= 64 (hd 96 spilled; SVAE_ATTN_FWD32=0: the 16x16 kernels, for A/B runs); its padding bit mask holds
-  // FWD32_MAXPAD keys and its DMA / store offsets are 32-bit byte offsets from a sequence's row 0
-  static const int fwd32_env = [] { const char* e = getenv("SVAE_ATTN_FWD32"); return e ? atoi(e) : 1; }();
-  static const int occ_env = [] { const char* e = getenv("SVAE_ATTN_FWD32_OCC"); return e ? atoi(e) : 3; }();
-  static const int ns_env = [] { const char* e = getenv("SVAE_ATTN_FWD32_NS"); return e ? atoi(e) : 2; }();
-  const bool fit32 = ((long long)d->Lk + 64) * std::max(d->sk, d->sv) * 2 < 0x7FFFFFF0LL &&
-                     ((long long)d->Lq + 128) * d->so * 2 < 0x7FFFFFF0LL && (!d->key_pad || d->Lk <= FWD32_MAXPAD) &&
-                     (!d->o_lo || ((long long)d->Lq + 128) * d->so_lo * 2 < 0x7FFFFFF0LL);   // (o_lo's 32-bit offsets too)
-  if (fwd32_env && fit32 && d->hd <= 64) {
-    if (ns_env == 3) hipLaunchKernelGGL((attn_fwd32_kernel<64, 3, 3>), grid, dim3(256), 0, s, p);
-    else if (occ_env == 4) hipLaunchKernelGGL((attn_fwd32_kernel<64, 4, 2>), grid, dim3(256), 0, s, p);
-    else hipLaunchKernelGGL((attn_fwd32_kernel<64, 3, 2>), grid, dim3(256), 0, s, p);
-  } else if (d->hd <= 64) hipLaunchKernelGGL(attn_fwd_kernel<64>, grid, dim3(256), 0, s, p);
-  else if (d->hd <= 96) hipLaunchKernelGGL((attn_fwd_kernel<128, 96>), grid, dim3(256), 0, s, p);
-  else hipLaunchKernelGGL(attn_fwd_kernel<128>, grid, dim3(256), 0, s, p);
+  int nsplit, kc;
+  fwd_split(d->B, d->H, d->Lq, d->Lk, d->causal != 0, d->window, nsplit, kc);
+  if (nsplit > 1 && d->fwd_ws &&
+      d->fwd_ws_elems >= svae_attn_fwd_ws_elems(d->B, d->H, d->Lq, d->Lk, d->hd, d->causal, d->window) &&
+      !((uintptr_t)d->fwd_ws & 15) && d->hd % 4 == 0) {
+    const long long D = (long long)d->H * d->hd, slice_o = (long long)d->B * d->Lq * D;
+    bf16* ohi = (bf16*)d->fwd_ws;
+    bf16* olo = ohi + (long long)nsplit * slice_o;
+    float* lse = (float*)(olo + (long long)nsplit * slice_o);
+    for (int sl = 0; sl < nsplit; ++sl) {
+      AP q = p;
+      const int k0 = sl * kc;
+      q.k = p.k + (long long)k0 * p.sk;
+      q.v = p.v + (long long)k0 * p.sv;
+      q.Lk = std::min(kc, d->Lk - k0);
+      q.pad = p.pad ? p.pad + k0 : nullptr;   // (ldpad stays the full row)
+      q.o = ohi + sl * slice_o; q.so = D; q.bo = d->Lq * D;
+      q.olo = olo + sl * slice_o; q.solo = D; q.bolo = d->Lq * D;
+      q.o32 = nullptr;
+      q.lse = lse + (long long)sl * d->B * d->H * d->Lq;
+      launch_fwd(q, s);
+    }
+    const long long n = (long long)d->B * d->Lq * d->H * (d->hd / 4);
+    hipLaunchKernelGGL(attn_fwd_combine_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, p, ohi, olo, lse,
+                       nsplit);
+  } else {
+    launch_fwd(p, s);
+  }
   SVAE_LAUNCH_CHECK();
   return SVAE_OK;
 }

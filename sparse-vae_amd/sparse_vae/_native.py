@@ -59,6 +59,7 @@ class AttnDesc(ctypes.Structure):
         ('window', c_int32),
         ('delta_ready', c_int32),
         ('o_lo', c_void_p), ('so_lo', c_int64), ('bo_lo', c_int64),
+        ('fwd_ws', c_void_p), ('fwd_ws_elems', c_int64),
     ]
 
 
@@ -104,6 +105,7 @@ _SIGS = {
     'svae_attn_bwd': [ctypes.POINTER(AttnDesc), c_void_p],
     'svae_attn_dq_part_elems': [c_int32, c_int32, c_int32, c_int32, c_int32],
     'svae_attn_dq_part_elems_w': [c_int32, c_int32, c_int32, c_int32, c_int32, c_int32],
+    'svae_attn_fwd_ws_elems': [c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32],
     'svae_transpose_blocks': [c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p],
     'svae_dq_finalize': [c_void_p, c_void_p, c_int64, c_int32, c_int32, c_void_p, c_int32, c_void_p],
     'svae_embedding_fwd': [c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p],
@@ -177,7 +179,7 @@ def _load():
         fn = getattr(lib, name)
         fn.argtypes = argtypes
         fn.restype = {'svae_version': ctypes.c_char_p, 'svae_attn_dq_part_elems': c_int64,
-                      'svae_attn_dq_part_elems_w': c_int64}.get(name, ctypes.c_int)
+                      'svae_attn_dq_part_elems_w': c_int64, 'svae_attn_fwd_ws_elems': c_int64}.get(name, ctypes.c_int)
     return lib
 
 

@@ -285,6 +285,7 @@ def attention(q, k, v, o, lse, *, B, H, Lq, Lk, hd, sq, sk, sv, so, bq, bk, bv, 
     d.o32, d.so32, d.bo32 = ptr(o32), so32, bo32
     d.o_lo, d.so_lo, d.bo_lo = ptr(o_lo), so_lo, bo_lo
     if backward:
+        d.fwd_ws, d.fwd_ws_elems = None, 0
         d.dout, d.sdo, d.bdo = dout.data_ptr(), sdo, bdo
         d.delta, d.bdq = delta.data_ptr(), bdq
         d.dk, d.dv, d.sdk, d.sdv, d.bdk, d.bdv = dk.data_ptr(), dv.data_ptr(), sdk, sdv, bdk, bdv
@@ -297,7 +298,26 @@ def attention(q, k, v, o, lse, *, B, H, Lq, Lk, hd, sq, sk, sv, so, bq, bk, bv, 
         check(lib.svae_attn_bwd(ctypes.byref(d), stream()), 'svae_attn_bwd')
     else:
         d.dout = None
+        # few queries over a long key sequence: the split-KV workspace (the library decides; 0 floats = one pass)
+        n = lib.svae_attn_fwd_ws_elems(B, H, Lq, Lk, hd, int(causal), int(window))
+        if n > 0:
+            ws = _fwd_workspace(n, q.device)
+            d.fwd_ws, d.fwd_ws_elems = ws.data_ptr(), ws.numel()
+        else:
+            d.fwd_ws, d.fwd_ws_elems = None, 0
         check(lib.svae_attn_fwd(ctypes.byref(d), stream()), 'svae_attn_fwd')
+
+
+_fwd_ws = {}
+
+
+def _fwd_workspace(n, device):
+    """f32 workspace of the split-KV attention forward (grown on demand, reused stream-ordered)."""
+    t = _fwd_ws.get(device)
+    if t is None or t.numel() < n:
+        t = torch.empty(n, dtype=torch.float32, device=device)
+        _fwd_ws[device] = t
+    return t
 
 
 def attn_dq_part_elems(B, H, Lq, Lk, hd, window=0):

@@ -49,27 +49,30 @@ def _noise_floor(name):
     if not os.path.exists(f):
         return {}
     with open(f) as fh:
-        return {k: v[0] for k, v in json.load(fh)['ratio_std_maxdev_mincos'].items()}
+        return {k: (v[0], v[2]) for k, v in json.load(fh)['ratio_std_maxdev_mincos'].items()}
 
 
 NOISE_MULT = 4.0   # the bar's multiple of the bf16 noise floor (4 sigma: ~1e-4 false alarms per parameter)
 
 
 def _grad_bars(worst, msg, name=None):
-    """Every parameter: cosine >= 0.995. Norm ratio within max(base, 4 sigma_bf16): base 2 % for every weight matrix,
+    """Every parameter: cosine >= min(0.995, 1 - 2 (1 - cos_bf16)), cos_bf16 the lowest cosine any of the 9 bf16
+    emulation draws reached for that parameter (the encoder bottleneck's key gradients go down to 0.9936 at the C5 shape).
+    Norm ratio within max(base, 4 sigma_bf16): base 2 % for every weight matrix,
     5 % for the 1-D parameters (biases, LayerNorm affine, learned queries: the key-projection bias gradient is a
     cancellation residual -- softmax is invariant to a bias added to every key up to the rotary phase); sigma_bf16 the
     parameter's measured bf16 noise floor at this configuration (_noise_floor). The encoder's self-attention over its
     64 latents (nearly alike keys) is where that floor lies above the base: q / k gradients at 1.0-2.0 % sigma at the
     C2 / C4 shapes (tests/golden/noise_floor_*.json; a correct bf16 emulation strays up to 4.4 % there), so a 2 % bar
     could not tell a regression from rounding."""
-    assert worst[0][0] >= 0.995, msg
     floor = _noise_floor(name) if name else {}
     zs = []
     for c, r, n in worst:
         base = 0.05 if (n.endswith('bias') or 'layer_norm' in n or n.startswith('output_layer.2.')
                         or n.endswith('learned_queries')) else 0.02
-        sig = floor.get(n, 0.0)
+        sig, cmin = floor.get(n, (0.0, 1.0))
+        cbar = min(0.995, 1.0 - 2.0 * (1.0 - cmin))
+        assert c >= cbar, f'{n}: cosine {c:.5f} (bar {cbar:.5f})\n' + msg
         tol = max(base, NOISE_MULT * sig)
         if sig > 0:
             zs.append((r - 1.0) / sig)

@@ -608,6 +608,10 @@ def _attn_ref(q, k, v, pad, causal, scale):
     (2, 4, 64, 520, 64, False, True, True),        # learned queries over 3 key blocks (the encoder's first layer)
     (1, 2, 1536, 1536, 64, True, False, False),    # 3 dQ planes of two 256-key sub-blocks each
     (1, 2, 256, 1300, 96, False, True, False),     # non-causal hd 96: 6 sub-blocks, the last partial, 3 planes
+    # few queries over many keys: the split-KV forward (key slices + combine), learned queries / padding / hd 96
+    (2, 2, 64, 5000, 64, False, True, True),
+    (1, 2, 100, 3000, 64, False, False, False),
+    (1, 2, 64, 4100, 96, False, True, False),
 ])
 def test_attention_fwd_bwd(B, H, Lq, Lk, hd, causal, padded, learned):
     torch.manual_seed(Lq * 7 + hd)
@@ -635,6 +639,13 @@ def test_attention_fwd_bwd(B, H, Lq, Lk, hd, causal, padded, learned):
     ref = _attn_ref(qr, kr, vr, pad, causal, scale)
     ref_o = ref.transpose(1, 2).reshape(B, Lq, d)
     assert _rel(o, ref_o) < 1e-2
+    with torch.no_grad():   # lse (the backward's row constant; the split-KV forward combines it over key slices)
+        sc = qr @ kr.transpose(-1, -2) * scale
+        if pad is not None:
+            sc = sc - pad[:, None, None, :].float() * 1e7
+        if causal:
+            sc = sc - torch.ones(Lq, Lk, device=dev).triu(1) * 1e7
+        assert (lse - torch.logsumexp(sc, -1)).abs().max().item() < 1e-4
     do = torch.randn(B, Lq, d, device=dev).bfloat16()
     ref_o.backward(do.float())
     dq = torch.full((B, Lq, d), 7.0, device=dev)    # written, not accumulated
