@@ -147,6 +147,18 @@ int svae_layernorm_bwd_gelu(const void* dy, const void* x, int32_t x_dtype, cons
 int svae_layernorm_fwd_z(float* x, const float* zrows, int32_t zmod, const float* w, const float* b, void* y,
                          float* mean, float* rstd, int32_t rows, int32_t D, svae_stream_t stream);
 int svae_layernorm_nblk(int32_t rows);
+/* n <= SVAE_LN_MULTI_MAX LayerNorms of ONE input with their own affines: the encoder middle layers'
+ * context_layer_norm(context) over the same x_emb (transformer_layer.py:52, one per middle layer, perceiver.py:43-46).
+ * svae_layernorm_fwd_multi: one pass over f32 x writes y[j] = bf16(LN(x) * w[j] + b[j]) (bit-identical to n
+ * svae_layernorm_fwd calls) and the shared mean / rstd. svae_layernorm_bwd_multi: the n backwards in one pass,
+ * dx = dres + sum_j LN'_j(dy[j]) (dres may alias dx), the affine-gradient partials of LayerNorm j into part[j]
+ * ([nblk][2][D] each, as svae_layernorm_bwd's part). f32 x, D % 4 == 0, D <= 1024. */
+#define SVAE_LN_MULTI_MAX 4
+int svae_layernorm_fwd_multi(const float* x, const float* const* w, const float* const* b, void* const* y, int32_t n,
+                             float* mean, float* rstd, int32_t rows, int32_t D, svae_stream_t stream);
+int svae_layernorm_bwd_multi(const void* const* dy, const float* x, const float* const* w, const float* mean,
+                             const float* rstd, const float* dres, float* dx, float* const* part, int32_t nblk,
+                             int32_t n, int32_t rows, int32_t D, svae_stream_t stream);
 
 /* ---- column sums: out[j] (+)= sum_i in[i*ld + j] (bias grads, LN affine grads, batch sums) ----------
  * in_dtype 0 = f32, 1 = bf16. accumulate: 0 = overwrite, 1 = add into out. */

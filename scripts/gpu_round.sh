@@ -27,6 +27,7 @@ if [[ $ST == *p* && $rc == 0 ]]; then
   tail -1 "$OUT/prof.log"
   # the per-step summary and the --stats table are small; the trace itself is dropped below (> 8 MB)
   [ $rc == 0 ] && python3 scripts/prof_summary.py "$OUT/prof" > "$OUT/kernel_summary.txt" 2>&1
+  [ $rc == 0 ] && python3 scripts/ln_census.py "$OUT/prof" > "$OUT/ln_census.txt" 2>&1
   find "$OUT/prof" -name '*kernel_stats.csv' -exec cp {} "$OUT/kernel_stats.csv" \;
 fi
 if [[ $ST == *m* && $rc == 0 ]]; then

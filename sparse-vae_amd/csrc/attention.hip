@@ -1667,6 +1667,14 @@ __device__ __forceinline__ void attn_bwd8_tile(const AP& p, char* smem, int kb, 
     dma16x2_lds(ors_o, dslot, oo[0], oo[1]);
     dma16x2_lds(ors_l, dslot + 2048, ol[0], ol[1]);
   };
+  // hd 64: p.scale for the direct tiles' dQ, re-read from LDS at the use. (Kept in a register across the q-tile loop,
+  // SGPR pressure -- 231 SGPR spills since the window / [CLS] / in-kernel-delta fields -- put it in scratch, and its
+  // reload's vmcnt(0) in the dQ phase waited for the next tile's DMA on every direct tile.)
+  float* sscl = nullptr;
+  if constexpr (HDC == 64) {
+    sscl = (float*)(dslot - (w - 4) * 4096 + 4 * 4096);
+    if (tid == 0) *sscl = p.scale;
+  }
   auto dik_reduce = [&](int buf, int qb) {   // after this wave's wait for the tile's DMA and its O / o_lo pieces
     const int ln = lane_id_fresh();
     const int rl = ln >> 2, r = 16 * (w - 4) + rl, c0 = 2 * (ln & 3);
@@ -1944,7 +1952,9 @@ __device__ __forceinline__ void attn_bwd8_tile(const AP& p, char* smem, int kb, 
       for (int u = 0; u < DQ_NT; ++u) {
         const int d = 16 * (dq_u0 + u) + 4 * (lf >> 4);
         const bool ok = qok && d < p.hd;
-        f32x4 v = dq[u] * p.scale;
+        float scl = p.scale;
+        if constexpr (HDC == 64) scl = *(volatile const float*)sscl;
+        f32x4 v = dq[u] * scl;
         if (p.dq_bf) {
           if (p.rot) {
             // (the tile's cos / sin slot; a masked lane's DMA wrote zeros and its store is dropped)
@@ -2044,7 +2054,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd8_kernel(AP p) {
   // and, hd 64, the rotary slots of the direct tiles
   __shared__ __attribute__((aligned(16))) char smem[8 * RowImg<HDC>::BYTES + 4 * Tile<64>::BYTES + 2 * 8 * 128 * 4 +
                                                     (HDC == 64 && NSUB == 2 ? 2 : 1) * 8 * (HDC / 32) * 1024 +
-                                                    (HDC == 64 ? 2 * 64 * 4 + 4 * 4096 : 0)];   // (+ in-kernel delta)
+                                                    (HDC == 64 ? 2 * 64 * 4 + 4 * 4096 + 16 : 0)];   // (+ in-kernel delta, scale)
   int kb, h, b;
   xcd_block(kb, h, b, p.causal ? 2 : 0);
   // NSUB 256-key sub-blocks per workgroup and dQ plane (1, or 2 as two instances of the sweep: the loop form spilled

@@ -44,6 +44,40 @@ __device__ __forceinline__ void ln_load_row(const T* __restrict__ xr, int lane, 
   }
 }
 
+// y = bf16((v - mean) * rstd * w + b) of one row held by a wave (the ln_col layout of MAXV)
+template <int MAXV>
+__device__ __forceinline__ void ln_store_row(const f32x4 (&v)[MAXV], float mean, float rstd, const float* __restrict__ w,
+                                             const float* __restrict__ b, bf16* __restrict__ yr, int lane, int D) {
+  if constexpr (MAXV % 2 == 0) {
+#pragma unroll
+    for (int j = 0; j < MAXV / 2; ++j) {
+      const int c = ln_col<MAXV>(lane, 2 * j);
+      if (c < D) {
+        bf16x8 o;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const f32x4 ww = *(const f32x4*)(w + c + 4 * h), bb = *(const f32x4*)(b + c + 4 * h);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[4 * h + e] = f2bf((v[2 * j + h][e] - mean) * rstd * ww[e] + bb[e]);
+        }
+        *(bf16x8*)(yr + c) = o;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k) {
+      const int c = ln_col<MAXV>(lane, k);
+      if (c < D) {
+        const f32x4 ww = *(const f32x4*)(w + c), bb = *(const f32x4*)(b + c);
+        f32x4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = (v[k][e] - mean) * rstd * ww[e] + bb[e];
+        store4_bf(yr + c, o);
+      }
+    }
+  }
+}
+
 // A wave walks rows wave, wave + waves, ... (the launcher sizes the grid so a few rows fall to each wave) with the
 // next row's loads issued before the current row's reductions and stores: the loads stay in flight across rows
 // instead of one load round trip per wave launch.
@@ -58,7 +92,6 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, co
                                                      int zmod = 0, float* __restrict__ xw = nullptr) {
   // even MAXV: D % 8 == 0 (checked by the launcher), each lane owns runs of 8 consecutive columns, so the bf16 output
   // is one 16-B store per run (the 4-column layout stores 8 B per lane); odd MAXV: runs of 4 columns
-  constexpr bool W8 = MAXV % 2 == 0;
   const int lane = threadIdx.x & 63;
   const int nw = gridDim.x * 4;
   int row = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -96,35 +129,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, co
       for (int e = 0; e < 4; ++e) { const float t = in ? v[k][e] - mean : 0.f; sq += t * t; }
     }
     const float rstd = rsqrtf(wave_sum(sq) / D + 1e-5f);
-    bf16* yr = y + (long long)row * D;
-    if constexpr (W8) {
-#pragma unroll
-      for (int j = 0; j < MAXV / 2; ++j) {
-        const int c = ln_col<MAXV>(lane, 2 * j);
-        if (c < D) {
-          bf16x8 o;
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const f32x4 ww = *(const f32x4*)(w + c + 4 * h), bb = *(const f32x4*)(b + c + 4 * h);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) o[4 * h + e] = f2bf((v[2 * j + h][e] - mean) * rstd * ww[e] + bb[e]);
-          }
-          *(bf16x8*)(yr + c) = o;
-        }
-      }
-    } else {
-#pragma unroll
-      for (int k = 0; k < MAXV; ++k) {
-        const int c = ln_col<MAXV>(lane, k);
-        if (c < D) {
-          const f32x4 ww = *(const f32x4*)(w + c), bb = *(const f32x4*)(b + c);
-          f32x4 o;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) o[e] = (v[k][e] - mean) * rstd * ww[e] + bb[e];
-          store4_bf(yr + c, o);
-        }
-      }
-    }
+    ln_store_row<MAXV>(v, mean, rstd, w, b, y + (long long)row * D, lane, D);
     if (lane == 0) { mean_out[row] = mean; rstd_out[row] = rstd; }
     if (next >= rows) break;
     for (int k = 0; k < MAXV; ++k) v[k] = vn[k];   // (register renames once unrolled by the optimiser)
@@ -364,6 +369,136 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16* __restrict__ dy
   }
 }
 
+// The encoder middle layers' context LayerNorms: n <= SVAE_LN_MULTI_MAX affines of one normalised input
+struct LnMulti {
+  const float* w[SVAE_LN_MULTI_MAX];
+  const float* b[SVAE_LN_MULTI_MAX];
+  bf16* y[SVAE_LN_MULTI_MAX];
+  const bf16* dy[SVAE_LN_MULTI_MAX];
+  float* part[SVAE_LN_MULTI_MAX];
+  int n;
+};
+
+// ln_fwd_kernel (f32 x, no z splice) writing m.n outputs from one read of the row: the statistics and every output
+// element are computed as ln_fwd_kernel computes them (bit-identical to m.n separate passes)
+template <int MAXV>
+__global__ __launch_bounds__(256) void ln_fwd_multi_kernel(const float* __restrict__ x, LnMulti m,
+                                                           float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                           int rows, int D) {
+  const int lane = threadIdx.x & 63;
+  const int nw = gridDim.x * 4;
+  int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  f32x4 v[MAXV], vn[MAXV];
+  ln_load_row<float, MAXV>(x + (long long)row * D, lane, D, v);
+#pragma nounroll
+  while (true) {
+    const int next = row + nw;
+    if (next < rows) ln_load_row<float, MAXV>(x + (long long)next * D, lane, D, vn);
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k) s += (v[k][0] + v[k][1]) + (v[k][2] + v[k][3]);
+    const float mean = wave_sum(s) / D;
+    float sq = 0.f;
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k) {
+      const bool in = ln_col<MAXV>(lane, k) < D;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { const float t = in ? v[k][e] - mean : 0.f; sq += t * t; }
+    }
+    const float rstd = rsqrtf(wave_sum(sq) / D + 1e-5f);
+#pragma unroll
+    for (int j = 0; j < SVAE_LN_MULTI_MAX; ++j)
+      if (j < m.n) ln_store_row<MAXV>(v, mean, rstd, m.w[j], m.b[j], m.y[j] + (long long)row * D, lane, D);
+    if (lane == 0) { mean_out[row] = mean; rstd_out[row] = rstd; }
+    if (next >= rows) break;
+    for (int k = 0; k < MAXV; ++k) v[k] = vn[k];
+    row = next;
+  }
+}
+
+// m.n LayerNorm backwards of one input in one pass (ln_bwd_kernel's row program): LN' is linear in g = dy * w, so
+// dx = dres + rstd (G - mean(G) - xh mean(G xh)) with G = sum_j dy[j] * w[j]; the affine partials per LayerNorm j
+// (sum dy[j] * xh, sum dy[j]) into m.part[j]. Moves 4 (x) + 2 n (dy) + 8 (dres, dx) bytes per element instead of
+// n (2 + 4 + 8). (dres may alias dx: no __restrict__.)
+template <int MAXV>
+__global__ __launch_bounds__(256) void ln_bwd_multi_kernel(LnMulti m, const float* __restrict__ x,
+                                                           const float* __restrict__ mean_in,
+                                                           const float* __restrict__ rstd_in, const float* dres,
+                                                           float* dx, int rows, int D) {
+  constexpr int NM = SVAE_LN_MULTI_MAX;
+  __shared__ float red[4][2][256 * MAXV];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  f32x4 adw[NM][MAXV], adb[NM][MAXV];
+#pragma unroll
+  for (int i = 0; i < NM; ++i)
+#pragma unroll
+    for (int j = 0; j < MAXV; ++j) { adw[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f}; adb[i][j] = adw[i][j]; }
+  for (int row = blockIdx.x * 4 + wave; row < rows; row += gridDim.x * 4) {
+    const long long base = (long long)row * D;
+    const float mean = mean_in[row], rstd = rstd_in[row];
+    f32x4 xh[MAXV], g[MAXV];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < MAXV; ++j) {
+      const int c = (lane + 64 * j) * 4;
+      g[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      xh[j] = g[j];
+      if (c < D) {
+        const f32x4 xv = *(const f32x4*)(x + base + c);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) xh[j][e] = (xv[e] - mean) * rstd;
+#pragma unroll
+        for (int i = 0; i < NM; ++i) {
+          if (i >= m.n) break;
+          const f32x4 dv = load4<bf16>(m.dy[i] + base + c);
+          const f32x4 ww = *(const f32x4*)(m.w[i] + c);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            g[j][e] += dv[e] * ww[e];
+            adw[i][j][e] += dv[e] * xh[j][e];
+            adb[i][j][e] += dv[e];
+          }
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { s1 += g[j][e]; s2 += g[j][e] * xh[j][e]; }
+      }
+    }
+    const float m1 = wave_sum(s1) / D, m2 = wave_sum(s2) / D;
+#pragma unroll
+    for (int j = 0; j < MAXV; ++j) {
+      const int c = (lane + 64 * j) * 4;
+      if (c < D) {
+        f32x4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = rstd * (g[j][e] - m1 - xh[j][e] * m2);
+        if (dres) o += *(const f32x4*)(dres + base + c);
+        *(f32x4*)(dx + base + c) = o;
+      }
+    }
+  }
+  // per LayerNorm: reduce the 4 waves' affine partials, write this block's slab of m.part[i]
+#pragma unroll
+  for (int i = 0; i < NM; ++i) {
+    if (i >= m.n) break;
+    if (i > 0) __syncthreads();   // (the previous LayerNorm's reads of red are done)
+#pragma unroll
+    for (int j = 0; j < MAXV; ++j) {
+      const int c = (lane + 64 * j) * 4;
+      if (c < D) {
+        *(f32x4*)&red[wave][0][c] = adw[i][j];
+        *(f32x4*)&red[wave][1][c] = adb[i][j];
+      }
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < 2 * D; c += 256) {
+      const int which = c / D, col = c % D;
+      const float s = red[0][which][col] + red[1][which][col] + red[2][which][col] + red[3][which][col];
+      m.part[i][((long long)blockIdx.x * 2 + which) * D + col] = s;
+    }
+  }
+}
+
 // out[j] += sum_i in[i*ld + j]. Block = 64 columns (16 column threads x 4) x 16 row threads, grid (column blocks,
 // row splits): every thread keeps 8 rows' loads in flight, the block reduces its 16 row threads in LDS and adds
 // its 64 sums with one atomic each. (Row-wave blocks with a serial row loop ran 7.9 us on the LayerNorm slabs'
@@ -565,6 +700,59 @@ SVAE_EXPORT int svae_resid_ln_fwd(const float* x, const void* y, int32_t y_dtype
     if (y_dtype == 0) SVAE_RLN(2, 8, float); else SVAE_RLN(2, 8, bf16);
   }
 #undef SVAE_RLN
+  SVAE_LAUNCH_CHECK();
+  return SVAE_OK;
+}
+
+SVAE_EXPORT int svae_layernorm_fwd_multi(const float* x, const float* const* w, const float* const* b, void* const* y,
+                                         int32_t n, float* mean, float* rstd, int32_t rows, int32_t D,
+                                         svae_stream_t stream) {
+  if (!x || !w || !b || !y || !mean || !rstd || n <= 0 || n > SVAE_LN_MULTI_MAX || rows <= 0 || D <= 0 || D % 4 ||
+      D > 1024)
+    return SVAE_EINVAL;
+  LnMulti m = {};
+  m.n = n;
+  for (int i = 0; i < n; ++i) {
+    if (!w[i] || !b[i] || !y[i]) return SVAE_EINVAL;
+    m.w[i] = w[i]; m.b[i] = b[i]; m.y[i] = (bf16*)y[i];
+  }
+  // the grid and the row layout of svae_layernorm_fwd (so the outputs are bit-identical to its)
+  static const int cap_env = [] { const char* e = getenv("SVAE_LN_FWD_BLOCKS"); return e ? atoi(e) : -1; }();
+  static const int c4 = [] { const char* e = getenv("SVAE_LN_FWD_4COL"); return e ? atoi(e) : 1; }();
+  const int cap = cap_env >= 0 ? cap_env : ((D <= 512 || (c4 && D <= 768)) ? 2048 : 1024);
+  const int need = (rows + 3) / 4;
+  dim3 grid((unsigned)(cap > 0 ? std::min(need, cap) : need));
+  hipStream_t s = (hipStream_t)stream;
+#define SVAE_LN_FWDM(MV) hipLaunchKernelGGL((ln_fwd_multi_kernel<MV>), grid, dim3(256), 0, s, x, m, mean, rstd, rows, D)
+  if (c4 && D > 512 && D <= 768) SVAE_LN_FWDM(3);
+  else if (D % 8 == 0 && D <= 512) SVAE_LN_FWDM(2);
+  else if (D % 8 == 0) SVAE_LN_FWDM(4);
+  else if (D <= 768) SVAE_LN_FWDM(3);
+  else SVAE_LN_FWDM(5);
+#undef SVAE_LN_FWDM
+  SVAE_LAUNCH_CHECK();
+  return SVAE_OK;
+}
+
+SVAE_EXPORT int svae_layernorm_bwd_multi(const void* const* dy, const float* x, const float* const* w, const float* mean,
+                                         const float* rstd, const float* dres, float* dx, float* const* part,
+                                         int32_t nblk, int32_t n, int32_t rows, int32_t D, svae_stream_t stream) {
+  if (!dy || !x || !w || !mean || !rstd || !dx || !part || n <= 0 || n > SVAE_LN_MULTI_MAX || rows <= 0 || D <= 0 ||
+      D % 4 || D > 1024 || nblk <= 0)
+    return SVAE_EINVAL;
+  LnMulti m = {};
+  m.n = n;
+  for (int i = 0; i < n; ++i) {
+    if (!dy[i] || !w[i] || !part[i]) return SVAE_EINVAL;
+    m.dy[i] = (const bf16*)dy[i]; m.w[i] = w[i]; m.part[i] = part[i];
+  }
+  hipStream_t s = (hipStream_t)stream;
+#define SVAE_LN_BWDM(MV) \
+  hipLaunchKernelGGL((ln_bwd_multi_kernel<MV>), dim3(nblk), dim3(256), 0, s, m, x, mean, rstd, dres, dx, rows, D)
+  if (D <= 512) SVAE_LN_BWDM(2);
+  else if (D <= 768) SVAE_LN_BWDM(3);
+  else SVAE_LN_BWDM(4);
+#undef SVAE_LN_BWDM
   SVAE_LAUNCH_CHECK();
   return SVAE_OK;
 }

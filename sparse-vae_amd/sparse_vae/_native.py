@@ -64,6 +64,7 @@ class AttnDesc(ctypes.Structure):
 
 
 COLSUM_MAX = 8
+LN_MULTI_MAX = 4        # SVAE_LN_MULTI_MAX
 
 
 ZPROJ_MAX = 32
@@ -139,6 +140,10 @@ _SIGS = {
     'svae_step_scalars': [c_void_p, c_void_p, c_void_p, c_float, c_void_p, c_void_p, c_void_p],
     'svae_zproj_bwd_multi': [c_void_p, c_int32, c_void_p, c_void_p, c_int32, c_int32, c_int32, c_void_p],
     'svae_zproj_fwd_multi': [c_void_p, c_int32, c_void_p, c_int32, c_int32, c_int32, c_void_p],
+    'svae_layernorm_fwd_multi': [c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_int32, c_int32,
+                                 c_void_p],
+    'svae_layernorm_bwd_multi': [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                 c_int32, c_int32, c_int32, c_int32, c_void_p],
     'svae_layernorm_fwd_z': [c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32,
                              c_int32, c_void_p],
     'svae_cast_bf16': [c_void_p, c_void_p, c_int64, c_void_p],

@@ -20,7 +20,7 @@ from collections import OrderedDict
 import torch
 
 from . import kernels as K
-from ._native import COLSUM_MAX, ZPROJ_MAX
+from ._native import COLSUM_MAX, LN_MULTI_MAX, ZPROJ_MAX
 from ._native import EPI_BF16, EPI_F32, EPI_F32_ACC, EPI_GELU, EPI_GELU_BWD, EPI_DROPOUT_RESID, \
     EPI_ROTARY_BF16, EPI_CE_STATS, EPI_F32_ATOMIC, EPI_CE_PROB, EPI_ROWSCALE_GATHER
 
@@ -43,13 +43,20 @@ def _attn_entries(pre, d, learned):
     return out
 
 
-def _layer_entries(pre, d, learned=None, cross=False):
+def _ctx_ln_entries(pre, d):
+    return [(pre + 'context_layer_norm.weight', (d,)), (pre + 'context_layer_norm.bias', (d,))]
+
+
+def _layer_entries(pre, d, learned=None, cross=False, ctx_ln=True):
+    """ctx_ln=False: the cross-attention layer's context LayerNorm is laid out elsewhere (layout_entries: after every
+    middle layer, where the batched context-LayerNorm backward completes it)."""
     out = _attn_entries(pre + 'attention.', d, learned)
     out += [(pre + 'attn_layer_norm.weight', (d,)), (pre + 'attn_layer_norm.bias', (d,))]
     if cross:
         out += _attn_entries(pre + 'cross_attention.', d, None)
-        out += [(pre + 'cross_attn_layer_norm.weight', (d,)), (pre + 'cross_attn_layer_norm.bias', (d,)),
-                (pre + 'context_layer_norm.weight', (d,)), (pre + 'context_layer_norm.bias', (d,))]
+        out += [(pre + 'cross_attn_layer_norm.weight', (d,)), (pre + 'cross_attn_layer_norm.bias', (d,))]
+        if ctx_ln:
+            out += _ctx_ln_entries(pre, d)
     out += [(pre + 'ffn.0.weight', (4 * d, d)), (pre + 'ffn.0.bias', (4 * d,)), (pre + 'ffn.2.weight', (d, 4 * d)),
             (pre + 'ffn_layer_norm.weight', (d,)), (pre + 'ffn_layer_norm.bias', (d,))]
     return out
@@ -57,6 +64,15 @@ def _layer_entries(pre, d, learned=None, cross=False):
 
 def _pos_linear_entries(pre, d):
     return [(pre + 'pos_linear.weight', (d, d)), (pre + 'pos_linear.bias', (d,))]
+
+
+def ctx_ln_batched(hp):
+    """The encoder middle layers' context LayerNorms -- one per middle layer, all over the same x_emb
+    (transformer_layer.py:52, perceiver.py:43-46) -- run as batched passes: one forward pass writes every layer's
+    normalised context (svae_layernorm_fwd_multi) and one backward pass after the middle layers' backward sums their
+    gradients (svae_layernorm_bwd_multi), instead of one forward and one backward pass per layer. On with >= 2 middle
+    layers (C4 / C5: 4); SVAE_CTX_LN_BATCH=0 restores the per-layer passes (A/B runs)."""
+    return hp.enc_layers - 2 >= 2 and os.environ.get('SVAE_CTX_LN_BATCH', '1') != '0'
 
 
 def layout_entries(hp):
@@ -73,10 +89,15 @@ def layout_entries(hp):
     live += [('q_of_z_given_x.linear.weight', (2 * Z, d)), ('q_of_z_given_x.linear.bias', (2 * Z,))]
     live += _layer_entries('encoder.bottleneck.', d, learned=1)
     dead += _pos_linear_entries('encoder.bottleneck.attention.', d)
-    for j in reversed(range(hp.enc_layers - 2)):
-        live += _layer_entries(f'encoder.middle_layers.{j}.', d, cross=True)
+    nmid = hp.enc_layers - 2
+    batched = ctx_ln_batched(hp)
+    for j in reversed(range(nmid)):
+        live += _layer_entries(f'encoder.middle_layers.{j}.', d, cross=True, ctx_ln=not batched)
         dead += _pos_linear_entries(f'encoder.middle_layers.{j}.attention.', d)
         dead += _pos_linear_entries(f'encoder.middle_layers.{j}.cross_attention.', d)
+    if batched:   # (their gradients complete together, after the middle layers' backward)
+        for j in reversed(range(nmid)):
+            live += _ctx_ln_entries(f'encoder.middle_layers.{j}.', d)
     live += _layer_entries('encoder.first_layer.', d, learned=N)
     dead += _pos_linear_entries('encoder.first_layer.attention.', d)
     live += [('input_layer.0.weight', (V, d))]
@@ -401,7 +422,7 @@ class VAEEngine:
     # ------------------------------------------------------------------ one transformer layer
     def layer_fwd(self, pre, x, B, Sx, L, pad, *, learned=0, cross=False, causal=False, ctx=None, heads, hd,
                   drop_p=0.0, seed=0, tag, out=None, window=0, fuse=False, h_in=None, next_ln=None, out_bf=None,
-                  zsplice=None):
+                  zsplice=None, ctx_ln=None):
         """TransformerLayer.forward (transformer_layer.py:44-61) on x f32 [B*Sx, d]. Returns the f32 output
         [B*Lq, d] and the saved state for layer_bwd. window > 0: sliding-window self-attention.
 
@@ -411,7 +432,8 @@ class VAEEngine:
         with the NEXT layer's attention LayerNorm: next_ln = (LayerNorm name, z rows [B, d] f32, L, next tag) -- the z
         splice's rows are taken from the z rows -- which leaves (h, (x, mean, rstd)) in st['next_h'] for the next
         layer's h_in; without next_ln (the last layer) only the bf16 copy of the output is written, into out_bf (the
-        head's input)."""
+        head's input). ctx_ln = (cx, (ctx, mean, rstd)): this layer's context LayerNorm output, computed by the batched
+        pass (ctx_ln_batched); its backward is then left to the caller (st['ctx_deferred'])."""
         d, ws, P = self.d, self.ws, self.P
         rows_x = B * Sx
         rot = self.rot(max(Sx, L), window)
@@ -472,7 +494,11 @@ class VAEEngine:
         if cross:                                  # transformer_layer.py:51-54
             c = pre + 'cross_attention.'
             rows_c = B * L
-            cx, st['ln_ctx'] = self._ln_fwd(pre + 'context_layer_norm', ctx, rows_c, tag + '.ln_ctx')
+            if ctx_ln is not None:
+                cx, st['ln_ctx'] = ctx_ln
+                st['ctx_deferred'] = True
+            else:
+                cx, st['ln_ctx'] = self._ln_fwd(pre + 'context_layer_norm', ctx, rows_c, tag + '.ln_ctx')
             hq, st['ln_cross'] = self._ln_fwd(pre + 'cross_attn_layer_norm', x1, rows_q, tag + '.ln_cross')
             qc = ws.get(tag + '.qc', (rows_q, d))
             K.gemm(hq, P.w(c + 'q_linear.weight'), qc, rows_q, d, d, epi=EPI_ROTARY_BF16, bias=P.f(c + 'q_linear.bias'),
@@ -587,12 +613,16 @@ class VAEEngine:
             dhq = ws.get('b.dhq', (rows_q, d))
             K.gemm(dqc, P.wT(c + 'q_linear.weight', d, d), dhq, rows_q, d, d, epi=EPI_BF16)
             self._dw(dkvc, st['cx'], c + 'k_linear.weight', rows_c, 2 * d, d, bias=c + 'k_linear.bias')
-            dcx = ws.get('b.dcx', (rows_c, d))
+            # (a deferred context LayerNorm: its own gradient buffer, read by the batched backward after the layers)
+            dcx = ws.get('b.dcx.' + st['tag'] if st.get('ctx_deferred') else 'b.dcx', (rows_c, d))
             K.gemm(dkvc, P.wT(c + 'k_linear.weight', 2 * d, d), dcx, rows_c, d, 2 * d, epi=EPI_BF16)
             dx1 = ws.get('b.dx1', (rows_q, d), f32)
             gx1 = ws.get('b.gx1', (rows_q, d))
             self._ln_bwd(pre + 'cross_attn_layer_norm', dhq, st['ln_cross'], rows_q, dxc, dx1, gx1)
-            self._ln_bwd(pre + 'context_layer_norm', dcx, st['ln_ctx'], rows_c, dctx, dctx)
+            if st.get('ctx_deferred'):
+                st['dcx'] = dcx
+            else:
+                self._ln_bwd(pre + 'context_layer_norm', dcx, st['ln_ctx'], rows_c, dctx, dctx)
         # ---- self / learned-query attention (attention.py:51-105)
         wo_dw = (gx1, st['O'], a + 'output_linear.weight', rows_q, d, d, None, None, a + 'output_linear.bias')
         dO = ws.get('b.dO', (rows_q, d))
@@ -763,9 +793,12 @@ class VAEEngine:
         z, st = self.layer_fwd('encoder.first_layer.', x_emb, B, L, L, padm, learned=N, heads=self.He, hd=64,
                                drop_p=dropout, seed=_mix_seed(seed, 1000), tag='e0')
         lay.append(st)
-        for j in range(hp.enc_layers - 2):
+        nmid = hp.enc_layers - 2
+        cxs = self._ctx_ln_fwd(x_emb, B * L, nmid) if ctx_ln_batched(hp) else [None] * nmid
+        for j in range(nmid):
             z, st = self.layer_fwd(f'encoder.middle_layers.{j}.', z, B, N, L, padm, cross=True, ctx=x_emb,
-                                   heads=self.He, hd=64, drop_p=dropout, seed=_mix_seed(seed, 1001 + j), tag=f'e{j + 1}')
+                                   heads=self.He, hd=64, drop_p=dropout, seed=_mix_seed(seed, 1001 + j), tag=f'e{j + 1}',
+                                   ctx_ln=cxs[j])
             lay.append(st)
         enc, st = self.layer_fwd('encoder.bottleneck.', z, B, N, L, padm, learned=1, heads=self.He, hd=64,
                                  drop_p=dropout, seed=_mix_seed(seed, 1999), tag='eb')
@@ -776,6 +809,45 @@ class VAEEngine:
         K.gemm(enc_bf, P.w('q_of_z_given_x.linear.weight'), stats, B, 2 * Z, d, epi=EPI_F32,
                bias=P.f('q_of_z_given_x.linear.bias'))
         return enc_bf, stats, lay
+
+    def _ctx_ln_fwd(self, x, rows, nmid):
+        """Every middle layer's context_layer_norm(x_emb) (transformer_layer.py:52) in batched passes of <= LN_MULTI_MAX
+        layers: returns per layer (cx bf16, (x, mean, rstd)) for layer_fwd's ctx_ln."""
+        D, ws, P = self.d, self.ws, self.P
+        mean = ws.get('ctx.ln.mean', (rows,), f32)
+        rstd = ws.get('ctx.ln.rstd', (rows,), f32)
+        out = []
+        for j0 in range(0, nmid, LN_MULTI_MAX):
+            js = range(j0, min(nmid, j0 + LN_MULTI_MAX))
+            names = [f'encoder.middle_layers.{j}.context_layer_norm' for j in js]
+            ys = [ws.get(f'e{j + 1}.ln_ctx.y', (rows, D)) for j in js]
+            K.layernorm_fwd_multi(x, [P.f(n + '.weight') for n in names], [P.f(n + '.bias') for n in names], ys, mean,
+                                  rstd, rows, D)
+            out += [(y, (x, mean, rstd)) for y in ys]
+        return out
+
+    def _ctx_ln_bwd(self, sts, dctx):
+        """The deferred context LayerNorm backwards of the middle layers' states sts (their dcx saved by layer_bwd), in
+        batched passes of <= LN_MULTI_MAX: dctx += sum of their input gradients; each layer's affine gradients."""
+        D, P = self.d, self.P
+        for j0 in range(0, len(sts), LN_MULTI_MAX):
+            grp = sts[j0:j0 + LN_MULTI_MAX]
+            x, mean, rstd = grp[0]['ln_ctx']
+            rows = x.shape[0]
+            names = [g['pre'] + 'context_layer_norm' for g in grp]
+            wgs = [P.grad[P.offsets[n + '.weight'][0]:][:2 * D] for n in names]
+            n1 = 1024 * 2 * D
+            if self.cs_batch:
+                if len(self._cs_pending) + len(grp) > COLSUM_MAX:
+                    self.flush_colsum()
+                k = len(self._cs_pending)
+                part = self.ws.get('ln.parts', (COLSUM_MAX * n1,), f32)[k * n1:(k + len(grp)) * n1]
+                defer = self._cs_pending
+            else:
+                part = self.ws.get('ln.partm', (LN_MULTI_MAX * n1,), f32)
+                defer = None
+            K.layernorm_bwd_multi([g['dcx'] for g in grp], x, [P.f(n + '.weight') for n in names], mean, rstd, dctx,
+                                  dctx, wgs, rows, D, part, defer=defer)
 
     def _inputs(self, ids, pad):
         """ids [B, L] -> (int32 ids, uint8 key-padding mask or None) in the workspace."""
@@ -1131,6 +1203,10 @@ class VAEEngine:
             self.layer_bwd(st, dcur, nxt, dctx=dx_emb)
             ready(P.end(st['pre'] + 'ffn_layer_norm.bias'))
             dcur = nxt
+        deferred = [st for st in enc if st.get('ctx_deferred')]
+        if deferred:   # the batched context LayerNorm backward (ctx_ln_batched); its parameters come next in the layout
+            self._ctx_ln_bwd(deferred[::-1], dx_emb)
+            ready(P.end(deferred[0]['pre'] + 'context_layer_norm.bias'))
         st0 = enc[0]
         if st0['resid']:   # L == num_latents: the first layer keeps its residual (transformer_layer.py:49)
             tmp = ws.get('b.dfirst', (T, d), f32)

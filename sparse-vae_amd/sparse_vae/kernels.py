@@ -242,6 +242,40 @@ def layernorm_bwd_gelu(dy, x, w, mean, rstd, gp, out_bf, wgrad2, rows, D, part_w
         colsum(part, nblk, 2 * D, 2 * D, wgrad2, accumulate=True)
 
 
+def _ptrs(ts):
+    return (ctypes.c_void_p * N.LN_MULTI_MAX)(*[t.data_ptr() for t in ts])
+
+
+def layernorm_fwd_multi(x, ws, bs, ys, mean, rstd, rows, D):
+    """svae_layernorm_fwd_multi: ys[j] = bf16(LN(x) * ws[j] + bs[j]) for n <= LN_MULTI_MAX affines of one f32 x
+    (the encoder middle layers' context LayerNorms), one pass; the shared mean / rstd."""
+    n = len(ys)
+    assert 0 < n <= N.LN_MULTI_MAX and len(ws) == n and len(bs) == n and x.dtype == f32
+    _dev(x, mean, rstd, *ws, *bs, *ys)
+    check(lib.svae_layernorm_fwd_multi(x.data_ptr(), _ptrs(ws), _ptrs(bs), _ptrs(ys), n, mean.data_ptr(),
+                                       rstd.data_ptr(), rows, D, stream()), 'svae_layernorm_fwd_multi')
+
+
+def layernorm_bwd_multi(dys, x, ws, mean, rstd, dres, dx, wgrads, rows, D, part_ws, defer=None):
+    """svae_layernorm_bwd_multi: dx = dres + sum_j LN'_j(dys[j]) (dres may be dx); wgrads[j] (the adjacent
+    [weight | bias] grads of LayerNorm j) += its affine grads, summed from part_ws (n slabs) now or by the caller's
+    deferred colsum_multi (defer, as layernorm_bwd)."""
+    n = len(dys)
+    assert 0 < n <= N.LN_MULTI_MAX and len(ws) == n and len(wgrads) == n and x.dtype == f32
+    _dev(x, mean, rstd, dx, *dys, *ws)
+    nblk = lib.svae_layernorm_nblk(rows)
+    parts = [part_ws[j * nblk * 2 * D:(j + 1) * nblk * 2 * D] for j in range(n)]
+    assert parts[-1].numel() == nblk * 2 * D
+    check(lib.svae_layernorm_bwd_multi(_ptrs(dys), x.data_ptr(), _ptrs(ws), mean.data_ptr(), rstd.data_ptr(),
+                                       ptr(dres), dx.data_ptr(), _ptrs(parts), nblk, n, rows, D, stream()),
+          'svae_layernorm_bwd_multi')
+    for part, wg in zip(parts, wgrads):
+        if defer is not None:
+            defer.append((part, nblk, 2 * D, 2 * D, wg))
+        else:
+            colsum(part, nblk, 2 * D, 2 * D, wg, accumulate=True)
+
+
 _colsum_segs = (N.ColsumSeg * N.COLSUM_MAX)()
 
 

@@ -515,6 +515,39 @@ def test_layernorm_fwd_zsplice(rows, L, D):
     assert torch.equal(y1, y0) and torch.equal(m1, m0) and torch.equal(r1, r0)
 
 
+@pytest.mark.parametrize('n,rows,D', [(4, 4100, 768), (3, 333, 512), (1, 77, 768), (2, 300, 96), (4, 65, 1024)])
+def test_layernorm_multi_matches_per_layer(n, rows, D):
+    # the encoder middle layers' context LayerNorms batched (one input, n affines): the forward equals n layernorm_fwd
+    # calls bit for bit; the backward's dx equals dres + the n layernorm_bwd contributions and each affine gradient
+    # equals its own pass's (up to f32 summation order: LN' summed before the row reductions)
+    torch.manual_seed(n + rows + D)
+    x = torch.randn(rows, D, device=dev) * 2 + 0.5
+    ws = [torch.randn(D, device=dev) * 0.1 + 1 for _ in range(n)]
+    bs = [torch.randn(D, device=dev) * 0.1 for _ in range(n)]
+    ys0 = [torch.empty(rows, D, device=dev, dtype=torch.bfloat16) for _ in range(n)]
+    m0, r0 = torch.empty(rows, device=dev), torch.empty(rows, device=dev)
+    for j in range(n):
+        K.layernorm_fwd(x, ws[j], bs[j], ys0[j], m0, r0, rows, D)
+    ys1 = [torch.full((rows, D), float('nan'), device=dev, dtype=torch.bfloat16) for _ in range(n)]
+    m1, r1 = torch.empty(rows, device=dev), torch.empty(rows, device=dev)
+    K.layernorm_fwd_multi(x, ws, bs, ys1, m1, r1, rows, D)
+    torch.cuda.synchronize()
+    assert torch.equal(m1, m0) and torch.equal(r1, r0)
+    assert all(torch.equal(a, b) for a, b in zip(ys0, ys1))
+    dys = [torch.randn(rows, D, device=dev).bfloat16() for _ in range(n)]
+    dres = torch.randn(rows, D, device=dev)
+    part = torch.empty(N.LN_MULTI_MAX * 1024 * 2 * D, device=dev)
+    dx0, wg0 = dres.clone(), [torch.zeros(2 * D, device=dev) for _ in range(n)]
+    for j in range(n):
+        K.layernorm_bwd(dys[j], x, ws[j], m0, r0, dx0, dx0, None, wg0[j], rows, D, part)
+    dx1, wg1 = dres.clone(), [torch.zeros(2 * D, device=dev) for _ in range(n)]
+    K.layernorm_bwd_multi(dys, x, ws, m1, r1, dx1, dx1, wg1, rows, D, part)
+    torch.cuda.synchronize()
+    assert _rel(dx1, dx0) < 1e-6
+    for j in range(n):
+        assert _rel(wg1[j], wg0[j]) < 1e-6
+
+
 @pytest.mark.parametrize('n,B,d,Z', [(6, 64, 512, 64), (3, 5, 200, 70), (12, 130, 768, 128)])
 def test_zproj_bwd_multi_matches_sequential(n, B, d, Z):
     # n z-projection backwards in one launch equal n svae_zproj_bwd calls in list order, bit for bit (dW, db, dz)
