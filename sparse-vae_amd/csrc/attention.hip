@@ -53,7 +53,29 @@ struct AP {
   // backward, sliding window on the attn_bwd8 path: dQ planes pk >= 1 hold only their band's wrows query rows
   // (queries pk kblk .. + wrows - 1), after plane 0's B x Lq rows: O(L) instead of O(L^2 / kblk) floats. 0 = dense.
   int wrows;
+  // forward, split-KV (svae_attn_fwd for few queries over many keys): grid z = B nsplit, slice sl = z % nsplit takes keys
+  // sl kc .. + kc - 1 and writes its O / o_lo / lse into the split workspace (fwd_slice); 1 = off
+  int nsplit, kc;
+  bf16* split_o; bf16* split_olo; float* split_lse;
 };
+
+// The split-KV forward's view of one slice: batch b of a grid of B nsplit batches is (b / nsplit, slice b % nsplit); the
+// slice's keys (pointers, padding row, length) and its outputs (the workspace's per-slice O, o_lo [B][Lq][H hd] and lse
+// [B][H][Lq]) replace the problem's in p
+__device__ __forceinline__ void fwd_slice(AP& p, int& b) {
+  const int sl = b % p.nsplit;
+  b /= p.nsplit;
+  const int k0 = sl * p.kc;
+  p.k += (long long)k0 * p.sk;
+  p.v += (long long)k0 * p.sv;
+  if (p.pad) p.pad += k0;   // (ldpad stays the full row)
+  p.Lk = min(p.kc, p.Lk - k0);
+  const long long D = (long long)p.H * p.hd, slice_o = (long long)p.B * p.Lq * D;
+  p.o = p.split_o + sl * slice_o; p.so = D; p.bo = (long long)p.Lq * D;
+  p.olo = p.split_olo + sl * slice_o; p.solo = D; p.bolo = (long long)p.Lq * D;
+  p.o32 = nullptr;
+  p.lse = p.split_lse + (long long)sl * p.B * p.H * p.Lq;
+}
 
 // Start of the (batch b) partial dQ of plane pk, indexed by ABSOLUTE query row: plane 0 and the dense layout [pk][B][Lq][D];
 // the window's compact planes [pk - 1][B][wrows][D] after plane 0 (rows pk kblk .. ; the returned base is offset back by
@@ -593,6 +615,7 @@ __global__ __launch_bounds__(256, HDC <= 96 ? 3 : 2) void attn_fwd_kernel(AP p) 
   __shared__ __attribute__((aligned(16))) char smem[ATTN_NS * 2 * FwdTile<HDP, HDC>::type::BYTES + 4 * ATTN_NS * 64 * 4];
   int bx, h, b;
   xcd_block(bx, h, b, p.causal ? 1 : 0);
+  if (p.nsplit > 1) fwd_slice(p, b);
   attn_fwd_tile<HDP, HDC>(p, smem, bx, h, b);
 }
 
@@ -674,6 +697,7 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd32_kernel(AP p) {
   __shared__ __attribute__((aligned(16))) char smem[NS * 2 * I::BYTES + FWD32_MAXPAD / 8];
   int bx, h, b;
   xcd_block(bx, h, b, p.causal ? 1 : 0);
+  if (p.nsplit > 1) fwd_slice(p, b);
   const int tid = threadIdx.x, lane = tid & 63, r32 = lane & 31, hh = lane >> 5;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int q0 = bx * 128, qw = q0 + 32 * w, qrow = qw + r32;
@@ -2369,6 +2393,8 @@ bool fill(const svae_attn_desc* d, AP& p) {
   p.cls_part = nullptr;
   p.delta_inkernel = 0;
   p.wrows = 0;
+  p.nsplit = 1; p.kc = p.Lk;
+  p.split_o = nullptr; p.split_olo = nullptr; p.split_lse = nullptr;
   if (p.window < 0 || (p.window > 0 && !p.causal)) return false;
   if (p.o32 && ((p.so32 | p.bo32) % 4)) return false;
   return true;
@@ -2424,17 +2450,20 @@ long long cls_slab_elems(int B, int H, int Lq, int hd) {
 
 namespace {
 
-// the forward's kernel choice for the (possibly key-sliced) problem p
+// the forward's kernel choice for the problem p (split-KV, p.nsplit > 1: one launch over B nsplit batches, the kernel
+// choice made for a slice's kc keys)
 void launch_fwd(const AP& p, hipStream_t s) {
-  dim3 grid((p.Lq + 127) / 128, p.H, p.B);
+  dim3 grid((p.Lq + 127) / 128, p.H, p.B * p.nsplit);
+  const int Lk = p.nsplit > 1 ? p.kc : p.Lk;
   // the 32x32-MFMA kernel for hd <= 64 (hd 96 spilled; SVAE_ATTN_FWD32=0: the 16x16 kernels, for A/B runs); its padding
   // bit mask holds FWD32_MAXPAD keys and its DMA / store offsets are 32-bit byte offsets from a sequence's row 0
   static const int fwd32_env = [] { const char* e = getenv("SVAE_ATTN_FWD32"); return e ? atoi(e) : 1; }();
   static const int occ_env = [] { const char* e = getenv("SVAE_ATTN_FWD32_OCC"); return e ? atoi(e) : 3; }();
   static const int ns_env = [] { const char* e = getenv("SVAE_ATTN_FWD32_NS"); return e ? atoi(e) : 2; }();
-  const bool fit32 = ((long long)p.Lk + 64) * std::max(p.sk, p.sv) * 2 < 0x7FFFFFF0LL &&
-                     ((long long)p.Lq + 128) * p.so * 2 < 0x7FFFFFF0LL && (!p.pad || p.Lk <= FWD32_MAXPAD) &&
-                     (!p.olo || ((long long)p.Lq + 128) * p.solo * 2 < 0x7FFFFFF0LL);   // (o_lo's 32-bit offsets too)
+  const long long so = p.nsplit > 1 ? (long long)p.H * p.hd : p.so, solo = p.nsplit > 1 ? so : p.solo;
+  const bool fit32 = ((long long)Lk + 64) * std::max(p.sk, p.sv) * 2 < 0x7FFFFFF0LL &&
+                     ((long long)p.Lq + 128) * so * 2 < 0x7FFFFFF0LL && (!p.pad || Lk <= FWD32_MAXPAD) &&
+                     (!p.olo || ((long long)p.Lq + 128) * solo * 2 < 0x7FFFFFF0LL);   // (o_lo's 32-bit offsets too)
   if (fwd32_env && fit32 && p.hd <= 64) {
     if (ns_env == 3) hipLaunchKernelGGL((attn_fwd32_kernel<64, 3, 3>), grid, dim3(256), 0, s, p);
     else if (occ_env == 4) hipLaunchKernelGGL((attn_fwd32_kernel<64, 4, 2>), grid, dim3(256), 0, s, p);
@@ -2447,7 +2476,8 @@ void launch_fwd(const AP& p, hipStream_t s) {
 // Split-KV forward for few queries over many keys (the encoder's 64 learned / latent queries against a long sequence:
 // at 2 x 16384 tokens one 128-query tile per (batch, head) gave 16 workgroups for the whole chip, 312 us per launch,
 // profiles/r06i_c2s16k_kernel_summary.txt): the keys are cut into nsplit slices of kc keys, each slice's attention runs
-// as its own problem into the workspace (O in bf16 + its bf16 residual, lse), and this kernel combines them:
+// as its own problem into the workspace (O in bf16 + its bf16 residual, lse; one launch, the slice a grid dimension:
+// fwd_slice), and this kernel combines them:
 // lse = log sum_s exp(lse_s), O = sum_s exp(lse_s - lse) O_s (a slice whose keys are all padding has lse_s = -inf and no
 // weight). One thread per 4 dims of one (batch, query, head).
 __global__ __launch_bounds__(256) void attn_fwd_combine_kernel(AP p, const bf16* so_hi, const bf16* so_lo,
@@ -2532,19 +2562,10 @@ SVAE_EXPORT int svae_attn_fwd(const svae_attn_desc* d, svae_stream_t stream) {
     bf16* ohi = (bf16*)d->fwd_ws;
     bf16* olo = ohi + (long long)nsplit * slice_o;
     float* lse = (float*)(olo + (long long)nsplit * slice_o);
-    for (int sl = 0; sl < nsplit; ++sl) {
-      AP q = p;
-      const int k0 = sl * kc;
-      q.k = p.k + (long long)k0 * p.sk;
-      q.v = p.v + (long long)k0 * p.sv;
-      q.Lk = std::min(kc, d->Lk - k0);
-      q.pad = p.pad ? p.pad + k0 : nullptr;   // (ldpad stays the full row)
-      q.o = ohi + sl * slice_o; q.so = D; q.bo = d->Lq * D;
-      q.olo = olo + sl * slice_o; q.solo = D; q.bolo = d->Lq * D;
-      q.o32 = nullptr;
-      q.lse = lse + (long long)sl * d->B * d->H * d->Lq;
-      launch_fwd(q, s);
-    }
+    AP q = p;
+    q.nsplit = nsplit; q.kc = kc;
+    q.split_o = ohi; q.split_olo = olo; q.split_lse = lse;
+    launch_fwd(q, s);
     const long long n = (long long)d->B * d->Lq * d->H * (d->hd / 4);
     hipLaunchKernelGGL(attn_fwd_combine_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, p, ohi, olo, lse,
                        nsplit);

@@ -45,6 +45,6 @@ def test_isa_has_no_dma_hazards_and_no_spills_in_the_attention_loops(tmp_path):
         for k, v in hits.items():
             assert v['vgpr_spill'] == 0 and v['scratch'] == 0, (k, v)
     # the k-weighted head dW's asm dword loads (kw_pre) were checked for an early use of their destination (ASYNC_EARLY_USE)
-    assert sum(v['async_loads'] for k, v in rep.items() if 'ILi64E' in k or 'ILi66E' in k) >= 3
+    assert sum(v['async_loads'] for k, v in rep.items() if 'gemm256' in k and ('ELi64E' in k or 'ELi66E' in k)) >= 3
     kw2 = {k: v for k, v in rep.items() if 'gemm256_kernelILb1ELb1ELi66E' in k}
     assert len(kw2) == 1 and all(v['scratch_in_mfma_loops'] == 0 for v in kw2.values()), kw2
