@@ -221,8 +221,9 @@ typedef struct svae_attn_desc {
   void* o_lo;
   int64_t so_lo, bo_lo;
   /* forward, few queries over many keys (<= 128 queries, non-causal, >= 2048 keys, < 128 query tiles in all): optional
-     f32 workspace of svae_attn_fwd_ws_elems floats (16-B aligned); when given, the keys are cut into slices run as
-     separate problems and combined (split-KV), so a long key sequence fills the chip. NULL: one pass. */
+     f32 workspace of svae_attn_fwd_ws_elems floats (16-B aligned); when given, the keys are cut into slices (one launch,
+     the slice a grid dimension) whose partial O / lse are combined (split-KV), so a long key sequence fills the chip.
+     NULL: one pass. */
   float* fwd_ws;
   int64_t fwd_ws_elems;
 } svae_attn_desc;

@@ -2090,7 +2090,11 @@ __global__ __launch_bounds__(512, 1) void attn_bwd8_kernel(AP p) {
     const int nsub = p.kblk / BWD8_KEYS;
     attn_bwd8_tile<HDC, 2, false>(p, smem, nsub * kb, h, b, nsub);
     if (nsub == 2 && (2 * kb + 1) * BWD8_KEYS < p.Lk) {
-      __syncthreads();   // the first sub-block's LDS reads done and its dQ plane stores drained (vmcnt(0))
+      // the first sub-block's dQ plane stores drained before the second reads them back by LDS-DMA (an explicit
+      // vmcnt(0): a workgroup barrier only waits lgkmcnt on gfx950, and the read-back need not come from the same
+      // wave and lane that stored), then its LDS reads done
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
       attn_bwd8_tile<HDC, 2, true>(p, smem, 2 * kb + 1, h, b, 2);
     }
   }
@@ -2525,12 +2529,14 @@ __global__ __launch_bounds__(256) void attn_fwd_combine_kernel(AP p, const bf16*
 
 // the split for a shape: slices of kc keys (a multiple of 64), nsplit of them; 1 = no split
 void fwd_split(int B, int H, int Lq, int Lk, bool causal, int window, int& nsplit, int& kc) {
+  // SVAE_ATTN_FWD_SPLIT: 0 = off, 1 = on (about 512 workgroups), N > 1 = about N workgroups (A/B runs)
   static const int env = [] { const char* e = getenv("SVAE_ATTN_FWD_SPLIT"); return e ? atoi(e) : 1; }();
   nsplit = 1;
   kc = Lk;
   const long long nwg = (long long)((Lq + 127) / 128) * H * B;
   if (!env || causal || window > 0 || Lq > 128 || nwg >= 128 || Lk < 2048) return;
-  int sp = (int)std::min<long long>((512 + nwg - 1) / nwg, (Lk + 511) / 512);
+  const long long target = env > 1 ? env : 512;
+  int sp = (int)std::min<long long>((target + nwg - 1) / nwg, (Lk + 255) / 256);
   if (sp < 2) return;
   kc = ((Lk + sp - 1) / sp + 63) / 64 * 64;
   nsplit = (Lk + kc - 1) / kc;
