@@ -1544,6 +1544,9 @@ __device__ __forceinline__ void bwd_cls_store_slab(const AP& p, float* slab, int
   }
 }
 
+#ifndef SVAE_BWD8_KEYMAP
+#define SVAE_BWD8_KEYMAP 1
+#endif
 template <int HDC, int NSUB, bool RMW>
 __device__ __forceinline__ void attn_bwd8_tile(const AP& p, char* smem, int kb, int h, int b, int nsub) {
   using R = RowImg<HDC>;
@@ -1578,7 +1581,12 @@ __device__ __forceinline__ void attn_bwd8_tile(const AP& p, char* smem, int kb, 
   const bf16* dO = p.dout + b * p.bdo + (long long)h * p.hd;
   const float* lse = p.lse + ((long long)b * p.H + h) * p.Lq;
   const float* delta = p.delta + ((long long)b * p.H + h) * p.Lq;
-  const int kw = k0 + 32 * w;                       // this wave's first key
+  // this wave's 32 keys: slot wk of the block's 8 (SVAE_BWD8_KEYMAP, default 1: waves w and w + 4 -- the two waves of
+  // one SIMD -- take slots w and 7 - w, an early and a late key group, so every SIMD carries the same causal work on
+  // the diagonal key blocks (live query tiles 4 + 1, 4 + 1, 3 + 2, 3 + 2 of a 4-tile sweep, instead of 4 + 2, 4 + 2,
+  // 3 + 1, 3 + 1 with slot = w); 0: slot = w)
+  const int wk = SVAE_BWD8_KEYMAP ? (w < 4 ? w : 11 - w) : w;
+  const int kw = k0 + 32 * wk;                      // this wave's first key
   bool key_ok[2];
   bf16x8 vf[2][NKK];
 #pragma unroll
@@ -1800,7 +1808,7 @@ __device__ __forceinline__ void attn_bwd8_tile(const AP& p, char* smem, int kb, 
     if (live) st_acc[6] += 1;
 #endif
     if (live && SVAE_BWD8_DIAG != 1) {
-      const char* Kw = Ks + (w >> 1) * R::BYTES;     // this wave's 32 keys: rows 32 (w & 1) .. of image w / 2
+      const char* Kw = Ks + (wk >> 1) * R::BYTES;    // this wave's 32 keys: rows 32 (wk & 1) .. of image wk / 2
       const bool edge = !keys_all_ok || qb + 64 > p.Lq || (p.causal && kw + 31 > qb) || qb + 63 >= band_end;
       const int qlim = min(p.Lq, band_end) - qb;
       constexpr int TPP = 2;
@@ -1812,7 +1820,7 @@ __device__ __forceinline__ void attn_bwd8_tile(const AP& p, char* smem, int kb, 
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
-          for (int kk = 0; kk < NKK; ++kk) kf[j][kk] = *(const bf16x8*)(Kw + R::off(32 * (w & 1) + 16 * j + li, g + 4 * kk));
+          for (int kk = 0; kk < NKK; ++kk) kf[j][kk] = *(const bf16x8*)(Kw + R::off(32 * (wk & 1) + 16 * j + li, g + 4 * kk));
         f32x4 s[2][TPP], dp[2][TPP];
 #pragma unroll
         for (int th = 0; th < TPP; ++th) {
@@ -1881,7 +1889,7 @@ __device__ __forceinline__ void attn_bwd8_tile(const AP& p, char* smem, int kb, 
         for (int j = 0; j < 2; ++j)
 #pragma unroll
           for (int th = 0; th < TPP; ++th)
-            *(bf16x4*)(dSs + TS::uoff(32 * w + 16 * j + li, 4 * (pass * TPP + th) + g)) =
+            *(bf16x4*)(dSs + TS::uoff(32 * wk + 16 * j + li, 4 * (pass * TPP + th) + g)) =
                 (bf16x4){f2bf(dp[j][th][0]), f2bf(dp[j][th][1]), f2bf(dp[j][th][2]), f2bf(dp[j][th][3])};
       }
     } else {
@@ -1889,7 +1897,7 @@ __device__ __forceinline__ void attn_bwd8_tile(const AP& p, char* smem, int kb, 
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
-        for (int t = 0; t < 4; ++t) *(bf16x4*)(dSs + TS::uoff(32 * w + 16 * j + li, 4 * t + g)) = z;
+        for (int t = 0; t < 4; ++t) *(bf16x4*)(dSs + TS::uoff(32 * wk + 16 * j + li, 4 * t + g)) = z;
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #ifdef SVAE_STAMPS
