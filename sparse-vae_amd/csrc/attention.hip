@@ -2628,7 +2628,9 @@ SVAE_EXPORT int svae_attn_bwd(const svae_attn_desc* d, svae_stream_t stream) {
     // in-kernel delta (SVAE_ATTN_DELTA_INKERNEL=0: the separate pass, A/B runs): the 8-wave kernel at hd <= 64 reads O
     // and o_lo itself; not with the [CLS] split (attn_bwd_cls_kernel reads delta from memory)
     static const int dik_env = [] { const char* e = getenv("SVAE_ATTN_DELTA_INKERNEL"); return e ? atoi(e) : 1; }();
-    if (dik_env && d->hd <= 64 && !d->delta_ready && d->o_lo && p.cls_q0 == 0 &&
+    // (with the [CLS] split too: every query row >= cls_q0 lies in the band of the key block holding its own key, whose
+    // workgroup stores its delta for attn_bwd_cls_kernel, launched after this kernel on the same stream)
+    if (dik_env && d->hd <= 64 && !d->delta_ready && d->o_lo &&
         ((long long)d->Lq + 64) * std::max(d->so, d->so_lo) * 2 < 0x7FFFFFF0LL)
       p.delta_inkernel = 1;
   }
