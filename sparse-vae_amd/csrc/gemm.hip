@@ -1536,203 +1536,6 @@ __global__ __launch_bounds__(512, 1) void gemm256_pair_kernel(GP2 q) {
 }
 
 // ===================================================================================================
-// gemm_pp: the 256-tile GEMM as a ping-pong of two 4-wave groups (verdict r05 item 3: the epilogue of the short-K,
-// epilogue-heavy GEMMs ran with no MFMA beside it). A 512-thread block walks 256 x 128 tiles; consecutive tiles of the
-// block alternate between group 0 (waves 0-3) and group 1 (waves 4-7), each wave 128 x 64 of its group's tile (the
-// gemm256 fragment walk). The block's K-tiles form one stream through ONE 3-stage LDS ring (48 KiB per stage: A
-// 256 x 64, B 128 x 64): at step s the computing group (C) multiplies K-tile s while the other group (E) issues the
-// DMA of K-tile s + 2 (two steps ahead: a step is half a gemm256 K-tile, shorter than the DMA's latency) and stores
-// one eighth of its previous tile's epilogue -- so the epilogue's VALU work and stores
-// run beside the other group's MFMAs, one SIMD = one C wave + one E wave. One barrier per step: the issuing group waits
-// for its DMA (counted vmcnt: only its younger epilogue stores may stay in flight), every wave retires its LDS reads
-// (lgkmcnt(0), so the stage the next DMA overwrites has been read), then s_barrier. The bias of a tile is copied to LDS
-// by its C group at the tile's last K-tile (its plain loads wait on that wave's own DMA only if it issued one lately),
-// and each wave reads only the 64 columns it wrote or its twin (same values) wrote. Interior shapes only (M % 256,
-// N % 128, K % 64 == 0, K >= 512; A [M][K], B [N][K]); epilogues bf16 and GELU (+ GELU').
-constexpr int PP_TA = 256 * 64 * 2, PP_TB = 128 * 64 * 2, PP_ST = PP_TA + PP_TB, PP_NS = 3;
-constexpr int PP_DMA = 12;   // vector-memory instructions of one K-tile's DMA per issuing wave (3 x 4 pieces)
-
-template <int EPI>
-__global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GP p) {
-  static_assert(EPI == SVAE_EPI_BF16 || EPI == SVAE_EPI_GELU, "gemm_pp epilogues: bf16, GELU");
-  constexpr int RS = EPI == SVAE_EPI_GELU ? 4 : 2;   // vector stores per epilogue row (store_rows_bf16: 2)
-  __shared__ __attribute__((aligned(16))) char smem[PP_NS * PP_ST + 2 * 128 * 4];
-  float* sbias_all = (float*)(smem + PP_NS * PP_ST);
-  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, li = lane & 15;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int gr = wave >> 2, ew = wave & 3, wr = ew >> 1, wc = ew & 1;
-  float* sbias = sbias_all + gr * 128;
-  const int nwg = gridDim.x;
-  int bid = blockIdx.x;
-  if (nwg >= 16) {
-    const int q = nwg / 8, r = nwg % 8, xcd = bid % 8, idx = bid / 8;
-    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
-  }
-  const int tm = p.M / 256, tn = p.N / 128, total = tm * tn;
-  if (bid >= total) return;
-  const int nt = (total - 1 - bid) / nwg + 1;   // this block's tiles: bid, bid + nwg, ...
-  const int nk = p.K / 64;                      // K-tiles per tile (>= 8: at most one epilogue row per step)
-  const int S = nt * nk;
-  auto tile_of = [&](int k, int& m0, int& n0) {
-    int bm, bn;
-    group_tile(bid + k * nwg, tm, tn, p.group, bm, bn);
-    m0 = bm * 256;
-    n0 = bn * 128;
-  };
-  // the group computing step s (K-tile s of the block's stream), and the issuer of K-tile t: the E group of step t - 2
-  // (group 1 for the two prologue K-tiles)
-  auto cgroup = [&](int st) { return (st / nk) & 1; };
-  auto issuer = [&](int t) { return t < 2 ? 1 : 1 - cgroup(t - 2); };
-  // this wave's DMA pieces as an issuer: A rows 64 ew .. + 63 (two 32-row piece groups), B rows 32 ew .. + 31
-  const G3Src sa0 = g3_src<false>(p.lda, 2 * ew, lane), sa1 = g3_src<false>(p.lda, 2 * ew + 1, lane);
-  const G3Src sb = g3_src<false>(p.ldb, ew, lane);
-  // counted waits: y1 / y2 = vector-memory instructions this wave issued after its most recent / second most recent DMA
-  int y1 = 0, y2 = 0;
-  auto issue = [&](int t) {   // K-tile t of the block's stream into stage t % 3 (the 4 waves of one group)
-    const int k = t / nk, kt = t - k * nk;
-    int m0, n0;
-    tile_of(k, m0, n0);
-    char* st = smem + (t % PP_NS) * PP_ST;
-    const u32x4 ra = buffer_rsrc(p.A + (long long)m0 * p.lda + kt * 64, 0x7FFFFFF0u);
-    const u32x4 rb = buffer_rsrc(p.B + (long long)n0 * p.ldb + kt * 64, 0x7FFFFFF0u);
-    dma16x4_lds(ra, st + (2 * ew) * 4 * 1024, sa0.off[0], sa0.off[1], sa0.off[2], sa0.off[3]);
-    dma16x4_lds(ra, st + (2 * ew + 1) * 4 * 1024, sa1.off[0], sa1.off[1], sa1.off[2], sa1.off[3]);
-    dma16x4_lds(rb, st + PP_TA + ew * 4 * 1024, sb.off[0], sb.off[1], sb.off[2], sb.off[3]);
-    y2 = y1 + PP_DMA;
-    y1 = 0;
-  };
-  // wait until at most n of this wave's vector-memory instructions are outstanding (n from the set y1 / y2 can take)
-  auto wait_n = [&](int n) {
-    if (n == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else if (n == RS) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(RS) : "memory");
-    else if (n == PP_DMA) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PP_DMA) : "memory");
-    else if (n == PP_DMA + RS) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PP_DMA + RS) : "memory");
-    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PP_DMA + 2 * RS) : "memory");
-  };
-  f32x4 acc[8][4];
-  auto epi_row = [&](int i, int m0, int n0) {   // fragment row i of this wave's 128 x 64 (the E role)
-    f32x4 v[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const f32x4 b4 = *(const f32x4*)(sbias + wc * 64 + j * 16 + 4 * g);
-      v[j] = p.alpha * acc[i][j] + b4;
-    }
-    const int mr = m0 + wr * 128 + i * 16, nc = n0 + wc * 64;
-    if constexpr (EPI == SVAE_EPI_GELU) {
-      f32x4 gg[4], dg[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int e = 0; e < 4; e += 2) {
-          f32x2 ge, de;
-          gelu_pair2((f32x2){v[j][e], v[j][e + 1]}, ge, de);
-          gg[j][e] = ge[0]; gg[j][e + 1] = ge[1];
-          dg[j][e] = de[0]; dg[j][e + 1] = de[1];
-        }
-      store_rows_bf16<false>((bf16*)p.C, p.ldc, mr, p.M, nc, p.N, gg, g, li);
-      store_rows_bf16<true>((bf16*)p.aux, p.ldaux, mr, p.M, nc, p.N, dg, g, li);
-    } else {
-      store_rows_bf16<false>((bf16*)p.C, p.ldc, mr, p.M, nc, p.N, v, g, li);
-    }
-    y1 += RS;
-    y2 += RS;
-  };
-
-  if (gr == 1) {   // group 1 is the E group of steps 0 and 1: it issues their K-tiles
-    issue(0);
-    if (S > 1) issue(1);
-  }
-  int last_t = gr == 1 ? (S > 1 ? 1 : 0) : -1;   // K-tile of this wave's most recent DMA
-  for (int s = 0; s < S; ++s) {
-    const int k = s / nk, kt = s - k * nk;
-    const bool isC = gr == (k & 1);
-    if (issuer(s) == gr) wait_n(last_t == s ? y1 : y2);   // its pieces of K-tile s have landed
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");    // (this wave's reads of the stage DMA'd next are done)
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    if (!isC) {
-      if (s + 2 < S) {
-        issue(s + 2);
-        last_t = s + 2;
-      }
-      // row i of the previous tile's epilogue at step (i nk) / 8 (at most one per step: nk >= 8)
-      const int row = (kt * 8 + nk - 1) / nk;
-      if (k >= 1 && row < 8 && (row * nk) / 8 == kt) {
-        int m0, n0;
-        tile_of(k - 1, m0, n0);
-        // (a static row index per unrolled copy: acc indexed at run time lives in scratch)
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-          if (i == row) epi_row(i, m0, n0);
-      }
-    } else {
-      if (kt == 0) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-      }
-      const char* la = smem + (s % PP_NS) * PP_ST;
-      const char* lb = la + PP_TA;
-      bf16x8 a0[4][2], a1[4][2], b0[2][2], b1[2][2];
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) a0[i][ks] = g3_afrag<false>(la, wr * 128 + i * 16, ks, lane);
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-          b0[j][ks] = g3_bfrag<false>(lb, wc * 64 + j * 16, ks, lane);
-          b1[j][ks] = g3_bfrag<false>(lb, wc * 64 + 32 + j * 16, ks, lane);
-        }
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j) acc[i][j] = mfma16(b0[j][ks], a0[i][ks], acc[i][j]);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) a1[i][ks] = g3_afrag<false>(la, wr * 128 + 64 + i * 16, ks, lane);
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j) acc[i][2 + j] = mfma16(b1[j][ks], a0[i][ks], acc[i][2 + j]);
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j) acc[4 + i][2 + j] = mfma16(b1[j][ks], a1[i][ks], acc[4 + i][2 + j]);
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j) acc[4 + i][j] = mfma16(b0[j][ks], a1[i][ks], acc[4 + i][j]);
-      if (kt == nk - 1) {   // the tile's bias for this group's epilogue (E role, next steps): this wave's 64 columns
-        int m0, n0;
-        tile_of(k, m0, n0);
-        sbias[wc * 64 + lane] = p.bias ? p.bias[n0 + wc * 64 + lane] : 0.f;
-      }
-    }
-  }
-  // the block's last tile: its group stores the whole epilogue
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  if (gr == ((nt - 1) & 1)) {
-    int m0, n0;
-    tile_of(nt - 1, m0, n0);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) epi_row(i, m0, n0);
-  }
-}
-
-// ===================================================================================================
 // gemm_skinny: M <= 64 rows (the encoder bottleneck layer, q(z|x), the z projections: one row per sequence).
 // A 128-row tile leaves such a GEMM to a handful of blocks that walk all of K serially (a 64 x 512 x 2048 dropout +
 // residual GEMM took 33 us). Here a block owns 32 columns, its 16 waves split K into contiguous slices (fragments
@@ -2040,28 +1843,6 @@ static int gemm_run(const svae_gemm_desc* d, svae_stream_t stream, bool* fused_d
     else return SVAE_EINVAL;
   }
   if (impl == 3 && !ok3) impl = 1;
-  // the ping-pong kernel (SVAE_GEMM_PP=1, A/B runs): interior X . W^T shapes with the bf16 / GELU epilogues
-  static const int pp_env = [] { const char* e = getenv("SVAE_GEMM_PP"); return e ? atoi(e) : 0; }();
-  if (pp_env && impl == 3 && !d->a_t && !d->b_t && d->batch == 1 && d->splits == 1 && !d->a_rowsum && !d->k_weight &&
-      (d->epi == SVAE_EPI_BF16 || (d->epi == SVAE_EPI_GELU && d->aux)) && !fused_delta && d->M % 256 == 0 &&
-      d->N % 128 == 0 && d->K % 64 == 0 && d->K >= 512 && d->lda % 8 == 0 && d->ldb % 8 == 0 && d->ldc % 8 == 0 &&
-      (d->epi != SVAE_EPI_GELU || d->ldaux % 8 == 0)) {
-    static const int ncu_pp = [] {
-      int dev = 0, n = 0;
-      if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-        n = 256;
-      return n > 0 ? n : 256;
-    }();
-    p.tn2 = d->N / 128;
-    p.tm2 = d->M / 256;
-    p.group = group_env >= 0 ? group_env : (p.tn2 >= 32 ? 4 : 0);
-    const long long tiles = (long long)p.tm2 * p.tn2;
-    const dim3 gp((unsigned)std::min<long long>(tiles, ncu_pp));
-    if (d->epi == SVAE_EPI_GELU) hipLaunchKernelGGL(gemm_pp_kernel<SVAE_EPI_GELU>, gp, dim3(512), 0, s, p);
-    else hipLaunchKernelGGL(gemm_pp_kernel<SVAE_EPI_BF16>, gp, dim3(512), 0, s, p);
-    SVAE_LAUNCH_CHECK();
-    return SVAE_OK;
-  }
   // float-atomic split-K (no slab workspace) is not a gemm256 epilogue: its staged 4-pass atomics cost 67-88 spilled
   // VGPRs there; the 128-tile kernels run it (the product's split-K weight gradients use the slab form)
   if (impl == 3 && epi_run == SVAE_EPI_F32_ATOMIC) impl = (kslice <= 2048 && !(d->a_t && d->b_t)) ? 2 : 1;
