@@ -434,9 +434,38 @@ __global__ __launch_bounds__(256) void ln_bwd_multi_kernel(LnMulti m, const floa
   for (int i = 0; i < NM; ++i)
 #pragma unroll
     for (int j = 0; j < MAXV; ++j) { adw[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f}; adb[i][j] = adw[i][j]; }
-  for (int row = blockIdx.x * 4 + wave; row < rows; row += gridDim.x * 4) {
+  // a row's inputs, loaded one row ahead (two rows' loads in flight per wave: at 192+ VGPRs two waves per SIMD fit, and
+  // one row in flight per wave ran the four-LayerNorm pass at 2.7 TB/s)
+  struct RowIn {
+    f32x4 xv[MAXV], rr[MAXV];
+    bf16x4 dv[NM][MAXV];
+    float mean, rstd;
+  };
+  auto load_row = [&](int row, RowIn& in) {
     const long long base = (long long)row * D;
-    const float mean = mean_in[row], rstd = rstd_in[row];
+    in.mean = mean_in[row];
+    in.rstd = rstd_in[row];
+#pragma unroll
+    for (int j = 0; j < MAXV; ++j) {
+      const int c = (lane + 64 * j) * 4;
+      const bool ok = c < D;
+      in.xv[j] = ok ? *(const f32x4*)(x + base + c) : (f32x4){0.f, 0.f, 0.f, 0.f};
+      in.rr[j] = ok && dres ? *(const f32x4*)(dres + base + c) : (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < NM; ++i) {
+        if (i >= m.n) break;
+        in.dv[i][j] = ok ? *(const bf16x4*)(m.dy[i] + base + c) : (bf16x4){};
+      }
+    }
+  };
+  const int stride = gridDim.x * 4;
+  int row = blockIdx.x * 4 + wave;
+  RowIn cur, nxt;
+  if (row < rows) load_row(row, cur);
+  for (; row < rows; row += stride) {
+    if (row + stride < rows) load_row(row + stride, nxt);
+    const long long base = (long long)row * D;
+    const float mean = cur.mean, rstd = cur.rstd;
     f32x4 xh[MAXV], g[MAXV];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
@@ -445,19 +474,18 @@ __global__ __launch_bounds__(256) void ln_bwd_multi_kernel(LnMulti m, const floa
       g[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
       xh[j] = g[j];
       if (c < D) {
-        const f32x4 xv = *(const f32x4*)(x + base + c);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) xh[j][e] = (xv[e] - mean) * rstd;
+        for (int e = 0; e < 4; ++e) xh[j][e] = (cur.xv[j][e] - mean) * rstd;
 #pragma unroll
         for (int i = 0; i < NM; ++i) {
           if (i >= m.n) break;
-          const f32x4 dv = load4<bf16>(m.dy[i] + base + c);
           const f32x4 ww = *(const f32x4*)(m.w[i] + c);
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            g[j][e] += dv[e] * ww[e];
-            adw[i][j][e] += dv[e] * xh[j][e];
-            adb[i][j][e] += dv[e];
+            const float dv = (float)cur.dv[i][j][e];
+            g[j][e] += dv * ww[e];
+            adw[i][j][e] += dv * xh[j][e];
+            adb[i][j][e] += dv;
           }
         }
 #pragma unroll
@@ -471,11 +499,11 @@ __global__ __launch_bounds__(256) void ln_bwd_multi_kernel(LnMulti m, const floa
       if (c < D) {
         f32x4 o;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] = rstd * (g[j][e] - m1 - xh[j][e] * m2);
-        if (dres) o += *(const f32x4*)(dres + base + c);
+        for (int e = 0; e < 4; ++e) o[e] = rstd * (g[j][e] - m1 - xh[j][e] * m2) + cur.rr[j][e];
         *(f32x4*)(dx + base + c) = o;
       }
     }
+    cur = nxt;
   }
   // per LayerNorm: reduce the 4 waves' affine partials, write this block's slab of m.part[i]
 #pragma unroll
