@@ -109,6 +109,8 @@ class FlatParams:
 
     def __init__(self, hp, device):
         live, dead = layout_entries(hp)
+        # the layout's choice for the context LayerNorms (the engine follows it, whatever the environment says later)
+        self.ctx_batched = ctx_ln_batched(hp)
         self.offsets = OrderedDict()
         off = 0
         for name, shape in live + dead:
@@ -794,7 +796,7 @@ class VAEEngine:
                                drop_p=dropout, seed=_mix_seed(seed, 1000), tag='e0')
         lay.append(st)
         nmid = hp.enc_layers - 2
-        cxs = self._ctx_ln_fwd(x_emb, B * L, nmid) if ctx_ln_batched(hp) else [None] * nmid
+        cxs = self._ctx_ln_fwd(x_emb, B * L, nmid) if P.ctx_batched else [None] * nmid
         for j in range(nmid):
             z, st = self.layer_fwd(f'encoder.middle_layers.{j}.', z, B, N, L, padm, cross=True, ctx=x_emb,
                                    heads=self.He, hd=64, drop_p=dropout, seed=_mix_seed(seed, 1001 + j), tag=f'e{j + 1}',
