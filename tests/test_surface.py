@@ -91,6 +91,32 @@ def test_flat_layout_invariants():
     assert all(off % 64 == 0 for off, _ in f.offsets.values())
 
 
+def test_context_layernorm_layout_follows_the_batching_switch(monkeypatch):
+    """With >= 2 encoder middle layers the context LayerNorms (one per middle layer, all over x_emb) are batched: their
+    [weight | bias] pairs sit together after every middle layer (their gradients complete in one backward pass after the
+    middle layers) and before the first layer; SVAE_CTX_LN_BATCH=0 keeps each inside its layer."""
+    from oracle.params import HParams
+    from sparse_vae.engine import FlatParams
+    hp = HParams(d_model=256, num_heads=4, num_layers=12)   # 6 encoder layers: 4 middle
+    f = FlatParams(hp, 'cpu')
+    assert f.ctx_batched
+    ctx = [f.offsets[f'encoder.middle_layers.{j}.context_layer_norm.weight'][0] for j in range(4)]
+    mids = [f.offsets[f'encoder.middle_layers.{j}.ffn_layer_norm.bias'][0] for j in range(4)]
+    first = f.offsets['encoder.first_layer.attention.k_linear.weight'][0]
+    assert min(ctx) > max(mids) and max(ctx) < first
+    for j in range(4):
+        n = f'encoder.middle_layers.{j}.context_layer_norm'
+        assert f.offsets[n + '.bias'][0] == f.offsets[n + '.weight'][0] + 256
+    monkeypatch.setenv('SVAE_CTX_LN_BATCH', '0')
+    g = FlatParams(hp, 'cpu')
+    assert not g.ctx_batched
+    for j in range(4):
+        pre = f'encoder.middle_layers.{j}.'
+        assert g.offsets[pre + 'cross_attn_layer_norm.bias'][0] < g.offsets[pre + 'context_layer_norm.weight'][0] \
+            < g.offsets[pre + 'ffn.0.weight'][0]
+    assert set(f.offsets) == set(g.offsets)
+
+
 def test_presets_and_cli_parsing():
     sys.path.insert(0, ROOT)
     import train
