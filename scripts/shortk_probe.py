@@ -29,7 +29,7 @@ def timeit(fn, reps=30):
 
 
 def main():
-    T, d = 32768, 512
+    T, d = int(os.environ.get('SHORTK_T', 32768)), 512   # SHORTK_T=4096: the encoder's latent rows (B x 64)
     torch.manual_seed(0)
     impl = os.environ.get('SVAE_GEMM_IMPL', 'auto')
     x = torch.randn(T, d, device=dev).bfloat16()
@@ -56,7 +56,7 @@ def main():
          lambda: K.gemm(f, w2, out32, T, d, 4 * d, epi=N.EPI_DROPOUT_RESID, resid=resid, ldr=d, drop_p=0.1, seed=7)),
         ('QKV rotary            N 1536 K 512', 2 * T * 3 * d * d,
          lambda: K.gemm(x, wq, qkv, T, 3 * d, d, epi=N.EPI_ROTARY_BF16, bias=bq, rot=rot, rot_cols=2 * d, rot_d=d,
-                        rot_seq=512)),
+                        rot_seq=min(T, 512))),
     ]
     for name, flop, fn in cases:
         t = timeit(fn)
